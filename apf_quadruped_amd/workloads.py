@@ -1,0 +1,173 @@
+"""Synthetic QP workloads of the controller's own shape.
+
+Every generator is a pure function of (seed, qp_id): uniforms come from a
+counter-based splitmix64 hash of (seed, qp_id, draw), so any shard of a batch can
+be regenerated independently on any rank.
+
+Contact-force QP ("C1", 12 vars / 20 ineq / 6 eq) -- the contact-force
+sub-problem of the stance QP built in dogbot_controller/src/client/main.cpp:
+  * foot order BR, BL, FL, FR (Jacobian stacking, main.cpp:825-837)
+  * nominal foot offsets x=0.186571, y=0.289186 (main.cpp:433-443)
+  * P = 50 Jc Jc^T + I           (main.cpp:1476-1480, force block)
+  * c = -50 Jc W                 (main.cpp:1573)
+  * A = Jc^T, b = W              (eigenA/eigenb rows 0-5, main.cpp:1580-1587)
+  * G = blkdiag4(cfr), h = 0     (friction pyramid mu=0.5, main.cpp:1603-1625)
+  * m = 21.261 kg (sum of <mass> in DogBotV4 dogbot.urdf)
+with Jc,i = [I3, -[r_i]x] and W = [m a; m(9.81 + a_z); tau].
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ROBOT_MASS = 21.261
+MU = 0.5
+X_NOM = 0.186571
+Y_NOM = 0.289186
+# BR, BL, FL, FR (main.cpp:438-441)
+FOOT_SIGNS = np.array([[+1.0, -1.0], [-1.0, -1.0], [-1.0, +1.0], [+1.0, +1.0]])
+FOOT_NAMES = ("BR", "BL", "FL", "FR")
+
+# Stance sets of the controller's gait phases.
+STANCE_SETS = {
+    "stance4": (0, 1, 2, 3),           # all feet (main.cpp:1471-1668)
+    "trot_blfr": (1, 3),               # BL + FR stance (main.cpp:1730-1733)
+    "trot_brfl": (0, 2),               # BR + FL stance (main.cpp:2486-2489)
+    "crawl_blflfr": (1, 2, 3),         # BR swing (main.cpp:2919-2922)
+}
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def uniforms(seed: int, qp_ids: np.ndarray, ndraw: int) -> np.ndarray:
+    """[len(qp_ids), ndraw] uniforms in [0, 1) from a counter-based hash."""
+    ids = np.asarray(qp_ids, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        key = _splitmix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ np.uint64(0xD1B54A32D192ED03))
+        ctr = ids[:, None] * np.uint64(ndraw) + np.arange(ndraw, dtype=np.uint64)[None, :]
+        h = _splitmix64(ctr ^ key)
+        h = _splitmix64(h + key)
+    return (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+
+def _skew(r: np.ndarray) -> np.ndarray:
+    """[..., 3] -> [..., 3, 3] cross-product matrices [r]x."""
+    z = np.zeros(r.shape[:-1])
+    rx, ry, rz = r[..., 0], r[..., 1], r[..., 2]
+    return np.stack([np.stack([z, -rz, ry], -1),
+                     np.stack([rz, z, -rx], -1),
+                     np.stack([-ry, rx, z], -1)], -2)
+
+
+def friction_block(mu: float = MU) -> np.ndarray:
+    """cfr (main.cpp:1610-1615): rows (t1-mu n), (t2-mu n), -(t1+mu n), -(t2+mu n), -n."""
+    return np.array([[1.0, 0.0, -mu],
+                     [0.0, 1.0, -mu],
+                     [-1.0, 0.0, -mu],
+                     [0.0, -1.0, -mu],
+                     [0.0, 0.0, -1.0]])
+
+
+def contact_terms(seed: int, qp_ids: np.ndarray):
+    """Per-QP contact Jacobian Jc [B,12,6] and desired wrench W [B,6]."""
+    u = uniforms(seed, qp_ids, 19)
+    h_com = 0.36 + 0.06 * u[:, 0]
+    jit = (0.06 * u[:, 1:13] - 0.03).reshape(-1, 4, 3)
+    r = np.empty((len(u), 4, 3))
+    r[..., 0] = FOOT_SIGNS[None, :, 0] * X_NOM
+    r[..., 1] = FOOT_SIGNS[None, :, 1] * Y_NOM
+    r[..., 2] = -h_com[:, None]
+    r = r + jit
+    acc = np.stack([4.0 * u[:, 13] - 2.0, 4.0 * u[:, 14] - 2.0, 2.0 * u[:, 15] - 1.0], -1)
+    tau = 4.0 * u[:, 16:19] - 2.0
+    W = np.concatenate([ROBOT_MASS * acc[:, :2],
+                        (ROBOT_MASS * (9.81 + acc[:, 2]))[:, None], tau], -1)
+    Jc = np.zeros((len(u), 12, 6))
+    eye = np.eye(3)
+    sk = _skew(r)
+    for i in range(4):
+        Jc[:, 3 * i:3 * i + 3, 0:3] = eye
+        Jc[:, 3 * i:3 * i + 3, 3:6] = -sk[:, i]
+    return Jc, W
+
+
+def contact_force_qp(seed: int, qp_ids, stance=(0, 1, 2, 3), mu: float = MU,
+                     feasible_wrench: bool = False):
+    """Dense contact-force QPs (12 vars, 5*len(stance) ineq, 6 eq).
+
+    feasible_wrench=False: W from random CoM accelerations/torques.
+    feasible_wrench=True: W = sum_i Jc,i^T f_i for random ground-reaction forces
+    f_i strictly inside the friction pyramid of each stance foot, so that QPs with
+    two or three stance feet (6 / 9 force unknowns against 6 wrench equalities)
+    stay feasible (config 3, mixed gait patterns).
+
+    Returns dict with P [B,12,12], c [B,12], A [B,6,12], b [B,6], G [B,m,12],
+    h [B,m]; row-major numpy arrays (dense; the solver converts them to CSC by
+    dropping exact zeros, as QP_SETUP_dense does)."""
+    qp_ids = np.atleast_1d(np.asarray(qp_ids, dtype=np.int64))
+    Jc, W = contact_terms(seed, qp_ids)
+    swing = [i for i in range(4) if i not in stance]
+    for i in swing:                    # swing legs carry no force: zero their rows of Jc
+        Jc[:, 3 * i:3 * i + 3, :] = 0.0
+    B = len(qp_ids)
+    if feasible_wrench:
+        u = uniforms(seed ^ 0x0F0ECE, qp_ids, 12).reshape(B, 4, 3)
+        fz = 40.0 + 80.0 * u[..., 2]
+        f = np.stack([(0.8 * u[..., 0] - 0.4) * mu * 2 * fz * 0.5,
+                      (0.8 * u[..., 1] - 0.4) * mu * 2 * fz * 0.5, fz], -1)
+        W = np.einsum("bfij,bfi->bj", Jc.reshape(B, 4, 3, 6), f)
+    P = 50.0 * np.einsum("bij,bkj->bik", Jc, Jc) + np.eye(12)[None]
+    c = -50.0 * np.einsum("bij,bj->bi", Jc, W)
+    A = np.ascontiguousarray(np.transpose(Jc, (0, 2, 1)))
+    b = W.copy()
+    cfr = friction_block(mu)
+    m = 5 * len(stance)
+    G = np.zeros((B, m, 12))
+    for k, foot in enumerate(stance):
+        G[:, 5 * k:5 * k + 5, 3 * foot:3 * foot + 3] = cfr
+    h = np.zeros((B, m))
+    return dict(n=12, m=m, p=6, P=P, c=c, A=A, b=b, G=G, h=h)
+
+
+def mpc_qp(seed: int, qp_ids, horizon: int = 10, mu: float = MU):
+    """Build-defined MPC contact-force QP.
+
+    u_k in R^12 per stage (n = 12*horizon); P = blkdiag(50 Jk Jk^T + I);
+    20 friction rows per stage (m = 20*horizon); 6 wrench-rate equality rows per
+    stage, Jk^T u_k - J(k-1)^T u_(k-1) = W_k - W_(k-1) (p = 6*horizon)."""
+    qp_ids = np.atleast_1d(np.asarray(qp_ids, dtype=np.int64))
+    B, H = len(qp_ids), horizon
+    n, m, p = 12 * H, 20 * H, 6 * H
+    stage_ids = (qp_ids[:, None] * H + np.arange(H)[None, :]).reshape(-1)
+    Jc, W = contact_terms(seed ^ 0x5EED_0004, stage_ids)
+    Jc = Jc.reshape(B, H, 12, 6)
+    W = W.reshape(B, H, 6)
+    P = np.zeros((B, n, n)); c = np.zeros((B, n))
+    A = np.zeros((B, p, n)); b = np.zeros((B, p))
+    G = np.zeros((B, m, n)); h = np.zeros((B, m))
+    cfr = friction_block(mu)
+    for k in range(H):
+        J = Jc[:, k]
+        sl = slice(12 * k, 12 * k + 12)
+        P[:, sl, sl] = 50.0 * np.einsum("bij,bkj->bik", J, J) + np.eye(12)[None]
+        c[:, sl] = -50.0 * np.einsum("bij,bj->bi", J, W[:, k])
+        A[:, 6 * k:6 * k + 6, sl] = np.transpose(J, (0, 2, 1))
+        b[:, 6 * k:6 * k + 6] = W[:, k]
+        if k > 0:
+            A[:, 6 * k:6 * k + 6, 12 * (k - 1):12 * k] = -np.transpose(Jc[:, k - 1], (0, 2, 1))
+            b[:, 6 * k:6 * k + 6] = W[:, k] - W[:, k - 1]
+        for f in range(4):
+            G[:, 20 * k + 5 * f:20 * k + 5 * f + 5, 12 * k + 3 * f:12 * k + 3 * f + 3] = cfr
+    return dict(n=n, m=m, p=p, P=P, c=c, A=A, b=b, G=G, h=h)
+
+
+def to_colmajor(M: np.ndarray) -> np.ndarray:
+    """[B, r, c] row-major -> [B, r*c] column-major (QP_SETUP_dense, ordering 30)."""
+    return np.ascontiguousarray(np.transpose(M, (0, 2, 1))).reshape(M.shape[0], -1)
