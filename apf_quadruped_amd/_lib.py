@@ -1,0 +1,75 @@
+"""Loader for the native library (libqpswift_hip.so, built in-tree).
+
+The product path has no CPU fallback: if the HIP library is missing or fails to
+load, every entry point raises.  Build it with `python -c "import
+__graft_entry__ as g; g.build()"` (or `make -C apf_quadruped_amd`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from .qpswift_abi import bind_qpswift
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libqpswift_hip.so")
+
+
+class QpbSettings(C.Structure):
+    _fields_ = [("maxit", C.c_long), ("reltol", C.c_double), ("abstol", C.c_double),
+                ("sigma_d", C.c_double)]
+
+
+class QpbPlanInfo(C.Structure):
+    _fields_ = [("n", C.c_long), ("m", C.c_long), ("p", C.c_long), ("N", C.c_long),
+                ("nnzP", C.c_long), ("nnzA", C.c_long), ("nnzG", C.c_long),
+                ("nnzK", C.c_long), ("lnz", C.c_long),
+                ("fac_updates", C.c_long), ("fac_divs", C.c_long),
+                ("ordering", C.c_int), ("exact", C.c_int), ("hash", C.c_uint64)]
+
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib() -> C.CDLL:
+    """The loaded native library; raises NativeLibraryMissing if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} not built -- the HIP path is the only path (no CPU fallback); "
+            "run __graft_entry__.build() first")
+    L = C.CDLL(LIB_PATH)
+    lp, dp, vp = C.POINTER(C.c_long), C.POINTER(C.c_double), C.c_void_p
+    L.qpb_last_error.restype = C.c_char_p
+    L.qpb_version.restype = C.c_char_p
+    L.qpb_default_settings.argtypes = [C.POINTER(QpbSettings)]
+    L.qpb_plan_create.restype = C.c_int
+    L.qpb_plan_create.argtypes = [C.POINTER(vp), C.c_long, C.c_long, C.c_long, C.c_int,
+                                  lp, lp, lp, lp, lp, lp, lp]
+    L.qpb_plan_destroy.argtypes = [vp]
+    L.qpb_plan_destroy.restype = None
+    L.qpb_plan_get_info.argtypes = [vp, C.POINTER(QpbPlanInfo)]
+    L.qpb_plan_get_perm.argtypes = [vp, lp]
+    L.qpb_plan_source.restype = C.c_long
+    L.qpb_plan_source.argtypes = [vp, C.c_char_p, C.c_long]
+    L.qpb_plan_compile.argtypes = [vp]
+    L.qpb_solve.restype = C.c_int
+    L.qpb_solve.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp]
+    L.qpb_argmin.restype = C.c_int
+    L.qpb_argmin.argtypes = [C.c_long, vp, vp, vp, vp]
+    if hasattr(L, "QP_SETUP"):
+        bind_qpswift(L)
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().qpb_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")

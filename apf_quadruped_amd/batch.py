@@ -1,0 +1,246 @@
+"""Batched qpSWIFT solve on MI355X: Python host side of include/qpswift_hip.h.
+
+    plan = Plan.from_dense(n, m, p, P0, A0, G0)        # pattern of one QP
+    vals = plan.pack(P, A, G, c, h, b)                  # [B, ...] dense -> SoA
+    out  = plan.solve(**vals, reltol=1e-6)              # one HIP launch, B QPs
+
+A Plan is the pattern half of QP_SETUP (dogbot_controller/src/qpSWIFT/
+qpSWIFT.c:60-234): KKT assembly, ordering, symbolic factorisation, and the
+generated gfx950 kernel.  `solve` is the value half (kkt_initialize) plus
+QP_SOLVE (qpSWIFT.c:473-644) for every QP of the batch.  Torch is used only to
+own device memory and streams; the arithmetic is the generated HIP kernel.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import QpbPlanInfo, QpbSettings, check
+
+QPB_P_FULL, QPB_P_UPPER, QPB_EXACT = 0x0, 0x1, 0x10
+QP_OPTIMAL, QP_KKTFAIL, QP_MAXIT, QP_FATAL = 0, 1, 2, 3
+
+
+def dense_pattern(M: np.ndarray, upper: bool = False):
+    """CSC (jc, ir) of the non-zeros of dense M (exact zeros dropped, as
+    densetosparse does, Auxilary.c:1154-1206); upper=True keeps rows <= col."""
+    M = np.asarray(M)
+    rows, cols = M.shape
+    nz = M != 0.0
+    if upper:
+        nz = nz & (np.arange(rows)[:, None] <= np.arange(cols)[None, :])
+    jc = np.zeros(cols + 1, np.int64)
+    jc[1:] = np.cumsum(nz.sum(0))
+    ir = np.nonzero(nz.T)[1].astype(np.int64)       # column-major scan, rows ascending
+    return jc, ir
+
+
+TILE = 64
+
+
+def ntiles(B: int) -> int:
+    return (int(B) + TILE - 1) // TILE
+
+
+def to_tiled(V: np.ndarray) -> np.ndarray:
+    """[B, nv] per-QP rows -> flat tiled-SoA array (include/qpswift_hip.h):
+    value j of QP q at [(q//64)*nv*64 + j*64 + q%64]; the last tile is zero-padded."""
+    V = np.asarray(V, dtype=np.float64)
+    if V.ndim == 1:
+        V = V[:, None]
+    B, nv = V.shape
+    T = ntiles(B)
+    buf = np.zeros((T * TILE, nv))
+    buf[:B] = V
+    return np.ascontiguousarray(buf.reshape(T, TILE, nv).transpose(0, 2, 1)).reshape(-1)
+
+
+def from_tiled(flat, B: int, nv: int):
+    """Inverse of to_tiled (numpy or torch): flat tiled array -> [B, nv]."""
+    T = ntiles(B)
+    t = flat.reshape(T, nv, TILE)
+    if hasattr(t, "permute"):
+        return t.permute(0, 2, 1).reshape(T * TILE, nv)[:B]
+    return t.transpose(0, 2, 1).reshape(T * TILE, nv)[:B]
+
+
+def _gather_values(M: np.ndarray, jc, ir) -> np.ndarray:
+    """[B, r, c] dense -> [B, nnz] values in CSC order."""
+    cols = np.repeat(np.arange(len(jc) - 1), np.diff(jc))
+    return np.ascontiguousarray(M[:, ir, cols])
+
+
+@dataclass
+class Patterns:
+    P: tuple
+    A: tuple
+    G: tuple
+
+
+class Plan:
+    """One sparsity pattern (+ KKT ordering) and its generated gfx950 kernel."""
+
+    def __init__(self, n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=None, p_upper=True, exact=False):
+        L = _lib.lib()
+        self.n, self.m, self.p = int(n), int(m), int(p)
+        self.p_upper, self.exact = bool(p_upper), bool(exact)
+        arr = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.int64)
+        self._keep = [arr(a) for a in (Pjc, Pir, Ajc, Air, Gjc, Gir, perm)]
+        Pjc, Pir, Ajc, Air, Gjc, Gir, perm = self._keep
+        self.patterns = Patterns((Pjc, Pir), (Ajc, Air), (Gjc, Gir))
+        lp = lambda a: None if a is None else a.ctypes.data_as(C.POINTER(C.c_long))
+        h = C.c_void_p()
+        flags = (QPB_P_UPPER if p_upper else QPB_P_FULL) | (QPB_EXACT if exact else 0)
+        check(L.qpb_plan_create(C.byref(h), self.n, self.m, self.p, flags, lp(Pjc), lp(Pir),
+                                lp(Ajc) if self.p else None, lp(Air) if self.p else None,
+                                lp(Gjc), lp(Gir), lp(perm)), "qpb_plan_create")
+        self._h = h
+        self.info = QpbPlanInfo()
+        check(L.qpb_plan_get_info(h, C.byref(self.info)), "qpb_plan_get_info")
+        self.N = self.info.N
+        self.perm = np.zeros(self.N, np.int64)
+        check(L.qpb_plan_get_perm(h, self.perm.ctypes.data_as(C.POINTER(C.c_long))), "qpb_plan_get_perm")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _lib.lib().qpb_plan_destroy(h)
+            self._h = None
+
+    @classmethod
+    def from_dense(cls, n, m, p, P, A, G, perm=None, p_upper=True, exact=False):
+        """Plan for the non-zero pattern of one dense QP (P [n,n], A [p,n], G [m,n])."""
+        Pjc, Pir = dense_pattern(P, upper=p_upper)
+        Ajc, Air = dense_pattern(A) if p else (None, None)
+        Gjc, Gir = dense_pattern(G)
+        return cls(n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=perm, p_upper=p_upper, exact=exact)
+
+    # -- inspection ---------------------------------------------------------
+    def source(self) -> str:
+        L = _lib.lib()
+        size = L.qpb_plan_source(self._h, None, 0)
+        buf = C.create_string_buffer(size + 1)
+        L.qpb_plan_source(self._h, buf, size + 1)
+        return buf.value.decode()
+
+    def compile(self) -> None:
+        check(_lib.lib().qpb_plan_compile(self._h), "qpb_plan_compile")
+
+    @property
+    def nnz(self):
+        return self.info.nnzP, self.info.nnzA, self.info.nnzG
+
+    def bytes_per_qp(self) -> int:
+        """Algorithmic HBM bytes per QP: inputs read once + outputs
+        written once + flag/iteration words."""
+        i = self.info
+        ins = i.nnzP + i.nnzA + i.nnzG + i.n + i.m + i.p
+        outs = i.n + i.p + 2 * i.m
+        return 8 * (ins + outs) + 8
+
+    # -- data ---------------------------------------------------------------
+    def pack(self, P, A, G, c, h, b):
+        """Dense numpy batches [B, ...] -> flat tiled-SoA numpy arrays for this
+        plan (values at the plan's pattern positions, CSC order)."""
+        (Pjc, Pir), (Ajc, Air), (Gjc, Gir) = self.patterns.P, self.patterns.A, self.patterns.G
+        out = dict(P=to_tiled(_gather_values(np.asarray(P), Pjc, Pir)),
+                   G=to_tiled(_gather_values(np.asarray(G), Gjc, Gir)),
+                   c=to_tiled(np.asarray(c)), h=to_tiled(np.asarray(h)))
+        if self.p:
+            out["A"] = to_tiled(_gather_values(np.asarray(A), Ajc, Air))
+            out["b"] = to_tiled(np.asarray(b))
+        return out
+
+    def alloc_outputs(self, B, device="cuda"):
+        import torch
+        T = ntiles(B) * TILE
+        f = dict(dtype=torch.float64, device=device)
+        return dict(x=torch.empty(self.n * T, **f), y=torch.empty(max(self.p, 1) * T, **f),
+                    z=torch.empty(self.m * T, **f), s=torch.empty(self.m * T, **f),
+                    flag=torch.empty(B, dtype=torch.int32, device=device),
+                    iters=torch.empty(B, dtype=torch.int32, device=device),
+                    fval=torch.empty(B, **f), stats=torch.empty(6 * T, **f))
+
+    def unpack(self, out, B):
+        """Device tiled outputs -> dict of host numpy arrays [B, n] etc."""
+        r = dict(x=from_tiled(out["x"], B, self.n).cpu().numpy(),
+                 z=from_tiled(out["z"], B, self.m).cpu().numpy(),
+                 s=from_tiled(out["s"], B, self.m).cpu().numpy(),
+                 flag=out["flag"].cpu().numpy(), iters=out["iters"].cpu().numpy(),
+                 fval=out["fval"].cpu().numpy())
+        r["y"] = from_tiled(out["y"], B, self.p).cpu().numpy() if self.p else np.zeros((B, 0))
+        if out.get("stats") is not None:
+            st = from_tiled(out["stats"], B, 6).cpu().numpy()
+            for k, name in enumerate(("n_rx", "n_ry", "n_rz", "n_mu", "alpha_p", "alpha_d")):
+                r[name] = st[:, k]
+        return r
+
+    def solve(self, P, G, c, h, A=None, b=None, B=None, reltol=1e-6, abstol=1e-6, maxit=100,
+              sigma_d=0.0, out=None, stream=None):
+        """Solve B QPs.  Inputs are flat tiled-SoA float64 arrays (torch device
+        tensors, or numpy arrays which are uploaded).  Asynchronous on `stream`
+        (torch stream or None = current stream)."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+        def t(a):
+            if a is None:
+                return None
+            if isinstance(a, np.ndarray):
+                a = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
+            if not (a.dtype == torch.float64 and a.is_cuda and a.is_contiguous()):
+                raise TypeError("inputs must be contiguous float64 device tensors")
+            return a
+
+        P, G, c, h, A, b = map(t, (P, G, c, h, A, b))
+        if B is None:
+            B = c.numel() // self.n
+        B = int(B)
+        T = ntiles(B) * TILE
+        for name, a, nv in (("P", P, self.info.nnzP), ("G", G, self.info.nnzG), ("c", c, self.n),
+                            ("h", h, self.m), ("A", A, self.info.nnzA), ("b", b, self.p)):
+            if a is not None and nv and a.numel() < nv * T:
+                raise ValueError(f"{name}: need {nv * T} values for B={B}, got {a.numel()}")
+        if out is None:
+            out = self.alloc_outputs(B, device=dev)
+        st = QpbSettings(int(maxit), float(reltol), float(abstol), float(sigma_d))
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda a: None if a is None else C.c_void_p(a.data_ptr())
+        check(_lib.lib().qpb_solve(self._h, B, ptr(P), ptr(A) if self.p else None, ptr(G), ptr(c), ptr(h),
+                                   ptr(b) if self.p else None, C.byref(st), ptr(out["x"]),
+                                   ptr(out["y"]) if self.p else None, ptr(out["z"]), ptr(out["s"]),
+                                   ptr(out["flag"]), ptr(out["iters"]), ptr(out["fval"]),
+                                   ptr(out.get("stats")), C.c_void_p(stream.cuda_stream)), "qpb_solve")
+        return out
+
+
+def argmin(fval, flag, out=None, stream=None):
+    """Device-side (fval, index) of the lowest-fval optimal QP (qpb_argmin)."""
+    import torch
+    if out is None:
+        out = torch.empty(2, dtype=torch.float64, device=fval.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(fval.device)
+    check(_lib.lib().qpb_argmin(fval.numel(), C.c_void_p(fval.data_ptr()), C.c_void_p(flag.data_ptr()),
+                                C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream)), "qpb_argmin")
+    return out
+
+
+def bucket_by_pattern(P, A, G):
+    """Group dense QPs by their exact-zero pattern (config 3, mixed sparsity).
+    Returns {key: index array}, key = (P mask, A mask, G mask) bytes."""
+    B = P.shape[0]
+    keys = {}
+    mP = (np.asarray(P) != 0).reshape(B, -1)
+    mA = (np.asarray(A) != 0).reshape(B, -1)
+    mG = (np.asarray(G) != 0).reshape(B, -1)
+    allm = np.concatenate([mP, mA, mG], 1)
+    packed = np.packbits(allm, axis=1)
+    uniq, inv = np.unique(packed, axis=0, return_inverse=True)
+    for u in range(len(uniq)):
+        keys[u] = np.nonzero(inv.reshape(-1) == u)[0]
+    return keys

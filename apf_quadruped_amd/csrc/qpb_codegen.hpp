@@ -1,0 +1,37 @@
+// qpb_codegen.hpp -- plan -> one straight-line HIP kernel (gfx950).
+#pragma once
+
+#include <string>
+
+#include "qpb_plan.hpp"
+
+namespace qpb {
+
+struct GenOptions {
+    // exact = true: every floating-point operation is issued in the reference's
+    // order with IEEE division and no FMA contraction, so results are
+    // bit-identical to qpSWIFT (and to the oracle).  exact = false: FMA
+    // contraction, reciprocal-multiply for the pivots and 1/z, division-free step
+    // length search (results within rounding of the reference).
+    bool exact = false;
+    int wg = 256;             // threads per workgroup (one QP per lane)
+    int waves_per_eu = 1;     // __launch_bounds__ minimum waves per SIMD
+};
+
+// Kernel argument block; identical layout in the generated device code.
+struct KernelArgs {
+    const double *P, *A, *G, *c, *h, *b;   // tiled SoA (see qpswift_hip.h)
+    double *x, *y, *z, *s;                  // tiled SoA outputs
+    int *flag, *iters;                      // [B]
+    double *fval;                           // [B]
+    double *stats;                          // optional, tiled with 6 values per QP
+    long B;
+    double tol;                             // reltol / sqrt(3) (qpSWIFT.c:521)
+    double abstol, sigma_d;
+    long maxit;
+};
+
+std::string kernel_name(const Plan &pl, const GenOptions &opt);
+std::string generate_kernel(const Plan &pl, const GenOptions &opt);
+
+}  // namespace qpb

@@ -1,0 +1,98 @@
+// qpb_plan.hpp -- host-side plan for one QP sparsity pattern.
+//
+// A plan is everything about a qpSWIFT solve that depends only on the sparsity
+// pattern (and the KKT ordering), never on values:
+//   * the full symmetric KKT CSC [P A' G'; A 0 0; G 0 -I] exactly as the
+//     reference assembles it (dogbot_controller/src/qpSWIFT/Auxilary.c:71-181),
+//     every slot tagged with the input value it comes from;
+//   * the KKT permutation (caller's, or our own minimum-degree ordering -- the
+//     reference runs SuiteSparse AMD every tick, qpSWIFT.c:416-440);
+//   * the elimination tree and column counts (ldl.c:187-240);
+//   * the exact operation schedule of the up-looking LDL' numeric factorisation
+//     (ldl.c:253-326), obtained by executing its index logic symbolically.
+// The code generator (qpb_codegen.cpp) turns a plan into one straight-line HIP
+// kernel in which every index is a compile-time constant.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace qpb {
+
+// Where one KKT CSC slot's value comes from.
+enum class Src : uint8_t { P, A, G, NegOne, ZDiag };
+
+struct Slot {
+    int32_t row;
+    Src kind;
+    int32_t idx;   // index into the P / A / G value array, or the z index for ZDiag
+};
+
+struct Pattern {
+    long rows = 0, cols = 0;
+    std::vector<long> jc, ir;
+    long nnz() const { return jc.empty() ? 0 : jc[cols]; }
+};
+
+// One step of the LDL' numeric schedule (ldl.c:276-322).
+enum class FacOp : uint8_t {
+    RowBegin,   // a = k
+    Scatter,    // Y[a] += K[slot b]                 (ldl.c:290)
+    Update,     // Y[a] -= L[b] * Y[c]               (ldl.c:311)
+    NewL,       // L[b] = Y[a] / D[a]; D[k] -= L[b]*Y[a] (ldl.c:313-316), a = i
+    RowEnd,     // D[k] = Y[k] first, regularise     (ldl.c:300, 319-320)
+};
+
+struct FacStep {
+    FacOp op;
+    int32_t a, b, c;
+};
+
+enum PModes : int { P_FULL = 0, P_UPPER = 1 };
+
+struct Plan {
+    long n = 0, m = 0, p = 0, N = 0;
+    int pmode = P_FULL;
+    Pattern Pin, A, G;                       // caller patterns (P full or upper)
+    Pattern Pf;  std::vector<long> Pf_src;   // full P pattern -> index into P values
+    Pattern At;  std::vector<long> At_src;   // A' -> index into A values
+    Pattern Gt;  std::vector<long> Gt_src;   // G' -> index into G values
+    Pattern K;                               // KKT CSC (reference layout)
+    std::vector<Slot> K_init;                // values as assembled (setup solve)
+    std::vector<Slot> K_loop;                // after updatekktmatrix (IPM loop)
+    std::vector<long> perm, pinv, parent, Lp, Li;
+    long lnz = 0;
+    int ordering_kind = 0;                   // 0 caller-given, 1 own min-degree, 2 identity
+    std::vector<FacStep> fac;                // numeric schedule
+    long fac_updates = 0, fac_divs = 0;      // op counts (flop accounting)
+    uint64_t hash = 0;
+    std::string key;                         // stable text key (hash input)
+};
+
+// Error codes: the same values as the QPB_E* macros of include/qpswift_hip.h.
+enum Err : int {
+    E_OK = 0,
+    E_INVAL = -1,
+    E_NOMEM = -2,
+    E_HIP = -3,
+    E_COMPILE = -4,
+    E_SHAPE = -5,
+};
+
+// Build a plan.  P pattern is either full (both triangles, as QP_SETUP takes it)
+// or upper-triangular (pmode = P_UPPER, symmetric semantics).  perm may be null:
+// then our own minimum-degree ordering is used.  Returns QPB_OK or an error.
+int build_plan(Plan &pl, long n, long m, long p, int pmode,
+               const long *Pjc, const long *Pir,
+               const long *Ajc, const long *Air,
+               const long *Gjc, const long *Gir,
+               const long *perm, std::string *err);
+
+// Minimum-degree ordering of a symmetric pattern (own implementation; ties go
+// to the lowest index).  Exposed for tests.
+std::vector<long> min_degree_order(const Pattern &sym);
+
+uint64_t fnv1a(const std::string &s);
+
+}  // namespace qpb

@@ -1,0 +1,278 @@
+// qpb_runtime.hip -- C ABI of the batched solver: plans, the code-object cache
+// (hiprtc JIT for gfx950 + on-disk cache), launches, and the argmin reduction.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/qpswift_hip.h"
+#include "qpb_codegen.hpp"
+#include "qpb_plan.hpp"
+#include "qpb_runtime.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+std::mutex g_mu;
+// kernel name -> code object bytes (compiled or read from disk)
+std::map<std::string, std::shared_ptr<std::vector<char>>> g_code;
+// (device, kernel name) -> loaded function
+std::map<std::pair<int, std::string>, std::pair<hipModule_t, hipFunction_t>> g_funcs;
+
+std::string cache_dir() {
+    const char *env = getenv("QPB_KCACHE");
+    if (env && *env) return env;
+    Dl_info info;
+    if (dladdr((void *)&cache_dir, &info) && info.dli_fname) {
+        std::string p(info.dli_fname);
+        size_t s = p.rfind('/');
+        if (s != std::string::npos) return p.substr(0, s) + "/kcache";
+    }
+    return "kcache";
+}
+
+bool read_file(const std::string &path, std::vector<char> &out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return !out.empty();
+}
+
+void write_file(const std::string &path, const std::vector<char> &data) {
+    std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) return;
+        f.write(data.data(), (std::streamsize)data.size());
+    }
+    rename(tmp.c_str(), path.c_str());
+}
+
+// Lowest fval among optimal QPs; one block, ties -> lowest index.
+__global__ void __launch_bounds__(1024) qpb_argmin_kernel(long B, const double *__restrict__ fval,
+                                                          const int *__restrict__ flag, double *__restrict__ out) {
+    __shared__ double sv[1024 / 64];
+    __shared__ long si[1024 / 64];
+    double bv = INFINITY;
+    long bi = -1;
+    for (long q = threadIdx.x; q < B; q += blockDim.x) {
+        double v = fval[q];
+        if (flag[q] == 0 && (v < bv || (v == bv && (bi < 0 || q < bi)))) { bv = v; bi = q; }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        double ov = __shfl_xor(bv, off, 64);
+        long oi = __shfl_xor(bi, off, 64);
+        bool take = (oi >= 0) && (bi < 0 || ov < bv || (ov == bv && oi < bi));
+        bv = take ? ov : bv;
+        bi = take ? oi : bi;
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sv[w] = bv; si[w] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x >> 6); k++) {
+            bool take = (si[k] >= 0) && (bi < 0 || sv[k] < bv || (sv[k] == bv && si[k] < bi));
+            bv = take ? sv[k] : bv;
+            bi = take ? si[k] : bi;
+        }
+        out[0] = bv;
+        out[1] = (double)bi;
+    }
+}
+
+}  // namespace
+
+namespace qpb {
+
+int compile_plan(qpb_plan *plan) {
+    if (plan->code) return QPB_OK;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_code.find(plan->kname);
+    if (it != g_code.end()) { plan->code = it->second; return QPB_OK; }
+    const std::string dir = cache_dir();
+    const std::string path = dir + "/" + plan->kname + ".hsaco";
+    auto code = std::make_shared<std::vector<char>>();
+    if (!getenv("QPB_NO_DISK_CACHE") && read_file(path, *code)) {
+        g_code[plan->kname] = code;
+        plan->code = code;
+        return QPB_OK;
+    }
+    std::string src = generate_kernel(plan->pl, plan->gen);
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), (plan->kname + ".hip").c_str(), 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+        return fail(QPB_ECOMPILE, "hiprtcCreateProgram failed");
+    std::vector<const char *> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    if (plan->gen.exact) opts.push_back("-ffp-contract=off");
+    hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
+    if (rc != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        hiprtcGetProgramLogSize(prog, &ls);
+        std::string log(ls, '\0');
+        if (ls) hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        return fail(QPB_ECOMPILE, "hiprtc: " + log.substr(0, 4000));
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    code->resize(cs);
+    hiprtcGetCode(prog, code->data());
+    hiprtcDestroyProgram(&prog);
+    mkdir(dir.c_str(), 0755);
+    write_file(path, *code);
+    g_code[plan->kname] = code;
+    plan->code = code;
+    return QPB_OK;
+}
+
+int get_function(qpb_plan *plan, hipFunction_t *fn) {
+    int rc = compile_plan(plan);
+    if (rc) return rc;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(QPB_EHIP, "hipGetDevice failed (no GPU?)");
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto key = std::make_pair(dev, plan->kname);
+    auto it = g_funcs.find(key);
+    if (it != g_funcs.end()) { *fn = it->second.second; return QPB_OK; }
+    hipModule_t mod;
+    hipError_t e = hipModuleLoadData(&mod, plan->code->data());
+    if (e != hipSuccess) return fail(QPB_EHIP, std::string("hipModuleLoadData: ") + hipGetErrorString(e));
+    hipFunction_t f;
+    e = hipModuleGetFunction(&f, mod, plan->kname.c_str());
+    if (e != hipSuccess) return fail(QPB_EHIP, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+    g_funcs[key] = {mod, f};
+    *fn = f;
+    return QPB_OK;
+}
+
+int set_error(int code, const char *msg) { return fail(code, msg); }
+
+}  // namespace qpb
+
+extern "C" {
+
+const char *qpb_last_error(void) { return g_err.c_str(); }
+const char *qpb_version(void) { return "qpswift-hip 0.1 (gfx950)"; }
+
+void qpb_default_settings(qpb_settings *st) {
+    st->maxit = 100;
+    st->reltol = 1e-6;
+    st->abstol = 1e-6;
+    st->sigma_d = 0.0;
+}
+
+int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
+                    const long *Pjc, const long *Pir, const long *Ajc, const long *Air,
+                    const long *Gjc, const long *Gir, const long *perm) {
+    if (!out) return fail(QPB_EINVAL, "plan out-pointer is NULL");
+    *out = nullptr;
+    std::unique_ptr<qpb_plan> plan(new (std::nothrow) qpb_plan());
+    if (!plan) return fail(QPB_ENOMEM, "out of host memory");
+    std::string err;
+    int rc = qpb::build_plan(plan->pl, n, m, p, (flags & QPB_P_UPPER) ? qpb::P_UPPER : qpb::P_FULL,
+                             Pjc, Pir, Ajc, Air, Gjc, Gir, perm, &err);
+    if (rc) return fail(rc, err);
+    plan->gen.exact = (flags & QPB_EXACT) != 0;
+    plan->gen.wg = 256;
+    plan->gen.waves_per_eu = 1;
+    plan->kname = qpb::kernel_name(plan->pl, plan->gen);
+    *out = plan.release();
+    return QPB_OK;
+}
+
+void qpb_plan_destroy(qpb_plan *plan) { delete plan; }
+
+int qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info) {
+    if (!plan || !info) return fail(QPB_EINVAL, "NULL argument");
+    const qpb::Plan &pl = plan->pl;
+    info->n = pl.n; info->m = pl.m; info->p = pl.p; info->N = pl.N;
+    info->nnzP = pl.Pin.nnz(); info->nnzA = pl.p ? pl.A.nnz() : 0; info->nnzG = pl.G.nnz();
+    info->nnzK = pl.K.nnz(); info->lnz = pl.lnz;
+    info->fac_updates = pl.fac_updates; info->fac_divs = pl.fac_divs;
+    info->ordering = pl.ordering_kind; info->exact = plan->gen.exact ? 1 : 0;
+    info->hash = pl.hash;
+    return QPB_OK;
+}
+
+int qpb_plan_get_perm(const qpb_plan *plan, long *perm) {
+    if (!plan || !perm) return fail(QPB_EINVAL, "NULL argument");
+    std::memcpy(perm, plan->pl.perm.data(), sizeof(long) * plan->pl.N);
+    return QPB_OK;
+}
+
+long qpb_plan_source(const qpb_plan *plan, char *buf, long cap) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    std::string s = qpb::generate_kernel(plan->pl, plan->gen);
+    if (buf && cap > 0) {
+        long k = std::min<long>(cap - 1, (long)s.size());
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (long)s.size();
+}
+
+int qpb_plan_compile(qpb_plan *plan) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    return qpb::compile_plan(plan);
+}
+
+int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
+              const double *c, const double *h, const double *b, const qpb_settings *st,
+              double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
+              double *stats, void *stream) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    if (B < 0) return fail(QPB_EINVAL, "need B >= 0");
+    if (B == 0) return QPB_OK;
+    const qpb::Plan &pl = plan->pl;
+    if (!P || !G || !c || !h || !x || !z || !s || !flag || !iters || !fval)
+        return fail(QPB_EINVAL, "NULL data pointer");
+    if (pl.p > 0 && (!A || !b || !y)) return fail(QPB_EINVAL, "p > 0 needs A, b and y");
+    hipFunction_t fn;
+    int rc = qpb::get_function(plan, &fn);
+    if (rc) return rc;
+    qpb_settings def;
+    qpb_default_settings(&def);
+    if (!st) st = &def;
+    qpb::KernelArgs a;
+    a.P = P; a.A = A; a.G = G; a.c = c; a.h = h; a.b = b;
+    a.x = x; a.y = y; a.z = z; a.s = s;
+    a.flag = flag; a.iters = iters; a.fval = fval; a.stats = stats;
+    a.B = B;
+    a.tol = st->reltol / std::sqrt(3.0);
+    a.abstol = st->abstol;
+    a.sigma_d = st->sigma_d;
+    a.maxit = st->maxit;
+    void *params[] = {&a};
+    const unsigned wg = (unsigned)plan->gen.wg;
+    const unsigned grid = (unsigned)((B + wg - 1) / wg);
+    hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, wg, 1, 1, 0, (hipStream_t)stream, params, nullptr);
+    if (e != hipSuccess) return fail(QPB_EHIP, std::string("launch: ") + hipGetErrorString(e));
+    return QPB_OK;
+}
+
+int qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *stream) {
+    if (B < 0 || !out2 || (B > 0 && (!fval || !flag))) return fail(QPB_EINVAL, "bad argmin arguments");
+    hipLaunchKernelGGL(qpb_argmin_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, fval, flag, out2);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(QPB_EHIP, std::string("argmin: ") + hipGetErrorString(e));
+    return QPB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,241 @@
+"""Benchmark: batched 12-var contact-force QP solves/s on MI355X (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+
+One step = one batched IPM solve (kkt_initialize + QP_SOLVE) of
+this rank's resident batch of synthetic contact-force QPs (12 vars / 20 ineq /
+6 eq) followed by the device-side argmin; for N > 1 the per-rank
+winners are exchanged with one RCCL all_gather (config 5's argmin gather).
+Shards are independent (weak scaling): rank r owns QP ids [r*B, (r+1)*B).
+
+The default per-GPU batch (2^20 QPs, ~2 GB of inputs) keeps the working set far
+above the 256 MB Infinity Cache, as SURVEY §8d asks for HBM-roofline numbers; the
+BASELINE configs[1] shape (1 024 QPs per launch) is reported beside it as
+`batch1024` (latency-bound).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1 << 20, help="QPs per GPU per step")
+    ap.add_argument("--tol", type=float, default=1e-6)
+    ap.add_argument("--exact", action="store_true", help="bench the bit-faithful kernel")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-sample", type=int, default=65536)
+    ap.add_argument("--cpu-passes", type=int, default=4)
+    return ap.parse_args()
+
+
+def make_shard(plan, seed, q0, B, chunk=65536):
+    """Synthetic C1 QPs [q0, q0+B) packed in the plan's tiled layout (host)."""
+    from apf_quadruped_amd import workloads as W
+    parts = {k: [] for k in ("P", "A", "G", "c", "h", "b")}
+    for s in range(0, B, chunk):
+        ids = np.arange(q0 + s, q0 + min(B, s + chunk))
+        d = W.contact_force_qp(seed, ids)
+        v = plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"])
+        for k in parts:
+            parts[k].append(v[k])
+    return {k: np.concatenate(v) for k, v in parts.items()}
+
+
+def flops_per_qp(info, iters):
+    """Algorithmic FP64 flops of one solve (FMA = 2), SURVEY §8d accounting."""
+    n, m, p, N, lnz = info.n, info.m, info.p, info.N, info.lnz
+    fac = 2 * info.fac_updates + 3 * info.fac_divs
+    solve = 4 * lnz + N
+    resid = 2 * (2 * info.nnzP + 2 * info.nnzG + 2 * info.nnzA) + 2 * (n + m + p)
+    vec = 30 * m + 10 * (n + p)
+    per_it = fac + 2 * solve + resid + vec
+    return (fac + solve + 2 * info.nnzG) + iters * per_it + resid
+
+
+def cpu_baseline(seed, sample, passes, tol):
+    """Reference qpSWIFT (oracle/_ref) on the host cores; port (oracle) if absent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from apf_quadruped_amd import workloads as W
+    threads = max(1, min(16, os.cpu_count() or 1))
+    d = W.contact_force_qp(seed, np.arange(sample))
+    P, A, G = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    c, h, b = (np.ascontiguousarray(d[k]) for k in ("c", "h", "b"))
+    x = np.zeros((sample, 12)); flags = np.zeros(sample, np.int64); iters = np.zeros(sample, np.int64)
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
+    lp = lambda a: a.ctypes.data_as(C.POINTER(C.c_long))
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_batch.so")
+    if os.path.exists(ref_so):
+        L = C.CDLL(ref_so)
+        L.ref_solve_dense_batch.argtypes = [C.c_long] * 4 + [C.POINTER(C.c_double)] * 6 + \
+            [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
+        run = lambda: L.ref_solve_dense_batch(sample, 12, 20, 6, dp(P), dp(A), dp(G), dp(c), dp(h), dp(b),
+                                              tol, dp(x), lp(flags), lp(iters), threads)
+        kind = "reference"
+    else:
+        from oracle_py import Oracle
+        o = Oracle()
+        run = lambda: o.lib.oracle_solve_dense_batch(sample, 12, 20, 6, dp(P), dp(A), dp(G), dp(c), dp(h),
+                                                     dp(b), None, tol, tol, 100, dp(x), lp(flags), lp(iters),
+                                                     threads)
+        kind = "port"
+    run()                                   # warm caches / page in
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        run()
+    dt = time.perf_counter() - t0
+    return dict(value=sample * passes / dt, unit="QP solves/s", cores=threads, kind=kind,
+                sample=f"{sample} C1 QPs x {passes} passes, setup+solve per QP (QP_SETUP_dense + QP_SOLVE "
+                       f"+ QP_CLEANUP_dense, AMD ordering), tol {tol:g}, {threads} threads, {dt:.2f} s wall",
+                mean_iters=float(iters.mean()), optimal_frac=float((flags == 0).mean()))
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from apf_quadruped_amd.batch import Plan, argmin, ntiles
+    from apf_quadruped_amd import plans
+
+    seed = plans.SEED + 1
+    d0 = plans.standard_qp("c1")
+    plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=args.exact)
+    plan.compile()
+    B = args.batch
+    host = make_shard(plan, seed, rank * B, B)
+    vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
+    del host
+    out = plan.alloc_outputs(B, device=dev)
+    best = torch.empty(2, dtype=torch.float64, device=dev)
+    gathered = torch.empty(2 * world, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        plan.solve(**vals, B=B, reltol=args.tol, abstol=args.tol, out=out, stream=stream)
+        argmin(out["fval"], out["flag"], out=best, stream=stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, best)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        plan.solve(**vals, B=B, reltol=args.tol, abstol=args.tol, out=out, stream=stream)
+        ev[i][1].record(stream)
+        argmin(out["fval"], out["flag"], out=best, stream=stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, best)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    flags = out["flag"].cpu().numpy()
+    iters = out["iters"].cpu().numpy()
+    mean_it = float(iters.mean())
+    if world > 1:
+        g = gathered.cpu().numpy().reshape(world, 2)
+    ms_step = elapsed * 1e3 / args.steps
+    value = world * B * args.steps / elapsed
+    bpq = plan.bytes_per_qp()
+    achieved = bpq * B / (kern_ms * 1e-3) / 1e9
+    fpq = flops_per_qp(plan.info, mean_it)
+    fp64_tf = fpq * B / (kern_ms * 1e-3) / 1e12
+
+    # configs[1]: one batch of 1 024 QPs per launch (latency-bound)
+    small = None
+    if rank == 0:
+        Bs = 1024
+        sv = {k: v[: ntiles(Bs) * 64 * (v.numel() // (ntiles(B) * 64))] for k, v in vals.items()}
+        so = plan.alloc_outputs(Bs, device=dev)
+        for _ in range(5):
+            plan.solve(**sv, B=Bs, reltol=args.tol, abstol=args.tol, out=so, stream=stream)
+        torch.cuda.synchronize()
+        n_small = 200
+        t1 = time.perf_counter()
+        for _ in range(n_small):
+            plan.solve(**sv, B=Bs, reltol=args.tol, abstol=args.tol, out=so, stream=stream)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t1
+        small = dict(batch=Bs, launches=n_small, us_per_launch=dt * 1e6 / n_small, qps=Bs * n_small / dt)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(seed, args.cpu_sample, args.cpu_passes, args.tol)
+
+    if rank == 0:
+        line = {
+            "metric": "QP solves/sec (batched 12-var contact-force QP)",
+            "value": value,
+            "unit": "QP solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (counter-based RNG, SURVEY §8d contact-force QPs, resident in HBM)",
+            "config": {"workload": "c1_contact_force_12v_20ineq_6eq", "qps_per_gpu": B,
+                       "global_batch": B * world, "tol": args.tol,
+                       "kernel": "exact" if args.exact else "fast",
+                       "ordering": "own min-degree", "kkt_N": plan.info.N, "nnz_L": plan.info.lnz,
+                       "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "bytes_per_qp": bpq, "kernel_ms": kern_ms},
+            "fp64": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
+                     "frac": fp64_tf / FP64_PEAK_TFLOPS, "flops_per_qp": fpq},
+            "mean_iters": mean_it,
+            "optimal_frac": float((flags == 0).mean()),
+            "batch1024": small,
+            "cpu_baseline": cpu,
+        }
+        if world > 1:
+            k = int(np.argmin(np.where(g[:, 1] >= 0, g[:, 0], np.inf)))
+            line["argmin"] = {"fval": float(g[k, 0]), "rank": k, "index": int(g[k, 1]) + k * B}
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

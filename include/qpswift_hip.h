@@ -1,0 +1,115 @@
+/*
+ * qpswift_hip.h -- batched qpSWIFT interior-point solver for AMD MI355X (gfx950).
+ *
+ * C ABI only: plain pointers and sizes, no C++ or torch types.  This header is
+ * the NEW batched entry point behind the reference's per-tick solve; the
+ * source/ABI-compatible single-QP drop-in (QP_SETUP / QP_SETUP_dense / QP_SOLVE /
+ * QP_CLEANUP / QP_CLEANUP_dense) is declared in qpSWIFT.h next to this file.
+ *
+ * Reference interface each entry point replaces (paths under
+ * /root/reference/dogbot_controller/):
+ *   qpb_plan_create   pattern half of QP_SETUP (src/qpSWIFT/qpSWIFT.c:60-234):
+ *                     transposes, KKT assembly (Auxilary.c:71-181), AMD ordering
+ *                     (qpSWIFT.c:416-440) and LDL_symbolic (ldl.c:187-240), done
+ *                     once per sparsity pattern instead of once per tick.
+ *   qpb_solve         value half of QP_SETUP (kkt_initialize, Auxilary.c:992-1089)
+ *                     + QP_SOLVE (qpSWIFT.c:473-644) for B independent QPs that
+ *                     share the plan's pattern, in one HIP launch.
+ *   qpb_plan_destroy  QP_CLEANUP (qpSWIFT.c:661-737) for the pattern state.
+ *
+ * Data layout (device memory, "tiled SoA", tile = 64 QPs = one wavefront): an
+ * array holding nv values per QP stores value j of QP q at
+ *       X[(q / 64) * nv * 64 + j * 64 + q % 64]
+ * i.e. the batch is cut into tiles of 64 QPs and each tile is an [nv][64] block;
+ * buffers hold ceil(B/64) tiles.  (For nv = 1 this is a plain [B] array.)
+ *   P  nv = nnz(P): values of the P pattern given at plan creation (full, or
+ *      upper triangle with QPB_P_UPPER), in CSC order
+ *   A  nv = nnz(A) (may be NULL when p == 0),   G  nv = nnz(G)
+ *   c nv = n, h nv = m, b nv = p
+ *   x nv = n, y nv = p, z nv = m, s nv = m           (outputs)
+ *   flag [B] (QP_OPTIMAL 0 / QP_MAXIT 2), iters [B], fval [B]
+ *   stats  optional, nv = 6: n_rx, n_ry, n_rz, n_mu, alpha_p, alpha_d
+ * All pointers passed to qpb_solve are DEVICE pointers.  The call is asynchronous
+ * on `stream` (a hipStream_t, NULL = default stream) and graph-capturable.
+ *
+ * Errors: every function returns 0 on success or a negative QPB_E* code and
+ * records a message readable with qpb_last_error(); nothing is printed.
+ */
+#ifndef QPSWIFT_HIP_H
+#define QPSWIFT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct qpb_plan qpb_plan;
+
+/* qpb_plan_create flags */
+#define QPB_P_FULL   0x0   /* P pattern holds both triangles (QP_SETUP semantics) */
+#define QPB_P_UPPER  0x1   /* P pattern is the upper triangle (symmetric P)        */
+#define QPB_EXACT    0x10  /* bit-faithful arithmetic: IEEE division, no FMA       */
+
+/* error codes */
+#define QPB_OK        0
+#define QPB_EINVAL   -1
+#define QPB_ENOMEM   -2
+#define QPB_EHIP     -3
+#define QPB_ECOMPILE -4
+#define QPB_ESHAPE   -5
+
+typedef struct qpb_settings {
+    long   maxit;     /* default 100  (GlobalOptions.h:46) */
+    double reltol;    /* default 1e-6 (GlobalOptions.h:47); controller uses 1e-2 */
+    double abstol;    /* default 1e-6 (GlobalOptions.h:48) */
+    double sigma_d;   /* 0 for QP_SETUP_dense (qpSWIFT.c:334) */
+} qpb_settings;
+
+typedef struct qpb_plan_info {
+    long n, m, p, N;             /* N = n + m + p (KKT order) */
+    long nnzP, nnzA, nnzG;       /* value counts per QP */
+    long nnzK, lnz;              /* nnz of the KKT and of its L factor */
+    long fac_updates, fac_divs;  /* LDL numeric op counts per factorisation */
+    int  ordering;               /* 0 caller permutation, 1 own minimum degree */
+    int  exact;
+    uint64_t hash;               /* pattern + permutation hash */
+} qpb_plan_info;
+
+void qpb_default_settings(qpb_settings *st);
+
+int  qpb_plan_create(qpb_plan **plan, long n, long m, long p, int flags,
+                     const long *Pjc, const long *Pir,
+                     const long *Ajc, const long *Air,
+                     const long *Gjc, const long *Gir,
+                     const long *perm /* length n+m+p, or NULL = own ordering */);
+void qpb_plan_destroy(qpb_plan *plan);
+int  qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info);
+int  qpb_plan_get_perm(const qpb_plan *plan, long *perm /* [N] */);
+/* Generated HIP source of the plan's kernel; returns its length (copies at most
+ * cap-1 bytes plus a NUL when buf is non-NULL). */
+long qpb_plan_source(const qpb_plan *plan, char *buf, long cap);
+/* Compile the plan's kernel for gfx950 (hiprtc) or fetch it from the code-object
+ * cache; needs no GPU.  qpb_solve calls this implicitly. */
+int  qpb_plan_compile(qpb_plan *plan);
+
+int  qpb_solve(qpb_plan *plan, long B,
+               const double *P, const double *A, const double *G,
+               const double *c, const double *h, const double *b,
+               const qpb_settings *st,
+               double *x, double *y, double *z, double *s,
+               int *flag, int *iters, double *fval, double *stats,
+               void *stream);
+
+/* Lowest-fval optimal QP of a batch (device-side reduction): writes
+ * {fval, index} of the minimum over q with flag[q] == 0 (ties -> lowest index;
+ * none -> {+inf, -1}) to out2 (device, 2 doubles; the index as a double). */
+int  qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *stream);
+
+const char *qpb_last_error(void);
+const char *qpb_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
