@@ -17,6 +17,7 @@
 //   LDL numeric / solves  ldl.c:253-326, 495-597
 #include "qpb_codegen.hpp"
 
+#include <map>
 #include <sstream>
 #include <vector>
 
@@ -36,28 +37,124 @@ struct Gen {
     // phase's working set).
     int phase = 0;
     std::vector<std::vector<std::string>> scopes{{}};
+    // Fast mode: "leaf" columns of L (no entries in their row, e.g. the z and y
+    // pivots eliminated before any x) satisfy L(k,j) = K(j,k) / D(j) exactly; their
+    // L entries are never stored -- every use is rewritten in terms of the KKT input
+    // value and 1/D(j).  leaf_slot[e] = KKT slot holding K(j,k) for L entry e.
+    std::vector<char> leaf;
+    std::vector<long> leaf_slot;
+    // Fast mode: A and G values live in LDS (each lane owns one private column, so
+    // no barriers are needed); lds_base[arr] = first LDS row of that array.
+    bool use_lds = false;
+    long lds_rows = 0, lds_A = -1, lds_G = -1, lds_P = -1;
 
-    Gen(const Plan &p, const GenOptions &g) : pl(p), opt(g) {}
+    Gen(const Plan &p, const GenOptions &g) : pl(p), opt(g) {
+        const long N = pl.N;
+        leaf.assign(N, !opt.exact);
+        if (!opt.exact) {
+            for (long e = 0; e < pl.lnz; e++) leaf[pl.Li[e]] = 0;     // row Li[e] has an entry
+            leaf_slot.assign(pl.lnz, -1);
+            std::vector<long> scat(N, -1);
+            long k = 0;
+            for (const FacStep &st : pl.fac) {
+                if (st.op == FacOp::RowBegin) { k = st.a; std::fill(scat.begin(), scat.end(), -1); }
+                else if (st.op == FacOp::Scatter) scat[st.a] = st.b;
+                else if (st.op == FacOp::NewL && leaf[st.a]) leaf_slot[st.b] = scat[st.a];
+            }
+            for (long e = 0; e < pl.lnz; e++) {
+                long j = -1;
+                for (long c = 0; c < N; c++) if (e >= pl.Lp[c] && e < pl.Lp[c + 1]) { j = c; break; }
+                if (leaf[j] && leaf_slot[e] < 0) leaf[j] = 0;          // not a pure scatter: keep L
+            }
+            const long nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz(), nP = pl.Pin.nnz();
+            if (opt.lds_mode >= 1) {
+                lds_A = 0; lds_G = nA; lds_rows = nA + nG;
+                if (opt.lds_mode == 2) { lds_P = lds_rows; lds_rows += nP; }
+                if (opt.lds_mode == 3) {      // park the loop vectors too
+                    const long n = pl.n, p = pl.p, m = pl.m;
+                    park["x"] = lds_rows; lds_rows += n;
+                    if (p) { park["y"] = lds_rows; lds_rows += p; }
+                    park["rx"] = lds_rows; lds_rows += n;
+                    if (p) { park["ry"] = lds_rows; lds_rows += p; }
+                    park["rz"] = lds_rows; lds_rows += m;
+                    if ((lds_rows + m) * opt.wg * 8 <= 160 * 1024) { park["s"] = lds_rows; lds_rows += m; }
+                }
+                use_lds = lds_rows > 0 && lds_rows * opt.wg * 8 <= 160 * 1024;
+                if (!use_lds) { lds_A = lds_G = lds_P = -1; park.clear(); }
+            }
+        }
+    }
+    long col_of(long e) const {
+        long lo = 0, hi = pl.N;
+        while (hi - lo > 1) { long mid = (lo + hi) / 2; if (pl.Lp[mid] <= e) lo = mid; else hi = mid; }
+        return lo;
+    }
 
     void ln(const std::string &s) {
         for (int i = 0; i < indent; i++) o << "  ";
         o << s << '\n';
     }
-    void open(const std::string &s) { ln(s); indent++; scopes.push_back({}); }
-    void close(const std::string &s = "}") { scopes.pop_back(); indent--; ln(s); }
-    void begin_phase() {
-        phase++;
-        ln("int lo" + S(phase) + " = lane; asm volatile(\"\" : \"+v\"(lo" + S(phase) + "));");
+    // Two independent "phases": gph for global-memory inputs, lph for LDS rows.
+    // A new phase gives fresh opaque lane offsets, i.e. forces re-loads.
+    int gph = 0, lph = 0, gctr = 0, lctr = 0;
+    std::vector<std::pair<int, int>> phase_stack;
+    void open(const std::string &s) { ln(s); indent++; scopes.push_back({}); phase_stack.push_back({gph, lph}); }
+    void close(const std::string &s = "}") {
+        scopes.pop_back(); indent--; ln(s);
+        // phases begun inside the block die with it; names stay unique via the counters
+        gph = phase_stack.back().first; lph = phase_stack.back().second; phase_stack.pop_back();
     }
-    // name of input value arr[j] for the current phase; emits its load on first use
-    std::string in(const char *arr, long j) {
-        std::string name = std::string(arr) + S(j) + "_" + S(phase);
+    void begin_phase(bool global = true, bool lds = true) {
+        if (global) {
+            gph = ++gctr;
+            ln("int lo" + S(gph) + " = lane; asm volatile(\"\" : \"+v\"(lo" + S(gph) + "));");
+        }
+        if (lds && use_lds) {
+            lph = ++lctr;
+            ln("int lt" + S(lph) + " = threadIdx.x; asm volatile(\"\" : \"+v\"(lt" + S(lph) + "));");
+        }
+    }
+    bool cached(const std::string &name) const {
         for (auto &sc : scopes)
             for (auto &nm : sc)
-                if (nm == name) return name;
-        ln("const double " + name + " = t" + arr + "[" + S(j * 64) + " + lo" + S(phase) + "];");
+                if (nm == name) return true;
+        return false;
+    }
+    void uncache(const std::string &prefix) {
+        for (auto &sc : scopes)
+            for (auto it = sc.begin(); it != sc.end();)
+                it = (it->compare(0, prefix.size(), prefix) == 0) ? sc.erase(it) : it + 1;
+    }
+    std::string lds_at(long row) const { return "qpb_lds[" + S(row * opt.wg) + " + lt" + S(lph) + "]"; }
+    std::string lds_st(long row) const { return "qpb_lds[" + S(row * opt.wg) + " + threadIdx.x]"; }
+    // name of input value arr[j] for the current phase; emits its load on first use
+    std::string in(const char *arr, long j) {
+        long base = (arr[1] != 0) ? -1 : arr[0] == 'A' ? lds_A : arr[0] == 'G' ? lds_G : arr[0] == 'P' ? lds_P : -1;
+        const bool lds = use_lds && base >= 0;
+        std::string name = std::string(arr) + S(j) + (lds ? "_l" + S(lph) : "_g" + S(gph));
+        if (cached(name)) return name;
+        if (lds) ln("const double " + name + " = " + lds_at(base + j) + ";");
+        else ln("const double " + name + " = t" + arr + "[" + S(j * 64) + " + lo" + S(gph) + "];");
         scopes.back().push_back(name);
         return name;
+    }
+    // Loop vectors (x, y, rx, ry, rz) may be "parked" in LDS rows (fast mode):
+    // rd() reads element i, wr() writes it.
+    std::map<std::string, long> park;
+    std::string rd(const std::string &v, long i) {
+        auto it = park.find(v);
+        if (it == park.end()) return V(v.c_str(), i);
+        std::string name = "pk_" + v + S(i) + "_l" + S(lph);
+        if (cached(name)) return name;
+        ln("const double " + name + " = " + lds_at(it->second + i) + ";");
+        scopes.back().push_back(name);
+        return name;
+    }
+    void wr(const std::string &v, long i, const std::string &expr) {
+        auto it = park.find(v);
+        if (it == park.end()) { ln(V(v.c_str(), i) + " = " + expr + ";"); return; }
+        ln(lds_st(it->second + i) + " = " + expr + ";");
+        uncache("pk_" + v + S(i) + "_");
     }
     static std::string S(long v) { return std::to_string(v); }
     static std::string V(const char *base, long i) { return std::string(base) + std::to_string(i); }
@@ -95,15 +192,23 @@ struct Gen {
         auto ensure_dk = [&]() {
             if (!dk_ready) { ln("double Dk = " + yval(k) + ";"); dk_ready = true; }
         };
+        auto update = [&](long r, const std::string &lv, const std::string &yi) {
+            if (yset[r]) ln(yname(r) + " = " + msub(yname(r), lv, yi) + ";");
+            else { ln("double " + yname(r) + " = -(" + lv + " * " + yi + ");"); yset[r] = 1; }
+        };
+        std::vector<const FacStep *> pend;     // buffered updates of a leaf column
+        bool dk_zero = false;                  // D(k) structurally 0 (no diag, no updates)
         for (const FacStep &st : pl.fac) {
             switch (st.op) {
                 case FacOp::RowBegin:
                     k = st.a;
                     std::fill(yset.begin(), yset.end(), 0);
                     dk_ready = false;
+                    dk_zero = true;
                     open("{ // LDL row " + S(k));
                     break;
                 case FacOp::Scatter: {
+                    if (st.a == k) dk_zero = false;
                     std::string v = slot(map[st.b]);
                     if (yset[st.a]) ln(yname(st.a) + " = " + yname(st.a) + " + " + v + ";");
                     else { ln("double " + yname(st.a) + " = " + v + ";"); yset[st.a] = 1; }
@@ -111,17 +216,30 @@ struct Gen {
                 }
                 case FacOp::Update: {
                     ensure_dk();
-                    std::string yi = yval(st.c), L = V("L", st.b);
-                    if (yset[st.a]) ln(yname(st.a) + " = " + msub(yname(st.a), L, yi) + ";");
-                    else { ln("double " + yname(st.a) + " = -(" + L + " * " + yi + ");"); yset[st.a] = 1; }
+                    if (leaf[st.c]) { pend.push_back(&st); break; }
+                    update(st.a, V("L", st.b), yval(st.c));
                     break;
                 }
                 case FacOp::NewL: {
                     ensure_dk();
-                    std::string yi = yval(st.a), L = V("L", st.b);
-                    if (opt.exact) ln(L + " = " + yi + " / " + V("D", st.a) + ";");
-                    else ln(L + " = " + yi + " * " + V("rD", st.a) + ";");
-                    ln("Dk = " + msub("Dk", L, yi) + ";");
+                    dk_zero = false;
+                    std::string yi = yval(st.a);
+                    if (opt.exact) {
+                        std::string L = V("L", st.b);
+                        ln(L + " = " + yi + " / " + V("D", st.a) + ";");
+                        ln("Dk = " + msub("Dk", L, yi) + ";");
+                    } else if (leaf[st.a]) {
+                        // l = L(k,i) = K(i,k)/D(i); Y[r] -= L(r,i)*K(i,k) == K(i,r)*l
+                        std::string l = "l" + S(st.b);
+                        ln("const double " + l + " = " + yi + " * " + V("rD", st.a) + ";");
+                        for (const FacStep *u : pend) update(u->a, slot(map[leaf_slot[u->b]]), l);
+                        pend.clear();
+                        ln("Dk = " + msub("Dk", l, yi) + ";");
+                    } else {
+                        std::string L = V("L", st.b);
+                        ln(L + " = " + yi + " * " + V("rD", st.a) + ";");
+                        ln("Dk = " + msub("Dk", L, yi) + ";");
+                    }
                     break;
                 }
                 case FacOp::RowEnd: {
@@ -130,7 +248,12 @@ struct Gen {
                     if (opt.exact)
                         ln("{ const double sg = Dk <= 0.0 ? -1.0 : 1.0; " + V("D", k) +
                            " = (sg * Dk <= 1e-14) ? sg * 1e-7 : Dk; }");
-                    else
+                    else if (dk_zero) {
+                        // D = 0 exactly -> always regularised to -1e-7 (ldl.c:319-320)
+                        char buf[64];
+                        snprintf(buf, sizeof buf, "%.17g", 1.0 / -1e-7);
+                        ln(V("rD", k) + " = " + buf + "; (void)Dk;");
+                    } else
                         ln("{ const double sg = Dk <= 0.0 ? -1.0 : 1.0; " + V("rD", k) +
                            " = qpb_rcp((sg * Dk <= 1e-14) ? sg * 1e-7 : Dk); }");
                     close();
@@ -142,24 +265,48 @@ struct Gen {
 
     // LDL_perm / lsolve / dsolve / ltsolve / permt (ldl.c:495-597).
     template <class In, class Out>
-    void solve(In rhs, Out out) {
+    void solve(const std::vector<Slot> &map, In rhs, Out out) {
         const long N = pl.N;
         open("{ // KKT solve");
+        begin_phase(false, true);   // fresh LDS offsets: no load merging across solves
         for (long j = 0; j < N; j++) ln("double X" + S(j) + " = " + rhs(pl.perm[j]) + ";");
-        for (long j = 0; j < N; j++)
+        if (!opt.exact) begin_phase();
+        for (long j = 0; j < N; j++) {
+            if (pl.Lp[j] == pl.Lp[j + 1]) continue;
+            if (!opt.exact && leaf[j]) {
+                ln("{ const double t = " + V("rD", j) + " * " + V("X", j) + ";");
+                for (long e = pl.Lp[j]; e < pl.Lp[j + 1]; e++) {
+                    std::string t = V("X", pl.Li[e]);
+                    ln("  " + t + " = " + msub(t, slot(map[leaf_slot[e]]), "t") + ";");
+                }
+                ln("}");
+                continue;
+            }
             for (long e = pl.Lp[j]; e < pl.Lp[j + 1]; e++) {
                 std::string t = V("X", pl.Li[e]);
                 ln(t + " = " + msub(t, V("L", e), V("X", j)) + ";");
             }
+        }
         for (long j = 0; j < N; j++) {
             if (opt.exact) ln(V("X", j) + " = " + V("X", j) + " / " + V("D", j) + ";");
             else ln(V("X", j) + " = " + V("X", j) + " * " + V("rD", j) + ";");
         }
-        for (long j = N - 1; j >= 0; j--)
-            for (long e = pl.Lp[j]; e < pl.Lp[j + 1]; e++) {
-                std::string t = V("X", j);
-                ln(t + " = " + msub(t, V("L", e), V("X", pl.Li[e])) + ";");
+        if (!opt.exact) begin_phase();
+        for (long j = N - 1; j >= 0; j--) {
+            if (pl.Lp[j] == pl.Lp[j + 1]) continue;
+            std::string t = V("X", j);
+            if (!opt.exact && leaf[j]) {
+                std::string acc;
+                for (long e = pl.Lp[j]; e < pl.Lp[j + 1]; e++) {
+                    std::string term = slot(map[leaf_slot[e]]);
+                    acc = acc.empty() ? term + " * " + V("X", pl.Li[e]) : madd(acc, term, V("X", pl.Li[e]));
+                }
+                ln(t + " = " + msub(t, V("rD", j), "(" + acc + ")") + ";");
+                continue;
             }
+            for (long e = pl.Lp[j]; e < pl.Lp[j + 1]; e++)
+                ln(t + " = " + msub(t, V("L", e), V("X", pl.Li[e])) + ";");
+        }
         for (long j = 0; j < N; j++) {
             std::string dst = out(pl.perm[j]);
             if (!dst.empty()) ln(dst + " = " + V("X", j) + ";");
@@ -174,7 +321,7 @@ struct Gen {
         for (long i = 0; i < M.cols; i++)
             for (long k = M.jc[i]; k < M.jc[i + 1]; k++) {
                 long r = M.ir[k];
-                std::string a = in(val, src ? (*src)[k] : k), x = V(xv, i), d = V(dst, r);
+                std::string a = in(val, src ? (*src)[k] : k), x = rd(xv, i), d = V(dst, r);
                 if (set[r]) ln(d + " = " + msub(d, x, a) + ";");
                 else { ln("double " + d + " = -(" + x + " * " + a + ");"); set[r] = 1; }
             }
@@ -185,8 +332,8 @@ struct Gen {
     // acc = sum a_i*b_i, sequential from 0 (Auxilary.c:451-462)
     void dot(const std::string &acc, long cnt, const char *a, const char *b) {
         if (cnt == 0) { ln("double " + acc + " = 0.0;"); return; }
-        ln("double " + acc + " = " + V(a, 0) + " * " + V(b, 0) + ";");
-        for (long i = 1; i < cnt; i++) ln(acc + " = " + madd(acc, V(a, i), V(b, i)) + ";");
+        ln("double " + acc + " = " + rd(a, 0) + " * " + rd(b, 0) + ";");
+        for (long i = 1; i < cnt; i++) ln(acc + " = " + madd(acc, rd(a, i), rd(b, i)) + ";");
     }
 
     void decl_vec(const char *base, long cnt, const char *init = nullptr) {
@@ -204,11 +351,12 @@ struct Gen {
     // findsteplength (Auxilary.c:359-393) into variables ap, ad.
     void step_length() {
         const long m = pl.m;
+        begin_phase(false, true);
         if (opt.exact) {
             ln("ap = 1e10; ad = 1e10;");
             open("{ bool hp = false, hd = false;");
             for (long i = 0; i < m; i++) {
-                ln("{ const double r = (-" + V("s", i) + ") / " + V("dsl", i) + "; const bool t = (" + V("dsl", i) +
+                ln("{ const double r = (-" + rd("s", i) + ") / " + V("dsl", i) + "; const bool t = (" + V("dsl", i) +
                    " < 0.0) && (r < ap); ap = t ? r : ap; hp = hp || t; }");
                 ln("{ const double r = (-" + V("z", i) + ") / " + V("dz", i) + "; const bool t = (" + V("dz", i) +
                    " < 0.0) && (r < ad); ad = t ? r : ad; hd = hd || t; }");
@@ -217,17 +365,17 @@ struct Gen {
             ln("if (!hd) ad = 1.0;");
             close();
         } else {
-            // min over {i: d_i < 0} of s_i / (-d_i), tracked as a fraction (num/den,
-            // den > 0) with cross-multiplied compares; one division at the end.
-            open("{ double pn = 1e10, pd = 1.0, dn = 1e10, dd = 1.0; bool hp = false, hd = false;");
+            // alpha = min over {i: d_i < 0} of v_i/(-d_i)  ==  1 / max_i(-d_i / v_i)
+            // (v = s or z > 0); the reference keeps alpha = 1 when no ratio is below
+            // its 1e10 start value (Auxilary.c:362-391) -> beta threshold 1e-10.
+            // v_rcp_f64 alone suffices: the step is damped by 0.99 afterwards.
+            open("{ double bp = 0.0, bd = 0.0;");
             for (long i = 0; i < m; i++) {
-                ln("{ const double nd = -" + V("dsl", i) + "; const bool t = (nd > 0.0) && (" + V("s", i) +
-                   " * pd < pn * nd); pn = t ? " + V("s", i) + " : pn; pd = t ? nd : pd; hp = hp || t; }");
-                ln("{ const double nd = -" + V("dz", i) + "; const bool t = (nd > 0.0) && (" + V("z", i) +
-                   " * dd < dn * nd); dn = t ? " + V("z", i) + " : dn; dd = t ? nd : dd; hd = hd || t; }");
+                ln("bp = __builtin_fmax(bp, -" + V("dsl", i) + " * __builtin_amdgcn_rcp(" + rd("s", i) + "));");
+                ln("bd = __builtin_fmax(bd, -" + V("dz", i) + " * " + V("rz_", i) + ");");
             }
-            ln("ap = hp ? pn / pd : 1.0;");
-            ln("ad = hd ? dn / dd : 1.0;");
+            ln("ap = bp > 1e-10 ? __builtin_amdgcn_rcp(bp) : 1.0;");
+            ln("ad = bd > 1e-10 ? __builtin_amdgcn_rcp(bd) : 1.0;");
             close();
         }
     }
@@ -277,28 +425,52 @@ struct Gen {
         tbase("h", m);
         if (p) tbase("b", p);
         // inputs
-        decl_vec("L", pl.lnz);
+        {
+            std::vector<long> keep;
+            for (long e = 0; e < pl.lnz; e++)
+                if (opt.exact || !leaf[col_of(e)]) keep.push_back(e);
+            for (size_t i0 = 0; i0 < keep.size(); i0 += 8) {
+                std::string d = "double ";
+                for (size_t i = i0; i < keep.size() && i < i0 + 8; i++) d += (i > i0 ? ", " : "") + V("L", keep[i]);
+                ln(d + ";");
+            }
+        }
+        if (use_lds) {
+            ln("__shared__ double qpb_lds[" + S(lds_rows * opt.wg) + "];");
+            ln("{ // stage this lane's matrix values in its private LDS column");
+            for (long j = 0; lds_A >= 0 && j < (pl.p ? pl.A.nnz() : 0); j++)
+                ln("  qpb_lds[" + S((lds_A + j) * opt.wg) + " + threadIdx.x] = tA[" + S(j * 64) + " + lane];");
+            for (long j = 0; lds_G >= 0 && j < pl.G.nnz(); j++)
+                ln("  qpb_lds[" + S((lds_G + j) * opt.wg) + " + threadIdx.x] = tG[" + S(j * 64) + " + lane];");
+            for (long j = 0; lds_P >= 0 && j < pl.Pin.nnz(); j++)
+                ln("  qpb_lds[" + S((lds_P + j) * opt.wg) + " + threadIdx.x] = tP[" + S(j * 64) + " + lane];");
+            ln("}");
+        }
         if (opt.exact) decl_vec("D", N);
         else decl_vec("rD", N);
-        decl_vec("x", n);
-        decl_vec("y", p);
-        decl_vec("s", m);
+        if (!park.count("x")) decl_vec("x", n);
+        if (!park.count("y")) decl_vec("y", p);
+        if (!park.count("s")) decl_vec("s", m);
         decl_vec("z", m);
 
         // ---- kkt_initialize (Auxilary.c:992-1089)
         ln("// setup: factor the KKT holding -I, solve for rhs [-c; b; h]");
         begin_phase();
         factor(pl.K_init);
-        solve([&](long t) -> std::string {
+        decl_vec("x0_", n);
+        decl_vec("y0_", p);
+        solve(pl.K_init, [&](long t) -> std::string {
                   if (t < n) return "(-" + in("c", t) + ")";
                   if (t < n + p) return in("b", t - n);
                   return in("h", t - n - p);
               },
               [&](long t) -> std::string {
-                  if (t < n) return V("x", t);
-                  if (t < n + p) return V("y", t - n);
+                  if (t < n) return V("x0_", t);
+                  if (t < n + p) return V("y0_", t - n);
                   return "";
               });
+        for (long i = 0; i < n; i++) wr("x", i, V("x0_", i));
+        for (long i = 0; i < p; i++) wr("y", i, V("y0_", i));
         open("{");
         spmv_neg(pl.G, nullptr, "G", "x", "zi");
         for (long i = 0; i < m; i++) ln(V("zi", i) + " = " + V("zi", i) + " + " + in("h", i) + ";");
@@ -308,7 +480,7 @@ struct Gen {
             ln("if (" + V("zi", i) + " > hi) hi = " + V("zi", i) + ";");
         }
         ln("const double sh = -lo;");
-        for (long i = 0; i < m; i++) ln(V("s", i) + " = sh < 0 ? " + V("zi", i) + " : " + V("zi", i) + " + (1 + sh);");
+        for (long i = 0; i < m; i++) wr("s", i, "sh < 0 ? " + V("zi", i) + " : " + V("zi", i) + " + (1 + sh)");
         for (long i = 0; i < m; i++) ln(V("z", i) + " = hi < 0 ? -" + V("zi", i) + " : -" + V("zi", i) + " + (1 + hi);");
         close();
 
@@ -319,117 +491,192 @@ struct Gen {
         open("for (;;) {");
         ln("if (it >= a.maxit) { flag = 2; break; }");
         begin_phase();
-        // residuals
-        spmv_neg(pl.Pf, &pl.Pf_src, "P", "x", "t");
-        dot("f1", n, "t", "x");
-        for (long j = 0; j < n; j++) in("c", j);
-        ln("double f2 = " + V("c", 0) + "_" + S(phase) + " * x0;");
-        for (long j = 1; j < n; j++) ln("f2 = " + madd("f2", V("c", j) + "_" + S(phase), V("x", j)) + ";");
-        ln("fval = -0.5 * f1 + f2;");
-        for (long j = 0; j < n; j++) ln("double " + V("rx", j) + " = " + V("t", j) + ";");
-        for (long j = 0; j < n; j++)
-            for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1]; k++)
-                ln(V("rx", j) + " = " + msub(V("rx", j), in("G", k), V("z", pl.G.ir[k])) + ";");
-        if (p)
+        // residuals (Auxilary.c:745-786) and objective (Auxilary.c:1133-1141)
+        if (opt.exact) {
+            spmv_neg(pl.Pf, &pl.Pf_src, "P", "x", "t");
+            ln("double f1 = t0 * " + rd("x", 0) + ";");
+            for (long j = 1; j < n; j++) ln("f1 = " + madd("f1", V("t", j), rd("x", j)) + ";");
+            ln("double f2 = " + in("c", 0) + " * " + rd("x", 0) + ";");
+            for (long j = 1; j < n; j++) ln("f2 = " + madd("f2", in("c", j), rd("x", j)) + ";");
+            ln("fval = -0.5 * f1 + f2;");
+            for (long j = 0; j < n; j++) ln("double " + V("rx", j) + " = " + V("t", j) + ";");
             for (long j = 0; j < n; j++)
-                for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++)
-                    ln(V("rx", j) + " = " + msub(V("rx", j), in("A", k), V("y", pl.A.ir[k])) + ";");
-        for (long j = 0; j < n; j++) ln(V("rx", j) + " = " + V("rx", j) + " - " + in("c", j) + ";");
-        dot("nrx2", n, "rx", "rx");
-        ln("st_rx = __builtin_sqrt(nrx2);");
-        if (p) {
-            spmv_neg(pl.A, nullptr, "A", "x", "ry");
-            for (long i = 0; i < p; i++) ln(V("ry", i) + " = " + V("ry", i) + " + " + in("b", i) + ";");
-            dot("nry2", p, "ry", "ry");
-            ln("st_ry = __builtin_sqrt(nry2);");
+                for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1]; k++)
+                    ln(V("rx", j) + " = " + msub(V("rx", j), in("G", k), V("z", pl.G.ir[k])) + ";");
+            if (p)
+                for (long j = 0; j < n; j++)
+                    for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++)
+                        ln(V("rx", j) + " = " + msub(V("rx", j), in("A", k), rd("y", pl.A.ir[k])) + ";");
+            for (long j = 0; j < n; j++) ln(V("rx", j) + " = " + V("rx", j) + " - " + in("c", j) + ";");
+            dot("nrx2", n, "rx", "rx");
+            ln("st_rx = __builtin_sqrt(nrx2);");
+            if (park.count("rx")) for (long j = 0; j < n; j++) wr("rx", j, V("rx", j));
+            if (p) {
+                spmv_neg(pl.A, nullptr, "A", "x", "ry");
+                for (long i = 0; i < p; i++) ln(V("ry", i) + " = " + V("ry", i) + " + " + in("b", i) + ";");
+                dot("nry2", p, "ry", "ry");
+                ln("st_ry = __builtin_sqrt(nry2);");
+                if (park.count("ry")) for (long i = 0; i < p; i++) wr("ry", i, V("ry", i));
+            }
+            spmv_neg(pl.G, nullptr, "G", "x", "rz");
+            for (long i = 0; i < m; i++) ln(V("rz", i) + " = " + V("rz", i) + " + (" + in("h", i) + " - " + rd("s", i) + ");");
+            dot("nrz2", m, "rz", "rz");
+            ln("st_rz = __builtin_sqrt(nrz2);");
+            if (park.count("rz")) for (long i = 0; i < m; i++) wr("rz", i, V("rz", i));
+
+        } else {
+            // Fast: one pass over every stored value, each used for both of its
+            // products while in a register (P upper-symmetric, A and G for their
+            // product and transposed product) -- same sums, another order.
+            for (long j = 0; j < n; j++) ln("double " + V("t", j) + " = 0.0;");
+            for (long j = 0; j < n; j++) ln("double " + V("rx", j) + " = 0.0;");
+            for (long i = 0; i < p; i++) ln("double " + V("ry", i) + " = " + in("b", i) + ";");
+            for (long i = 0; i < m; i++) ln("double " + V("rz", i) + " = " + in("h", i) + " - " + rd("s", i) + ";");
+            if (pl.pmode == P_UPPER) {
+                for (long c = 0; c < n; c++)
+                    for (long k = pl.Pin.jc[c]; k < pl.Pin.jc[c + 1]; k++) {
+                        long r = pl.Pin.ir[k];
+                        std::string v = in("P", k);
+                        ln(V("t", r) + " = " + msub(V("t", r), v, rd("x", c)) + ";");
+                        if (r != c) ln(V("t", c) + " = " + msub(V("t", c), v, rd("x", r)) + ";");
+                    }
+            } else {
+                for (long c = 0; c < n; c++)
+                    for (long k = pl.Pf.jc[c]; k < pl.Pf.jc[c + 1]; k++)
+                        ln(V("t", pl.Pf.ir[k]) + " = " + msub(V("t", pl.Pf.ir[k]), in("P", pl.Pf_src[k]), rd("x", c)) + ";");
+            }
+            for (long j = 0; j < n; j++)
+                for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1]; k++) {
+                    std::string v = in("G", k);
+                    long r = pl.G.ir[k];
+                    ln(V("rx", j) + " = " + msub(V("rx", j), v, V("z", r)) + ";");
+                    ln(V("rz", r) + " = " + msub(V("rz", r), v, rd("x", j)) + ";");
+                }
+            if (p)
+                for (long j = 0; j < n; j++)
+                    for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++) {
+                        std::string v = in("A", k);
+                        long r = pl.A.ir[k];
+                        ln(V("rx", j) + " = " + msub(V("rx", j), v, rd("y", r)) + ";");
+                        ln(V("ry", r) + " = " + msub(V("ry", r), v, rd("x", j)) + ";");
+                    }
+            ln("double f1 = t0 * " + rd("x", 0) + ";");
+            for (long j = 1; j < n; j++) ln("f1 = " + madd("f1", V("t", j), rd("x", j)) + ";");
+            ln("double f2 = " + in("c", 0) + " * " + rd("x", 0) + ";");
+            for (long j = 1; j < n; j++) ln("f2 = " + madd("f2", in("c", j), rd("x", j)) + ";");
+            ln("fval = -0.5 * f1 + f2;");
+            for (long j = 0; j < n; j++) ln(V("rx", j) + " = " + V("rx", j) + " + " + V("t", j) + " - " + in("c", j) + ";");
+            dot("nrx2", n, "rx", "rx");
+            ln("st_rx = __builtin_sqrt(nrx2);");
+            if (park.count("rx")) for (long j = 0; j < n; j++) wr("rx", j, V("rx", j));
+            if (p) {
+                dot("nry2", p, "ry", "ry");
+                ln("st_ry = __builtin_sqrt(nry2);");
+                if (park.count("ry")) for (long i = 0; i < p; i++) wr("ry", i, V("ry", i));
+            }
+            dot("nrz2", m, "rz", "rz");
+            ln("st_rz = __builtin_sqrt(nrz2);");
+            if (park.count("rz")) for (long i = 0; i < m; i++) wr("rz", i, V("rz", i));
         }
-        spmv_neg(pl.G, nullptr, "G", "x", "rz");
-        for (long i = 0; i < m; i++) ln(V("rz", i) + " = " + V("rz", i) + " + (" + in("h", i) + " - " + V("s", i) + ");");
-        dot("nrz2", m, "rz", "rz");
-        ln("st_rz = __builtin_sqrt(nrz2);");
         dot("sz", m, "s", "z");
         ln("st_mu = sz / " + S(m) + ".0;");
         ln(std::string("if (st_rx < a.tol && st_rz < a.tol") + (p ? " && st_ry < a.tol" : "") +
            " && st_mu < a.abstol) { flag = 0; break; }");
         // lambda, mu (qpSWIFT.c:537-538)
-        for (long i = 0; i < m; i++) ln("const double " + V("lam", i) + " = __builtin_sqrt(" + V("s", i) + " * " + V("z", i) + ");");
-        dot("mu2", m, "lam", "lam");
-        ln("const double mu = mu2 / " + S(m) + ".0;");
+        // lambda = sqrt(s.*z) (Auxilary.c:638-646) only ever enters squared, so the
+        // fast kernel uses lambda^2 = s.*z directly (no sqrt).
+        if (opt.exact) {
+            for (long i = 0; i < m; i++) ln("const double " + V("lam", i) + " = __builtin_sqrt(" + rd("s", i) + " * " + V("z", i) + ");");
+            dot("mu2", m, "lam", "lam");
+            ln("const double mu = mu2 / " + S(m) + ".0;");
+        } else {
+            ln("const double mu = st_mu;");
+        }
+        auto lam2 = [&](long i) {
+            return opt.exact ? "(" + V("lam", i) + " * " + V("lam", i) + ")" : "(" + rd("s", i) + " * " + V("z", i) + ")";
+        };
         ln("const bool pc = sigma > a.sigma_d;");
         if (!opt.exact)
             for (long i = 0; i < m; i++) ln("const double " + V("rz_", i) + " = qpb_rcp(" + V("z", i) + ");");
+
         // updatekktmatrix: -s/z on the z diagonal (Auxilary.c:211-215)
         for (long i = 0; i < m; i++) {
-            if (opt.exact) ln("const double " + V("kd", i) + " = (-" + V("s", i) + ") / " + V("z", i) + ";");
-            else ln("const double " + V("kd", i) + " = -" + V("s", i) + " * " + V("rz_", i) + ";");
+            if (opt.exact) ln("const double " + V("kd", i) + " = (-" + rd("s", i) + ") / " + V("z", i) + ";");
+            else ln("const double " + V("kd", i) + " = -" + rd("s", i) + " * " + V("rz_", i) + ";");
         }
-        // form_ds: predictor (pure Newton) or pure centering (qpSWIFT.c:542, 574-575)
+        begin_phase();
+        factor(pl.K_loop);
+        // form_ds: predictor (pure Newton) or pure centering (qpSWIFT.c:542, 574-575);
+        // ds does not enter the factorisation, so it is formed after it (shorter
+        // live range)
+        begin_phase(false, true);
         decl_vec("ds", m);
         ln("if (!pc) sigma = a.sigma_d;");
         for (long i = 0; i < m; i++)
-            ln(V("ds", i) + " = pc ? (-" + V("lam", i) + ") * " + V("lam", i) + " : -(" + V("lam", i) + " * " +
-               V("lam", i) + ") + (sigma * mu);");
-        begin_phase();
-        factor(pl.K_loop);
+            ln(V("ds", i) + " = pc ? " + (opt.exact ? "(-" + V("lam", i) + ") * " + V("lam", i) : "-" + lam2(i)) +
+               " : -" + lam2(i) + " + (sigma * mu);");
         decl_vec("dx", n);
         decl_vec("dy", p);
         decl_vec("dz", m);
         decl_vec("dsl", m);
         auto rhs = [&](long t) -> std::string {
-            if (t < n) return V("rx", t);
-            if (t < n + p) return V("ry", t - n);
+            if (t < n) return rd("rx", t);
+            if (t < n + p) return rd("ry", t - n);
             long i = t - n - p;
-            if (opt.exact) return "(" + V("rz", i) + " - (" + V("ds", i) + " / " + V("z", i) + "))";
-            return "__builtin_fma(-" + V("ds", i) + ", " + V("rz_", i) + ", " + V("rz", i) + ")";
+            if (opt.exact) return "(" + rd("rz", i) + " - (" + V("ds", i) + " / " + V("z", i) + "))";
+            return "__builtin_fma(-" + V("ds", i) + ", " + V("rz_", i) + ", " + rd("rz", i) + ")";
         };
         auto dsl_from_dz = [&]() {
+            begin_phase(false, true);
             for (long i = 0; i < m; i++) {
-                std::string num = V("ds", i) + " - (" + V("s", i) + " * " + V("dz", i) + ")";
+                std::string num = V("ds", i) + " - (" + rd("s", i) + " * " + V("dz", i) + ")";
                 if (opt.exact) ln(V("dsl", i) + " = (" + num + ") / " + V("z", i) + ";");
-                else ln(V("dsl", i) + " = __builtin_fma(-" + V("s", i) + ", " + V("dz", i) + ", " + V("ds", i) +
+                else ln(V("dsl", i) + " = __builtin_fma(-" + rd("s", i) + ", " + V("dz", i) + ", " + V("ds", i) +
                         ") * " + V("rz_", i) + ";");
             }
         };
         // predictor solve, step, rho, sigma, corrector ds (kktsolve_1, qpSWIFT.c:552-569)
         open("if (pc) {");
-        solve(rhs, [&](long t) -> std::string {
+        solve(pl.K_loop, rhs, [&](long t) -> std::string {
             if (t < n + p) return "";
             return V("dz", t - n - p);
         });
         dsl_from_dz();
         step_length();
+        begin_phase(false, true);
         ln("double rho_n = 0.0;");
         for (long i = 0; i < m; i++)
-            ln("rho_n = rho_n + (" + V("s", i) + " + (ap * " + V("dsl", i) + ")) * (" + V("z", i) + " + (ad * " + V("dz", i) + "));");
+            ln("rho_n = rho_n + (" + rd("s", i) + " + (ap * " + V("dsl", i) + ")) * (" + V("z", i) + " + (ad * " + V("dz", i) + "));");
         ln("const double rho = rho_n / sz;");
         ln("const double r1 = 1 > rho ? rho : 1;");
         ln("const double cube = r1 * r1 * r1;");
         ln("sigma = a.sigma_d < cube ? cube : a.sigma_d;");
         for (long i = 0; i < m; i++)
-            ln(V("ds", i) + " = -(" + V("lam", i) + " * " + V("lam", i) + ") - (" + V("dsl", i) + " * " + V("dz", i) +
+            ln(V("ds", i) + " = -" + lam2(i) + " - (" + V("dsl", i) + " * " + V("dz", i) +
                ") + (sigma * mu);");
         close();
         // corrector / centering solve (kktsolve_2, Auxilary.c:524-564)
-        solve(rhs, [&](long t) -> std::string {
+        solve(pl.K_loop, rhs, [&](long t) -> std::string {
             if (t < n) return V("dx", t);
             if (t < n + p) return V("dy", t - n);
             return V("dz", t - n - p);
         });
         dsl_from_dz();
         step_length();
+        begin_phase(false, true);
         ln("ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;");
         ln("ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;");
-        for (long i = 0; i < n; i++) ln(V("x", i) + " = " + madd(V("x", i), V("dx", i), "ap") + ";");
-        for (long i = 0; i < p; i++) ln(V("y", i) + " = " + madd(V("y", i), V("dy", i), "ad") + ";");
-        for (long i = 0; i < m; i++) ln(V("s", i) + " = " + madd(V("s", i), V("dsl", i), "ap") + ";");
+        for (long i = 0; i < n; i++) wr("x", i, madd(rd("x", i), V("dx", i), "ap"));
+        for (long i = 0; i < p; i++) wr("y", i, madd(rd("y", i), V("dy", i), "ad"));
+        for (long i = 0; i < m; i++) wr("s", i, madd(rd("s", i), V("dsl", i), "ap"));
         for (long i = 0; i < m; i++) ln(V("z", i) + " = " + madd(V("z", i), V("dz", i), "ad") + ";");
         ln("it++;");
         close();
         // outputs
+        begin_phase(false, true);
         auto store = [&](const char *arr, long nv, const char *base) {
-            ln(std::string("{ double *__restrict__ o = a.") + arr + " + tile * " + S(nv * 64) + " + lane;");
-            for (long i = 0; i < nv; i++) ln("  o[" + S(i * 64) + "] = " + V(base, i) + ";");
-            ln("}");
+            ln(std::string("double *__restrict__ o_") + arr + " = a." + arr + " + tile * " + S(nv * 64) + " + lane;");
+            for (long i = 0; i < nv; i++) ln("o_" + std::string(arr) + "[" + S(i * 64) + "] = " + rd(base, i) + ";");
         };
         store("x", n, "x");
         if (p) store("y", p, "y");
@@ -447,8 +694,28 @@ struct Gen {
 
 std::string kernel_name(const Plan &pl, const GenOptions &opt) {
     char buf[96];
-    snprintf(buf, sizeof buf, "qpb_ipm_%016llx_%s_w%d", (unsigned long long)pl.hash, opt.exact ? "x" : "f", opt.wg);
+    snprintf(buf, sizeof buf, "qpb_ipm_%016llx_%s_w%d_l%d", (unsigned long long)pl.hash, opt.exact ? "x" : "f",
+             opt.wg, opt.exact ? 0 : opt.lds_mode);
     return buf;
+}
+
+GenOptions choose_options(const Plan &pl, bool exact) {
+    GenOptions o;
+    o.exact = exact;
+    o.wg = 256;
+    o.waves_per_eu = 1;
+    o.lds_mode = 0;
+    if (exact) return o;
+    const long nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz(), nP = pl.Pin.nnz();
+    const long cap = 160 * 1024 / 8;           // doubles of LDS per CU
+    const long vec = 2 * pl.n + 2 * pl.p + pl.m;  // parked loop vectors (mode 3)
+    if ((nA + nG + vec) * 256 <= cap) { o.lds_mode = 3; o.wg = 256; }
+    else if ((nA + nG + vec) * 128 <= cap) { o.lds_mode = 3; o.wg = 128; }
+    else if ((nP + nA + nG) * 256 <= cap) { o.lds_mode = 2; o.wg = 256; }
+    else if ((nP + nA + nG) * 128 <= cap) { o.lds_mode = 2; o.wg = 128; }
+    else if ((nA + nG) * 256 <= cap) { o.lds_mode = 1; o.wg = 256; }
+    else if ((nA + nG) * 128 <= cap) { o.lds_mode = 1; o.wg = 128; }
+    return o;
 }
 
 std::string generate_kernel(const Plan &pl, const GenOptions &opt) {

@@ -16,6 +16,9 @@ struct GenOptions {
     bool exact = false;
     int wg = 256;             // threads per workgroup (one QP per lane)
     int waves_per_eu = 1;     // __launch_bounds__ minimum waves per SIMD
+    // Fast mode: which matrix inputs are staged in LDS (each lane owns a private
+    // LDS column: no barriers).  0 = none, 1 = A and G, 2 = P, A and G.
+    int lds_mode = 1;
 };
 
 // Kernel argument block; identical layout in the generated device code.
@@ -32,6 +35,9 @@ struct KernelArgs {
 };
 
 std::string kernel_name(const Plan &pl, const GenOptions &opt);
+// Pick workgroup size / LDS placement for a plan (fast mode): keep every matrix
+// input on-chip when it fits the 160 KiB LDS of a CU.
+GenOptions choose_options(const Plan &pl, bool exact);
 std::string generate_kernel(const Plan &pl, const GenOptions &opt);
 
 }  // namespace qpb

@@ -189,9 +189,10 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     int rc = qpb::build_plan(plan->pl, n, m, p, (flags & QPB_P_UPPER) ? qpb::P_UPPER : qpb::P_FULL,
                              Pjc, Pir, Ajc, Air, Gjc, Gir, perm, &err);
     if (rc) return fail(rc, err);
-    plan->gen.exact = (flags & QPB_EXACT) != 0;
-    plan->gen.wg = 256;
-    plan->gen.waves_per_eu = 1;
+    plan->gen = qpb::choose_options(plan->pl, (flags & QPB_EXACT) != 0);
+    // experiment overrides (kernel name encodes them, so caches stay consistent)
+    if (const char *e = getenv("QPB_WG")) plan->gen.wg = atoi(e);
+    if (const char *e = getenv("QPB_LDS")) plan->gen.lds_mode = atoi(e);
     plan->kname = qpb::kernel_name(plan->pl, plan->gen);
     *out = plan.release();
     return QPB_OK;

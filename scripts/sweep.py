@@ -1,0 +1,80 @@
+"""A/B kernel variants in one process on one GPU (cdna guide rule 24).
+
+    python scripts/sweep.py [--batch B] [--reps R] VARIANT...
+VARIANT = "wg:lds" (fast kernel) or "exact".  Prints one JSON line per variant.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import torch
+    from apf_quadruped_amd import plans, workloads as W
+    from apf_quadruped_amd.batch import Plan
+    import bench
+    torch.cuda.set_device(0)
+    d0 = plans.standard_qp("c1")
+    seed = plans.SEED + 1
+    base = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0])
+    host = bench.make_shard(base, seed, 0, a.batch)
+    vals = {k: torch.from_numpy(v).cuda() for k, v in host.items()}
+    plans_ = {}
+    for v in a.variants:
+        if v == "exact":
+            os.environ.pop("QPB_WG", None); os.environ.pop("QPB_LDS", None)
+            plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=True)
+        else:
+            wg, lds = v.split(":")
+            os.environ["QPB_WG"], os.environ["QPB_LDS"] = wg, lds
+            plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0])
+        t0 = time.time(); plans_[v].compile(); ct = time.time() - t0
+        print(f"compiled {v} in {ct:.1f}s", file=sys.stderr)
+    os.environ.pop("QPB_WG", None); os.environ.pop("QPB_LDS", None)
+    from oracle_py import Oracle
+    o = Oracle()
+    ids = np.arange(0, a.batch, a.batch // 16)
+    dd = W.contact_force_qp(seed, ids)
+    Pc, Ac, Gc = W.to_colmajor(dd["P"]), W.to_colmajor(dd["A"]), W.to_colmajor(dd["G"])
+    times = {v: [] for v in a.variants}
+    outs = {}
+    for r in range(a.rounds):
+        for v in a.variants:
+            pl = plans_[v]
+            out = pl.solve(**vals, B=a.batch)
+            torch.cuda.synchronize()
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(); pl.solve(**vals, B=a.batch, out=out); e1.record(); torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1))
+            outs[v] = out
+    for v in a.variants:
+        pl = plans_[v]
+        res = pl.unpack(outs[v], a.batch)
+        err = 0.0
+        for k, q in enumerate(ids):
+            ref = o.solve_dense(12, 20, 6, Pc[k], Ac[k], Gc[k], dd["c"][k], dd["h"][k], dd["b"][k], perm=pl.perm)
+            err = max(err, float(np.max(np.abs(ref["x"] - res["x"][q]))))
+        ms = float(np.median(times[v]))
+        print(json.dumps(dict(variant=v, kernel=pl.info.hash, ms_median=ms, ms_min=float(np.min(times[v])),
+                              qps=a.batch / ms * 1e3, gbs=pl.bytes_per_qp() * a.batch / ms / 1e6,
+                              mean_iters=float(res["iters"].mean()), optimal=float((res["flag"] == 0).mean()),
+                              max_err_vs_oracle=err)))
+
+
+if __name__ == "__main__":
+    main()

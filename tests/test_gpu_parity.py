@@ -63,24 +63,37 @@ def test_exact_kernel_bit_identical_to_reference(name):
 @pytest.mark.parametrize("name", DENSE_CASES)
 @pytest.mark.parametrize("exact,own_order", [(False, False), (False, True), (True, True)])
 def test_kernel_within_tolerance_of_reference(name, exact, own_order):
+    """Fast kernel and/or own ordering vs the reference: |.|_inf <= 1e-6 * max(1, |ref|).
+
+    With another KKT ordering the dynamic regularisation (ldl.c:319-320) lands on
+    other pivots; where A has a row-rank defect (2-foot trot: rank 5) the dual y
+    is then only unique modulo null(A^T), so y is compared through A^T y there.
+    Truncated iterates (maxit < 100) are compared only under the reference order."""
     g = golden(name)
-    if name == "edge_zero_g_row" and own_order:
-        pytest.skip("the reference's zero-G-row behaviour depends on its AMD order")
+    truncated = int(g["maxit"]) < 100
+    if own_order and (name == "edge_zero_g_row" or truncated):
+        pytest.skip("depends on the reference's own KKT order")
     _, r = _solve(g, perm=None if own_order else g["perm"][0], exact=exact, p_upper=True)
-    conv = g["flag"] == 0
-    if int(g["maxit"]) >= 100:
+    n, m, p, P, A, G = _dense(g)
+    sel = slice(None) if truncated else (g["flag"] == 0)
+    if not truncated:
         np.testing.assert_array_equal(r["flag"], g["flag"])
-    for k in ("x", "y", "z", "s"):
-        if k == "y" and not int(g["p"]):
-            continue
-        ref = g[k][conv] if int(g["maxit"]) >= 100 else g[k]
-        got = r[k][conv] if int(g["maxit"]) >= 100 else r[k]
+
+    def close(got, ref, what, tol=TOL):
         scale = max(1.0, float(np.max(np.abs(ref)))) if ref.size else 1.0
         err = float(np.max(np.abs(got - ref))) if ref.size else 0.0
-        if int(g["maxit"]) < 100:      # truncated iterates: tolerance scaled to the iterate
-            assert err <= 1e-6 * scale * 10, (name, k, err)
+        assert err <= tol * scale, (name, what, err)
+
+    tol = 10 * TOL if truncated else TOL
+    for k in ("x", "z", "s"):
+        close(r[k][sel], g[k][sel], k, tol)
+    if p:
+        rank = np.linalg.matrix_rank(A[0])
+        if rank == p or not own_order:
+            close(r["y"][sel], g["y"][sel], "y", tol)
         else:
-            assert err <= TOL * scale, (name, k, err)
+            close(np.einsum("bji,bj->bi", A[sel], r["y"][sel]), np.einsum("bji,bj->bi", A[sel], g["y"][sel]),
+                  "A^T y", tol)
 
 
 @pytest.mark.gpu
