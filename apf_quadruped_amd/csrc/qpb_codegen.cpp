@@ -330,10 +330,13 @@ struct Gen {
     }
 
     // acc = sum a_i*b_i, sequential from 0 (Auxilary.c:451-462)
-    void dot(const std::string &acc, long cnt, const char *a, const char *b) {
+    // regs = true: the operands are the register copies (e.g. residuals just
+    // computed, before they are parked)
+    void dot(const std::string &acc, long cnt, const char *a, const char *b, bool regs = false) {
+        auto get = [&](const char *v, long i) { return regs ? V(v, i) : rd(v, i); };
         if (cnt == 0) { ln("double " + acc + " = 0.0;"); return; }
-        ln("double " + acc + " = " + rd(a, 0) + " * " + rd(b, 0) + ";");
-        for (long i = 1; i < cnt; i++) ln(acc + " = " + madd(acc, rd(a, i), rd(b, i)) + ";");
+        ln("double " + acc + " = " + get(a, 0) + " * " + get(b, 0) + ";");
+        for (long i = 1; i < cnt; i++) ln(acc + " = " + madd(acc, get(a, i), get(b, i)) + ";");
     }
 
     void decl_vec(const char *base, long cnt, const char *init = nullptr) {
@@ -508,19 +511,19 @@ struct Gen {
                     for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++)
                         ln(V("rx", j) + " = " + msub(V("rx", j), in("A", k), rd("y", pl.A.ir[k])) + ";");
             for (long j = 0; j < n; j++) ln(V("rx", j) + " = " + V("rx", j) + " - " + in("c", j) + ";");
-            dot("nrx2", n, "rx", "rx");
+            dot("nrx2", n, "rx", "rx", true);
             ln("st_rx = __builtin_sqrt(nrx2);");
             if (park.count("rx")) for (long j = 0; j < n; j++) wr("rx", j, V("rx", j));
             if (p) {
                 spmv_neg(pl.A, nullptr, "A", "x", "ry");
                 for (long i = 0; i < p; i++) ln(V("ry", i) + " = " + V("ry", i) + " + " + in("b", i) + ";");
-                dot("nry2", p, "ry", "ry");
+                dot("nry2", p, "ry", "ry", true);
                 ln("st_ry = __builtin_sqrt(nry2);");
                 if (park.count("ry")) for (long i = 0; i < p; i++) wr("ry", i, V("ry", i));
             }
             spmv_neg(pl.G, nullptr, "G", "x", "rz");
             for (long i = 0; i < m; i++) ln(V("rz", i) + " = " + V("rz", i) + " + (" + in("h", i) + " - " + rd("s", i) + ");");
-            dot("nrz2", m, "rz", "rz");
+            dot("nrz2", m, "rz", "rz", true);
             ln("st_rz = __builtin_sqrt(nrz2);");
             if (park.count("rz")) for (long i = 0; i < m; i++) wr("rz", i, V("rz", i));
 
@@ -566,15 +569,15 @@ struct Gen {
             for (long j = 1; j < n; j++) ln("f2 = " + madd("f2", in("c", j), rd("x", j)) + ";");
             ln("fval = -0.5 * f1 + f2;");
             for (long j = 0; j < n; j++) ln(V("rx", j) + " = " + V("rx", j) + " + " + V("t", j) + " - " + in("c", j) + ";");
-            dot("nrx2", n, "rx", "rx");
+            dot("nrx2", n, "rx", "rx", true);
             ln("st_rx = __builtin_sqrt(nrx2);");
             if (park.count("rx")) for (long j = 0; j < n; j++) wr("rx", j, V("rx", j));
             if (p) {
-                dot("nry2", p, "ry", "ry");
+                dot("nry2", p, "ry", "ry", true);
                 ln("st_ry = __builtin_sqrt(nry2);");
                 if (park.count("ry")) for (long i = 0; i < p; i++) wr("ry", i, V("ry", i));
             }
-            dot("nrz2", m, "rz", "rz");
+            dot("nrz2", m, "rz", "rz", true);
             ln("st_rz = __builtin_sqrt(nrz2);");
             if (park.count("rz")) for (long i = 0; i < m; i++) wr("rz", i, V("rz", i));
         }
