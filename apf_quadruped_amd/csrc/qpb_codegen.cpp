@@ -610,41 +610,60 @@ struct Gen {
         begin_phase();
         factor(pl.K_loop);
         // form_ds: predictor (pure Newton) or pure centering (qpSWIFT.c:542, 574-575);
-        // ds does not enter the factorisation, so it is formed after it (shorter
-        // live range)
-        begin_phase(false, true);
-        decl_vec("ds", m);
+        // ds does not enter the factorisation, so it is formed after it.
+        //
+        // Fast kernel algebra (same Newton systems, fewer live values): with
+        // ds = -s.*z + cc the rhs z-part is rz - ds/z = rz + s - cc/z and
+        // dsl = (ds - s.*dz)/z = -s + (cc - s.*dz)/z, where cc = 0 for the
+        // predictor, cc = sigma*mu - dsl.*dz for the corrector and sigma_d*mu for
+        // the pure centering step; so ds itself is never materialised.
         ln("if (!pc) sigma = a.sigma_d;");
-        for (long i = 0; i < m; i++)
-            ln(V("ds", i) + " = pc ? " + (opt.exact ? "(-" + V("lam", i) + ") * " + V("lam", i) : "-" + lam2(i)) +
-               " : -" + lam2(i) + " + (sigma * mu);");
+        if (opt.exact) {
+            begin_phase(false, true);
+            decl_vec("ds", m);
+            for (long i = 0; i < m; i++)
+                ln(V("ds", i) + " = pc ? (-" + V("lam", i) + ") * " + V("lam", i) + " : -" + lam2(i) + " + (sigma * mu);");
+        } else {
+            decl_vec("cc", m);
+        }
         decl_vec("dx", n);
         decl_vec("dy", p);
         decl_vec("dz", m);
         decl_vec("dsl", m);
-        auto rhs = [&](long t) -> std::string {
-            if (t < n) return rd("rx", t);
-            if (t < n + p) return rd("ry", t - n);
-            long i = t - n - p;
-            if (opt.exact) return "(" + rd("rz", i) + " - (" + V("ds", i) + " / " + V("z", i) + "))";
-            return "__builtin_fma(-" + V("ds", i) + ", " + V("rz_", i) + ", " + rd("rz", i) + ")";
+        // rhs z-part; pred = true only for the predictor solve (cc == 0)
+        auto rhs_with = [&](bool pred) {
+            return [&, pred](long t) -> std::string {
+                if (t < n) return rd("rx", t);
+                if (t < n + p) return rd("ry", t - n);
+                long i = t - n - p;
+                if (opt.exact) return "(" + rd("rz", i) + " - (" + V("ds", i) + " / " + V("z", i) + "))";
+                if (pred) return "(" + rd("rz", i) + " + " + rd("s", i) + ")";
+                return "__builtin_fma(-" + V("cc", i) + ", " + V("rz_", i) + ", " + rd("rz", i) + " + " + rd("s", i) + ")";
+            };
         };
-        auto dsl_from_dz = [&]() {
+        auto dsl_from_dz = [&](bool pred) {
             begin_phase(false, true);
             for (long i = 0; i < m; i++) {
-                std::string num = V("ds", i) + " - (" + rd("s", i) + " * " + V("dz", i) + ")";
-                if (opt.exact) ln(V("dsl", i) + " = (" + num + ") / " + V("z", i) + ";");
-                else ln(V("dsl", i) + " = __builtin_fma(-" + rd("s", i) + ", " + V("dz", i) + ", " + V("ds", i) +
-                        ") * " + V("rz_", i) + ";");
+                if (opt.exact) {
+                    std::string num = V("ds", i) + " - (" + rd("s", i) + " * " + V("dz", i) + ")";
+                    ln(V("dsl", i) + " = (" + num + ") / " + V("z", i) + ";");
+                } else if (pred) {
+                    ln(V("dsl", i) + " = -" + rd("s", i) + " * __builtin_fma(" + V("dz", i) + ", " + V("rz_", i) + ", 1.0);");
+                } else {
+                    ln(V("dsl", i) + " = __builtin_fma(__builtin_fma(-" + rd("s", i) + ", " + V("dz", i) + ", " + V("cc", i) +
+                       "), " + V("rz_", i) + ", -" + rd("s", i) + ");");
+                }
             }
         };
         // predictor solve, step, rho, sigma, corrector ds (kktsolve_1, qpSWIFT.c:552-569)
+        if (!opt.exact)
+            for (long i = 0; i < m; i++) ln(V("cc", i) + " = sigma * mu;");   // centering (!pc) default
         open("if (pc) {");
-        solve(pl.K_loop, rhs, [&](long t) -> std::string {
+        solve(pl.K_loop, rhs_with(true), [&](long t) -> std::string {
             if (t < n + p) return "";
             return V("dz", t - n - p);
         });
-        dsl_from_dz();
+        dsl_from_dz(true);
         step_length();
         begin_phase(false, true);
         ln("double rho_n = 0.0;");
@@ -654,17 +673,20 @@ struct Gen {
         ln("const double r1 = 1 > rho ? rho : 1;");
         ln("const double cube = r1 * r1 * r1;");
         ln("sigma = a.sigma_d < cube ? cube : a.sigma_d;");
-        for (long i = 0; i < m; i++)
-            ln(V("ds", i) + " = -" + lam2(i) + " - (" + V("dsl", i) + " * " + V("dz", i) +
-               ") + (sigma * mu);");
+        for (long i = 0; i < m; i++) {
+            if (opt.exact)
+                ln(V("ds", i) + " = -" + lam2(i) + " - (" + V("dsl", i) + " * " + V("dz", i) + ") + (sigma * mu);");
+            else
+                ln(V("cc", i) + " = __builtin_fma(-" + V("dsl", i) + ", " + V("dz", i) + ", sigma * mu);");
+        }
         close();
         // corrector / centering solve (kktsolve_2, Auxilary.c:524-564)
-        solve(pl.K_loop, rhs, [&](long t) -> std::string {
+        solve(pl.K_loop, rhs_with(false), [&](long t) -> std::string {
             if (t < n) return V("dx", t);
             if (t < n + p) return V("dy", t - n);
             return V("dz", t - n - p);
         });
-        dsl_from_dz();
+        dsl_from_dz(false);
         step_length();
         begin_phase(false, true);
         ln("ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;");
