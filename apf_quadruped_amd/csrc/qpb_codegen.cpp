@@ -46,7 +46,7 @@ struct Gen {
     // Fast mode: A and G values live in LDS (each lane owns one private column, so
     // no barriers are needed); lds_base[arr] = first LDS row of that array.
     bool use_lds = false;
-    long lds_rows = 0, lds_A = -1, lds_G = -1, lds_P = -1;
+    long lds_rows = 0, lds_A = -1, lds_G = -1, lds_P = -1, lds_c = -1, lds_h = -1, lds_b = -1;
 
     Gen(const Plan &p, const GenOptions &g) : pl(p), opt(g) {
         const long N = pl.N;
@@ -69,8 +69,13 @@ struct Gen {
             const long nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz(), nP = pl.Pin.nnz();
             if (opt.lds_mode >= 1) {
                 lds_A = 0; lds_G = nA; lds_rows = nA + nG;
-                if (opt.lds_mode == 2) { lds_P = lds_rows; lds_rows += nP; }
-                if (opt.lds_mode == 3) {      // park the loop vectors too
+                if (opt.lds_mode == 2 || opt.lds_mode == 4) { lds_P = lds_rows; lds_rows += nP; }
+                if (opt.lds_mode == 4) {      // every input on chip
+                    lds_c = lds_rows; lds_rows += pl.n;
+                    lds_h = lds_rows; lds_rows += pl.m;
+                    if (pl.p) { lds_b = lds_rows; lds_rows += pl.p; }
+                }
+                if (opt.lds_mode == 3 || opt.lds_mode == 4) {      // park the loop vectors too
                     const long n = pl.n, p = pl.p, m = pl.m;
                     park["x"] = lds_rows; lds_rows += n;
                     if (p) { park["y"] = lds_rows; lds_rows += p; }
@@ -78,9 +83,13 @@ struct Gen {
                     if (p) { park["ry"] = lds_rows; lds_rows += p; }
                     park["rz"] = lds_rows; lds_rows += m;
                     if ((lds_rows + m) * opt.wg * 8 <= 160 * 1024) { park["s"] = lds_rows; lds_rows += m; }
+                    if (opt.lds_mode == 4 && (lds_rows + 2 * m) * opt.wg * 8 <= 160 * 1024) {
+                        park["z"] = lds_rows; lds_rows += m;
+                        park["rzi"] = lds_rows; lds_rows += m;
+                    }
                 }
                 use_lds = lds_rows > 0 && lds_rows * opt.wg * 8 <= 160 * 1024;
-                if (!use_lds) { lds_A = lds_G = lds_P = -1; park.clear(); }
+                if (!use_lds) { lds_A = lds_G = lds_P = lds_c = lds_h = lds_b = -1; park.clear(); }
             }
         }
     }
@@ -129,7 +138,8 @@ struct Gen {
     std::string lds_st(long row) const { return "qpb_lds[" + S(row * opt.wg) + " + threadIdx.x]"; }
     // name of input value arr[j] for the current phase; emits its load on first use
     std::string in(const char *arr, long j) {
-        long base = (arr[1] != 0) ? -1 : arr[0] == 'A' ? lds_A : arr[0] == 'G' ? lds_G : arr[0] == 'P' ? lds_P : -1;
+        long base = (arr[1] != 0) ? -1 : arr[0] == 'A' ? lds_A : arr[0] == 'G' ? lds_G : arr[0] == 'P' ? lds_P
+                  : arr[0] == 'c' ? lds_c : arr[0] == 'h' ? lds_h : arr[0] == 'b' ? lds_b : -1;
         const bool lds = use_lds && base >= 0;
         std::string name = std::string(arr) + S(j) + (lds ? "_l" + S(lph) : "_g" + S(gph));
         if (cached(name)) return name;
@@ -361,7 +371,7 @@ struct Gen {
             for (long i = 0; i < m; i++) {
                 ln("{ const double r = (-" + rd("s", i) + ") / " + V("dsl", i) + "; const bool t = (" + V("dsl", i) +
                    " < 0.0) && (r < ap); ap = t ? r : ap; hp = hp || t; }");
-                ln("{ const double r = (-" + V("z", i) + ") / " + V("dz", i) + "; const bool t = (" + V("dz", i) +
+                ln("{ const double r = (-" + rd("z", i) + ") / " + V("dz", i) + "; const bool t = (" + V("dz", i) +
                    " < 0.0) && (r < ad); ad = t ? r : ad; hd = hd || t; }");
             }
             ln("if (!hp) ap = 1.0;");
@@ -375,7 +385,7 @@ struct Gen {
             open("{ double bp = 0.0, bd = 0.0;");
             for (long i = 0; i < m; i++) {
                 ln("bp = __builtin_fmax(bp, -" + V("dsl", i) + " * __builtin_amdgcn_rcp(" + rd("s", i) + "));");
-                ln("bd = __builtin_fmax(bd, -" + V("dz", i) + " * " + V("rz_", i) + ");");
+                ln("bd = __builtin_fmax(bd, -" + V("dz", i) + " * " + rd("rzi", i) + ");");
             }
             ln("ap = bp > 1e-10 ? __builtin_amdgcn_rcp(bp) : 1.0;");
             ln("ad = bd > 1e-10 ? __builtin_amdgcn_rcp(bd) : 1.0;");
@@ -383,15 +393,10 @@ struct Gen {
         }
     }
 
-    std::string div(const std::string &a, const std::string &zidx_base, long i) const {
-        // a / z_i (exact) or a * (1/z_i) (fast)
-        if (opt.exact) return "(" + a + ") / " + V(zidx_base.c_str(), i);
-        return "(" + a + ") * " + V("rz_", i);
-    }
 
     std::string build() {
         const long n = pl.n, m = pl.m, p = pl.p, N = pl.N;
-        const std::string kname = kernel_name(pl, opt);
+        const std::string kname = "QPB_KERNEL_NAME";
         o << "// generated by qpb_codegen for plan " << std::hex << pl.hash << std::dec
           << ": n=" << n << " m=" << m << " p=" << p << " N=" << N << " nnz(L)=" << pl.lnz
           << (opt.exact ? " [exact]" : " [fast]") << "\n";
@@ -447,6 +452,12 @@ struct Gen {
                 ln("  qpb_lds[" + S((lds_G + j) * opt.wg) + " + threadIdx.x] = tG[" + S(j * 64) + " + lane];");
             for (long j = 0; lds_P >= 0 && j < pl.Pin.nnz(); j++)
                 ln("  qpb_lds[" + S((lds_P + j) * opt.wg) + " + threadIdx.x] = tP[" + S(j * 64) + " + lane];");
+            for (long j = 0; lds_c >= 0 && j < n; j++)
+                ln("  qpb_lds[" + S((lds_c + j) * opt.wg) + " + threadIdx.x] = tc[" + S(j * 64) + " + lane];");
+            for (long j = 0; lds_h >= 0 && j < m; j++)
+                ln("  qpb_lds[" + S((lds_h + j) * opt.wg) + " + threadIdx.x] = th[" + S(j * 64) + " + lane];");
+            for (long j = 0; lds_b >= 0 && j < p; j++)
+                ln("  qpb_lds[" + S((lds_b + j) * opt.wg) + " + threadIdx.x] = tb[" + S(j * 64) + " + lane];");
             ln("}");
         }
         if (opt.exact) decl_vec("D", N);
@@ -454,7 +465,7 @@ struct Gen {
         if (!park.count("x")) decl_vec("x", n);
         if (!park.count("y")) decl_vec("y", p);
         if (!park.count("s")) decl_vec("s", m);
-        decl_vec("z", m);
+        if (!park.count("z")) decl_vec("z", m);
 
         // ---- kkt_initialize (Auxilary.c:992-1089)
         ln("// setup: factor the KKT holding -I, solve for rhs [-c; b; h]");
@@ -484,7 +495,7 @@ struct Gen {
         }
         ln("const double sh = -lo;");
         for (long i = 0; i < m; i++) wr("s", i, "sh < 0 ? " + V("zi", i) + " : " + V("zi", i) + " + (1 + sh)");
-        for (long i = 0; i < m; i++) ln(V("z", i) + " = hi < 0 ? -" + V("zi", i) + " : -" + V("zi", i) + " + (1 + hi);");
+        for (long i = 0; i < m; i++) wr("z", i, "hi < 0 ? -" + V("zi", i) + " : -" + V("zi", i) + " + (1 + hi)");
         close();
 
         // ---- QP_SOLVE loop (qpSWIFT.c:502-602)
@@ -505,7 +516,7 @@ struct Gen {
             for (long j = 0; j < n; j++) ln("double " + V("rx", j) + " = " + V("t", j) + ";");
             for (long j = 0; j < n; j++)
                 for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1]; k++)
-                    ln(V("rx", j) + " = " + msub(V("rx", j), in("G", k), V("z", pl.G.ir[k])) + ";");
+                    ln(V("rx", j) + " = " + msub(V("rx", j), in("G", k), rd("z", pl.G.ir[k])) + ";");
             if (p)
                 for (long j = 0; j < n; j++)
                     for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++)
@@ -552,7 +563,7 @@ struct Gen {
                 for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1]; k++) {
                     std::string v = in("G", k);
                     long r = pl.G.ir[k];
-                    ln(V("rx", j) + " = " + msub(V("rx", j), v, V("z", r)) + ";");
+                    ln(V("rx", j) + " = " + msub(V("rx", j), v, rd("z", r)) + ";");
                     ln(V("rz", r) + " = " + msub(V("rz", r), v, rd("x", j)) + ";");
                 }
             if (p)
@@ -589,23 +600,26 @@ struct Gen {
         // lambda = sqrt(s.*z) (Auxilary.c:638-646) only ever enters squared, so the
         // fast kernel uses lambda^2 = s.*z directly (no sqrt).
         if (opt.exact) {
-            for (long i = 0; i < m; i++) ln("const double " + V("lam", i) + " = __builtin_sqrt(" + rd("s", i) + " * " + V("z", i) + ");");
+            for (long i = 0; i < m; i++) ln("const double " + V("lam", i) + " = __builtin_sqrt(" + rd("s", i) + " * " + rd("z", i) + ");");
             dot("mu2", m, "lam", "lam");
             ln("const double mu = mu2 / " + S(m) + ".0;");
         } else {
             ln("const double mu = st_mu;");
         }
         auto lam2 = [&](long i) {
-            return opt.exact ? "(" + V("lam", i) + " * " + V("lam", i) + ")" : "(" + rd("s", i) + " * " + V("z", i) + ")";
+            return opt.exact ? "(" + V("lam", i) + " * " + V("lam", i) + ")" : "(" + rd("s", i) + " * " + rd("z", i) + ")";
         };
         ln("const bool pc = sigma > a.sigma_d;");
         if (!opt.exact)
-            for (long i = 0; i < m; i++) ln("const double " + V("rz_", i) + " = qpb_rcp(" + V("z", i) + ");");
+            for (long i = 0; i < m; i++) {
+                if (park.count("rzi")) wr("rzi", i, "qpb_rcp(" + rd("z", i) + ")");
+                else ln("const double " + V("rzi", i) + " = qpb_rcp(" + rd("z", i) + ");");
+            }
 
         // updatekktmatrix: -s/z on the z diagonal (Auxilary.c:211-215)
         for (long i = 0; i < m; i++) {
-            if (opt.exact) ln("const double " + V("kd", i) + " = (-" + rd("s", i) + ") / " + V("z", i) + ";");
-            else ln("const double " + V("kd", i) + " = -" + rd("s", i) + " * " + V("rz_", i) + ";");
+            if (opt.exact) ln("const double " + V("kd", i) + " = (-" + rd("s", i) + ") / " + rd("z", i) + ";");
+            else ln("const double " + V("kd", i) + " = -" + rd("s", i) + " * " + rd("rzi", i) + ";");
         }
         begin_phase();
         factor(pl.K_loop);
@@ -636,9 +650,9 @@ struct Gen {
                 if (t < n) return rd("rx", t);
                 if (t < n + p) return rd("ry", t - n);
                 long i = t - n - p;
-                if (opt.exact) return "(" + rd("rz", i) + " - (" + V("ds", i) + " / " + V("z", i) + "))";
+                if (opt.exact) return "(" + rd("rz", i) + " - (" + V("ds", i) + " / " + rd("z", i) + "))";
                 if (pred) return "(" + rd("rz", i) + " + " + rd("s", i) + ")";
-                return "__builtin_fma(-" + V("cc", i) + ", " + V("rz_", i) + ", " + rd("rz", i) + " + " + rd("s", i) + ")";
+                return "__builtin_fma(-" + V("cc", i) + ", " + rd("rzi", i) + ", " + rd("rz", i) + " + " + rd("s", i) + ")";
             };
         };
         auto dsl_from_dz = [&](bool pred) {
@@ -646,12 +660,12 @@ struct Gen {
             for (long i = 0; i < m; i++) {
                 if (opt.exact) {
                     std::string num = V("ds", i) + " - (" + rd("s", i) + " * " + V("dz", i) + ")";
-                    ln(V("dsl", i) + " = (" + num + ") / " + V("z", i) + ";");
+                    ln(V("dsl", i) + " = (" + num + ") / " + rd("z", i) + ";");
                 } else if (pred) {
-                    ln(V("dsl", i) + " = -" + rd("s", i) + " * __builtin_fma(" + V("dz", i) + ", " + V("rz_", i) + ", 1.0);");
+                    ln(V("dsl", i) + " = -" + rd("s", i) + " * __builtin_fma(" + V("dz", i) + ", " + rd("rzi", i) + ", 1.0);");
                 } else {
                     ln(V("dsl", i) + " = __builtin_fma(__builtin_fma(-" + rd("s", i) + ", " + V("dz", i) + ", " + V("cc", i) +
-                       "), " + V("rz_", i) + ", -" + rd("s", i) + ");");
+                       "), " + rd("rzi", i) + ", -" + rd("s", i) + ");");
                 }
             }
         };
@@ -668,7 +682,7 @@ struct Gen {
         begin_phase(false, true);
         ln("double rho_n = 0.0;");
         for (long i = 0; i < m; i++)
-            ln("rho_n = rho_n + (" + rd("s", i) + " + (ap * " + V("dsl", i) + ")) * (" + V("z", i) + " + (ad * " + V("dz", i) + "));");
+            ln("rho_n = rho_n + (" + rd("s", i) + " + (ap * " + V("dsl", i) + ")) * (" + rd("z", i) + " + (ad * " + V("dz", i) + "));");
         ln("const double rho = rho_n / sz;");
         ln("const double r1 = 1 > rho ? rho : 1;");
         ln("const double cube = r1 * r1 * r1;");
@@ -694,7 +708,7 @@ struct Gen {
         for (long i = 0; i < n; i++) wr("x", i, madd(rd("x", i), V("dx", i), "ap"));
         for (long i = 0; i < p; i++) wr("y", i, madd(rd("y", i), V("dy", i), "ad"));
         for (long i = 0; i < m; i++) wr("s", i, madd(rd("s", i), V("dsl", i), "ap"));
-        for (long i = 0; i < m; i++) ln(V("z", i) + " = " + madd(V("z", i), V("dz", i), "ad") + ";");
+        for (long i = 0; i < m; i++) wr("z", i, madd(rd("z", i), V("dz", i), "ad"));
         ln("it++;");
         close();
         // outputs
@@ -745,7 +759,21 @@ GenOptions choose_options(const Plan &pl, bool exact) {
 
 std::string generate_kernel(const Plan &pl, const GenOptions &opt) {
     Gen g(pl, opt);
-    return g.build();
+    std::string src = g.build();
+    // The kernel (and code-object cache) name carries a hash of the generated
+    // source, so any change of the generator yields a new name.
+    const uint64_t h = fnv1a(src);
+    char suffix[32];
+    snprintf(suffix, sizeof suffix, "_%08llx", (unsigned long long)(h & 0xffffffffull));
+    const std::string name = kernel_name(pl, opt) + suffix;
+    for (size_t pos; (pos = src.find("QPB_KERNEL_NAME")) != std::string::npos;) src.replace(pos, 15, name);
+    return src;
+}
+
+std::string kernel_name_of(const std::string &src) {
+    size_t a = src.find("qpb_ipm_");
+    size_t b = src.find('(', a);
+    return src.substr(a, b - a);
 }
 
 }  // namespace qpb

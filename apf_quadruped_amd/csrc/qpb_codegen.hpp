@@ -39,5 +39,6 @@ std::string kernel_name(const Plan &pl, const GenOptions &opt);
 // input on-chip when it fits the 160 KiB LDS of a CU.
 GenOptions choose_options(const Plan &pl, bool exact);
 std::string generate_kernel(const Plan &pl, const GenOptions &opt);
+std::string kernel_name_of(const std::string &src);   // name inside generated source
 
 }  // namespace qpb

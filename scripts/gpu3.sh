@@ -1,0 +1,3 @@
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; echo "list rc=$?"
+timeout -k 10 600 python scripts/sweep.py --batch 1048576 --reps 5 --rounds 2 128:3 128:2 256:1 exact > gpurun_out/sweep.log 2> gpurun_out/sweep.err; echo "sweep rc=$?"

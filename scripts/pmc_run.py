@@ -1,0 +1,33 @@
+"""Small fixed workload for rocprofv3 PMC passes: solve B C1 QPs `reps` times
+with the kernel variant selected by QPB_WG / QPB_LDS (or --exact)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=262144)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--exact", action="store_true")
+    a = ap.parse_args()
+    import torch
+    from apf_quadruped_amd import plans
+    from apf_quadruped_amd.batch import Plan
+    import bench
+    torch.cuda.set_device(0)
+    d0 = plans.standard_qp("c1")
+    plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=a.exact)
+    vals = {k: torch.from_numpy(v).cuda() for k, v in bench.make_shard(plan, plans.SEED + 1, 0, a.batch).items()}
+    out = plan.solve(**vals, B=a.batch)
+    for _ in range(a.reps):
+        plan.solve(**vals, B=a.batch, out=out)
+    torch.cuda.synchronize()
+    print("iters", float(out["iters"].float().mean()))
+
+
+if __name__ == "__main__":
+    main()
