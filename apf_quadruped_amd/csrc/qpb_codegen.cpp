@@ -66,31 +66,31 @@ struct Gen {
                 for (long c = 0; c < N; c++) if (e >= pl.Lp[c] && e < pl.Lp[c + 1]) { j = c; break; }
                 if (leaf[j] && leaf_slot[e] < 0) leaf[j] = 0;          // not a pure scatter: keep L
             }
-            const long nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz(), nP = pl.Pin.nnz();
-            if (opt.lds_mode >= 1) {
-                lds_A = 0; lds_G = nA; lds_rows = nA + nG;
-                if (opt.lds_mode == 2 || opt.lds_mode == 4) { lds_P = lds_rows; lds_rows += nP; }
-                if (opt.lds_mode == 4) {      // every input on chip
-                    lds_c = lds_rows; lds_rows += pl.n;
-                    lds_h = lds_rows; lds_rows += pl.m;
-                    if (pl.p) { lds_b = lds_rows; lds_rows += pl.p; }
-                }
-                if (opt.lds_mode == 3 || opt.lds_mode == 4) {      // park the loop vectors too
-                    const long n = pl.n, p = pl.p, m = pl.m;
-                    park["x"] = lds_rows; lds_rows += n;
-                    if (p) { park["y"] = lds_rows; lds_rows += p; }
-                    park["rx"] = lds_rows; lds_rows += n;
-                    if (p) { park["ry"] = lds_rows; lds_rows += p; }
-                    park["rz"] = lds_rows; lds_rows += m;
-                    if ((lds_rows + m) * opt.wg * 8 <= 160 * 1024) { park["s"] = lds_rows; lds_rows += m; }
-                    if (opt.lds_mode == 4 && (lds_rows + 2 * m) * opt.wg * 8 <= 160 * 1024) {
-                        park["z"] = lds_rows; lds_rows += m;
-                        park["rzi"] = lds_rows; lds_rows += m;
-                    }
-                }
-                use_lds = lds_rows > 0 && lds_rows * opt.wg * 8 <= 160 * 1024;
-                if (!use_lds) { lds_A = lds_G = lds_P = lds_c = lds_h = lds_b = -1; park.clear(); }
+        }
+        const long nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz(), nP = pl.Pin.nnz();
+        if (opt.lds_mode >= 1) {
+            lds_A = 0; lds_G = nA; lds_rows = nA + nG;
+            if (opt.lds_mode == 2 || opt.lds_mode == 4) { lds_P = lds_rows; lds_rows += nP; }
+            if (opt.lds_mode == 4) {      // every input on chip
+                lds_c = lds_rows; lds_rows += pl.n;
+                lds_h = lds_rows; lds_rows += pl.m;
+                if (pl.p) { lds_b = lds_rows; lds_rows += pl.p; }
             }
+            if (opt.lds_mode == 3 || opt.lds_mode == 4) {      // park the loop vectors too
+                const long n = pl.n, p = pl.p, m = pl.m;
+                park["x"] = lds_rows; lds_rows += n;
+                if (p) { park["y"] = lds_rows; lds_rows += p; }
+                park["rx"] = lds_rows; lds_rows += n;
+                if (p) { park["ry"] = lds_rows; lds_rows += p; }
+                park["rz"] = lds_rows; lds_rows += m;
+                if ((lds_rows + m) * opt.wg * 8 <= 160 * 1024) { park["s"] = lds_rows; lds_rows += m; }
+                if (opt.lds_mode == 4 && opt.park_z && (lds_rows + 2 * m) * opt.wg * 8 <= 160 * 1024) {
+                    park["z"] = lds_rows; lds_rows += m;
+                    park["rzi"] = lds_rows; lds_rows += m;
+                }
+            }
+            use_lds = lds_rows > 0 && lds_rows * opt.wg * 8 <= 160 * 1024;
+            if (!use_lds) { lds_A = lds_G = lds_P = lds_c = lds_h = lds_b = -1; park.clear(); }
         }
     }
     long col_of(long e) const {
@@ -120,9 +120,14 @@ struct Gen {
         }
         if (lds && use_lds) {
             lph = ++lctr;
-            ln("int lt" + S(lph) + " = threadIdx.x; asm volatile(\"\" : \"+v\"(lt" + S(lph) + "));");
+            // one opaque base per 64 KiB window of the LDS image, so every access
+            // is base + 16-bit immediate (no per-access address arithmetic)
+            for (long w = 0; w * win_rows() < lds_rows; w++)
+                ln("int lt" + S(lph) + "_" + S(w) + " = threadIdx.x + " + S(w * win_rows() * opt.wg) +
+                   "; asm volatile(\"\" : \"+v\"(lt" + S(lph) + "_" + S(w) + "));");
         }
     }
+    long win_rows() const { return 65536 / (8 * opt.wg); }
     bool cached(const std::string &name) const {
         for (auto &sc : scopes)
             for (auto &nm : sc)
@@ -134,7 +139,10 @@ struct Gen {
             for (auto it = sc.begin(); it != sc.end();)
                 it = (it->compare(0, prefix.size(), prefix) == 0) ? sc.erase(it) : it + 1;
     }
-    std::string lds_at(long row) const { return "qpb_lds[" + S(row * opt.wg) + " + lt" + S(lph) + "]"; }
+    std::string lds_at(long row) const {
+        const long w = row / win_rows();
+        return "qpb_lds[" + S((row - w * win_rows()) * opt.wg) + " + lt" + S(lph) + "_" + S(w) + "]";
+    }
     std::string lds_st(long row) const { return "qpb_lds[" + S(row * opt.wg) + " + threadIdx.x]"; }
     // name of input value arr[j] for the current phase; emits its load on first use
     std::string in(const char *arr, long j) {
@@ -734,26 +742,30 @@ struct Gen {
 std::string kernel_name(const Plan &pl, const GenOptions &opt) {
     char buf[96];
     snprintf(buf, sizeof buf, "qpb_ipm_%016llx_%s_w%d_l%d", (unsigned long long)pl.hash, opt.exact ? "x" : "f",
-             opt.wg, opt.exact ? 0 : opt.lds_mode);
+             opt.wg, opt.lds_mode);
     return buf;
 }
 
 GenOptions choose_options(const Plan &pl, bool exact) {
+    // Measured on MI355X (profiles/): what costs is VMEM latency of
+    // spills and reloads, so keep the matrix values (P, A, G) on chip and then
+    // maximise waves per CU; all inputs + loop vectors on chip (mode 4) wins only
+    // at equal wave count.  LDS is 160 KiB per CU.
     GenOptions o;
     o.exact = exact;
-    o.wg = 256;
     o.waves_per_eu = 1;
-    o.lds_mode = 0;
-    if (exact) return o;
     const long nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz(), nP = pl.Pin.nnz();
-    const long cap = 160 * 1024 / 8;           // doubles of LDS per CU
-    const long vec = 2 * pl.n + 2 * pl.p + pl.m;  // parked loop vectors (mode 3)
-    if ((nA + nG + vec) * 256 <= cap) { o.lds_mode = 3; o.wg = 256; }
-    else if ((nA + nG + vec) * 128 <= cap) { o.lds_mode = 3; o.wg = 128; }
-    else if ((nP + nA + nG) * 256 <= cap) { o.lds_mode = 2; o.wg = 256; }
-    else if ((nP + nA + nG) * 128 <= cap) { o.lds_mode = 2; o.wg = 128; }
-    else if ((nA + nG) * 256 <= cap) { o.lds_mode = 1; o.wg = 256; }
-    else if ((nA + nG) * 128 <= cap) { o.lds_mode = 1; o.wg = 128; }
+    const long mats = nP + nA + nG;
+    const long all = mats + pl.n + pl.m + pl.p + (2 * pl.n + 2 * pl.p + 2 * pl.m);   // mode 4 rows (no z park)
+    const long cap = 160 * 1024 / 8;            // doubles of LDS per CU
+    struct Cand { int wg, mode; long rows; };
+    const Cand cands[] = {{256, 4, all}, {256, 2, mats}, {128, 4, all}, {128, 2, mats},
+                          {256, 1, nA + nG}, {64, 4, all}, {128, 1, nA + nG}};
+    o.wg = 256;
+    o.lds_mode = 0;
+    o.park_z = 0;
+    for (const Cand &c : cands)
+        if (c.rows > 0 && c.rows * c.wg <= cap) { o.wg = c.wg; o.lds_mode = c.mode; break; }
     return o;
 }
 

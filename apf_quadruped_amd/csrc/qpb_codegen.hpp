@@ -19,6 +19,7 @@ struct GenOptions {
     // Fast mode: which matrix inputs are staged in LDS (each lane owns a private
     // LDS column: no barriers).  0 = none, 1 = A and G, 2 = P, A and G.
     int lds_mode = 1;
+    int park_z = 1;           // mode 4: also keep z and 1/z in LDS
 };
 
 // Kernel argument block; identical layout in the generated device code.

@@ -193,6 +193,7 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     // experiment overrides (kernel name encodes them, so caches stay consistent)
     if (const char *e = getenv("QPB_WG")) plan->gen.wg = atoi(e);
     if (const char *e = getenv("QPB_LDS")) plan->gen.lds_mode = atoi(e);
+    if (const char *e = getenv("QPB_PARKZ")) plan->gen.park_z = atoi(e);
     plan->kname = qpb::kernel_name_of(qpb::generate_kernel(plan->pl, plan->gen));
     *out = plan.release();
     return QPB_OK;

@@ -39,12 +39,14 @@ def main():
             os.environ.pop("QPB_WG", None); os.environ.pop("QPB_LDS", None)
             plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=True)
         else:
-            wg, lds = v.split(":")
-            os.environ["QPB_WG"], os.environ["QPB_LDS"] = wg, lds
+            parts = v.split(":")
+            os.environ["QPB_WG"], os.environ["QPB_LDS"] = parts[0], parts[1]
+            os.environ["QPB_PARKZ"] = parts[2] if len(parts) > 2 else "1"
             plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0])
         t0 = time.time(); plans_[v].compile(); ct = time.time() - t0
         print(f"compiled {v} in {ct:.1f}s", file=sys.stderr)
-    os.environ.pop("QPB_WG", None); os.environ.pop("QPB_LDS", None)
+    for k in ("QPB_WG", "QPB_LDS", "QPB_PARKZ"):
+        os.environ.pop(k, None)
     from oracle_py import Oracle
     o = Oracle()
     ids = np.arange(0, a.batch, a.batch // 16)
