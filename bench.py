@@ -167,6 +167,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
+    traffic = None
+    kname = plan.source().split("(qpb_args")[0].split()[-1]
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        t = json.load(open(tfile)).get(kname)
+        if t and int(t.get("batch", -1)) == B:
+            traffic = float(t["hbm_bytes_per_launch"])
     flags = out["flag"].cpu().numpy()
     iters = out["iters"].cpu().numpy()
     mean_it = float(iters.mean())
@@ -220,8 +227,9 @@ def main():
                        "ordering": "own min-degree", "kkt_N": plan.info.N, "nnz_L": plan.info.lnz,
                        "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "bytes_per_qp": bpq, "kernel_ms": kern_ms},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": bpq * B, "bytes_per_qp": bpq,
+                         "kernel_ms": kern_ms, "kernel": kname},
             "fp64": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
                      "frac": fp64_tf / FP64_PEAK_TFLOPS, "flops_per_qp": fpq},
             "mean_iters": mean_it,
