@@ -66,36 +66,50 @@ void write_file(const std::string &path, const std::vector<char> &data) {
     rename(tmp.c_str(), path.c_str());
 }
 
-// Lowest fval among optimal QPs; one block, ties -> lowest index.
-__global__ void __launch_bounds__(1024) qpb_argmin_kernel(long B, const double *__restrict__ fval,
-                                                          const int *__restrict__ flag, double *__restrict__ out) {
+// Lowest fval among optimal QPs, ties -> lowest index.  Two stages: every
+// block reduces a contiguous chunk to one (fval, index) pair, then one block
+// reduces the pairs.  "better(a, b)": a is optimal and (lower fval, or equal
+// fval and lower index).
+__device__ __forceinline__ bool qpb_better(double va, long ia, double vb, long ib) {
+    return ia >= 0 && (ib < 0 || va < vb || (va == vb && ia < ib));
+}
+
+__device__ __forceinline__ void qpb_block_argmin(double &bv, long &bi) {
     __shared__ double sv[1024 / 64];
     __shared__ long si[1024 / 64];
-    double bv = INFINITY;
-    long bi = -1;
-    for (long q = threadIdx.x; q < B; q += blockDim.x) {
-        double v = fval[q];
-        if (flag[q] == 0 && (v < bv || (v == bv && (bi < 0 || q < bi)))) { bv = v; bi = q; }
-    }
     for (int off = 32; off > 0; off >>= 1) {
         double ov = __shfl_xor(bv, off, 64);
         long oi = __shfl_xor(bi, off, 64);
-        bool take = (oi >= 0) && (bi < 0 || ov < bv || (ov == bv && oi < bi));
-        bv = take ? ov : bv;
-        bi = take ? oi : bi;
+        if (qpb_better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
     }
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) { sv[w] = bv; si[w] = bi; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < (int)(blockDim.x >> 6); k++) {
-            bool take = (si[k] >= 0) && (bi < 0 || sv[k] < bv || (sv[k] == bv && si[k] < bi));
-            bv = take ? sv[k] : bv;
-            bi = take ? si[k] : bi;
-        }
-        out[0] = bv;
-        out[1] = (double)bi;
-    }
+    if (threadIdx.x == 0)
+        for (int k = 1; k < (int)(blockDim.x >> 6); k++)
+            if (qpb_better(sv[k], si[k], bv, bi)) { bv = sv[k]; bi = si[k]; }
+}
+
+__global__ void __launch_bounds__(256) qpb_argmin_partial(long B, long chunk, const double *__restrict__ fval,
+                                                          const int *__restrict__ flag, double *__restrict__ pv,
+                                                          long *__restrict__ pi) {
+    const long lo = (long)blockIdx.x * chunk, hi = lo + chunk < B ? lo + chunk : B;
+    double bv = INFINITY;
+    long bi = -1;
+    for (long q = lo + threadIdx.x; q < hi; q += blockDim.x)
+        if (flag[q] == 0 && qpb_better(fval[q], q, bv, bi)) { bv = fval[q]; bi = q; }
+    qpb_block_argmin(bv, bi);
+    if (threadIdx.x == 0) { pv[blockIdx.x] = bv; pi[blockIdx.x] = bi; }
+}
+
+__global__ void __launch_bounds__(1024) qpb_argmin_final(long nb, const double *__restrict__ pv,
+                                                         const long *__restrict__ pi, double *__restrict__ out) {
+    double bv = INFINITY;
+    long bi = -1;
+    for (long k = threadIdx.x; k < nb; k += blockDim.x)
+        if (qpb_better(pv[k], pi[k], bv, bi)) { bv = pv[k]; bi = pi[k]; }
+    qpb_block_argmin(bv, bi);
+    if (threadIdx.x == 0) { out[0] = bv; out[1] = (double)bi; }
 }
 
 }  // namespace
@@ -271,7 +285,23 @@ int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const do
 
 int qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *stream) {
     if (B < 0 || !out2 || (B > 0 && (!fval || !flag))) return fail(QPB_EINVAL, "bad argmin arguments");
-    hipLaunchKernelGGL(qpb_argmin_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, fval, flag, out2);
+    // partials live in a per-device scratch buffer (grown on demand, never freed)
+    static thread_local std::map<int, std::pair<void *, long>> scratch;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(QPB_EHIP, "hipGetDevice failed");
+    const long nb = std::max(1L, std::min(1024L, (B + 4095) / 4096));
+    const long chunk = (B + nb - 1) / nb;
+    auto &buf = scratch[dev];
+    if (buf.second < nb) {
+        if (buf.first) (void)hipFree(buf.first);
+        if (hipMalloc(&buf.first, (size_t)nb * 16) != hipSuccess) { buf = {nullptr, 0}; return fail(QPB_ENOMEM, "argmin scratch"); }
+        buf.second = nb;
+    }
+    double *pv = (double *)buf.first;
+    long *pi = (long *)((char *)buf.first + nb * 8);
+    hipLaunchKernelGGL(qpb_argmin_partial, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, B, chunk, fval, flag,
+                       pv, pi);
+    hipLaunchKernelGGL(qpb_argmin_final, dim3(1), dim3(1024), 0, (hipStream_t)stream, nb, pv, pi, out2);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("argmin: ") + hipGetErrorString(e));
     return QPB_OK;

@@ -15,18 +15,24 @@ import sys
 from collections import defaultdict
 
 
-def per_kernel(path, counter):
+def per_kernel(path, counter, batch):
+    """Mean counter value over the dispatches of `batch` QPs (grid == batch
+    rounded up to whole workgroups)."""
     vals = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and "qpb_ipm" in r["Kernel_Name"]:
-            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] != counter or "qpb_ipm" not in r["Kernel_Name"]:
+            continue
+        wg = int(r["Workgroup_Size"])
+        if int(r["Grid_Size"]) != (batch + wg - 1) // wg * wg:
+            continue
+        vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
 def main():
     fetch, write, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    f = per_kernel(fetch, "FETCH_SIZE")
-    w = per_kernel(write, "WRITE_SIZE")
+    f = per_kernel(fetch, "FETCH_SIZE", batch)
+    w = per_kernel(write, "WRITE_SIZE", batch)
     out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
     for k in f:
