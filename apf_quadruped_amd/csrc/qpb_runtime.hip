@@ -112,6 +112,15 @@ __global__ void __launch_bounds__(1024) qpb_argmin_final(long nb, const double *
     if (threadIdx.x == 0) { out[0] = bv; out[1] = (double)bi; }
 }
 
+// Strided segment copies dst[i * ds] = src[i * ss]; blockIdx.y selects the
+// segment.  Used by the single-QP drop-in to move packed host-order vectors in
+// and out of the tiled SoA layout with one H2D and one D2H transfer.
+__global__ void __launch_bounds__(256) qpb_strided_copy(qpb::CopySegs t) {
+    const qpb::CopySeg sg = t.seg[blockIdx.y];
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < sg.n; i += (long)gridDim.x * blockDim.x)
+        sg.dst[i * sg.ds] = sg.src[i * sg.ss];
+}
+
 }  // namespace
 
 namespace qpb {
@@ -177,6 +186,17 @@ int get_function(qpb_plan *plan, hipFunction_t *fn) {
 }
 
 int set_error(int code, const char *msg) { return fail(code, msg); }
+
+int strided_copy(const CopySegs &t, void *stream) {
+    if (t.nseg <= 0) return QPB_OK;
+    long mx = 1;
+    for (int i = 0; i < t.nseg; i++) mx = std::max(mx, t.seg[i].n);
+    const unsigned gx = (unsigned)std::min<long>(64, (mx + 255) / 256);
+    hipLaunchKernelGGL(qpb_strided_copy, dim3(gx, (unsigned)t.nseg), dim3(256), 0, (hipStream_t)stream, t);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(QPB_EHIP, std::string("strided copy: ") + hipGetErrorString(e));
+    return QPB_OK;
+}
 
 }  // namespace qpb
 

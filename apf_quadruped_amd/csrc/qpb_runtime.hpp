@@ -16,6 +16,17 @@ struct qpb_plan {
 };
 
 namespace qpb {
+struct CopySeg {
+    const double *src;
+    double *dst;
+    long n, ss, ds;   // element count, source stride, destination stride
+};
+struct CopySegs {
+    CopySeg seg[8];
+    int nseg;
+};
+// Device-side strided copies on `stream` (one launch for all segments).
+int strided_copy(const CopySegs &t, void *stream);
 int compile_plan(qpb_plan *plan);
 int set_error(int code, const char *msg);
 }  // namespace qpb

@@ -1,0 +1,515 @@
+// qpswift_dropin.cpp -- qpSWIFT's public API (include/qpSWIFT.h) on the gfx950
+// kernel: QP_SETUP, QP_SETUP_dense, QP_SOLVE, QP_CLEANUP, QP_CLEANUP_dense.
+//
+// Mirrors reference dogbot_controller/src/qpSWIFT/qpSWIFT.c:
+//   QP_SETUP          :60-234   (CSC inputs and c, h, b borrowed, caller sigma_d)
+//   QP_SETUP_dense    :260-456  (dense -> CSC copies dropping exact zeros,
+//                                Auxilary.c:1154-1273; sigma_d = 0)
+//   QP_SOLVE          :473-644
+//   QP_CLEANUP(_dense):661-839  (caller's Permut is never freed, AMD_RESULT -3)
+// The pattern work of setup (transposes, KKT layout, ordering, symbolic LDL') is
+// a cached qpb_plan; the value work (initial point, Mehrotra loop) runs on the
+// GPU inside QP_SOLVE as a batch of one.  There is deliberately no host solver
+// here: without a GPU, QP_SOLVE reports QP_FATAL.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/qpSWIFT.h"
+#include "../../include/qpswift_hip.h"
+#include "qpb_runtime.hpp"
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+
+double seconds_since(clk::time_point t0) {
+    return std::chrono::duration<double>(clk::now() - t0).count();
+}
+
+struct PlanDeleter {
+    void operator()(qpb_plan *p) const { qpb_plan_destroy(p); }
+};
+using PlanPtr = std::shared_ptr<qpb_plan>;
+
+// Plan cache keyed by the exact sparsity pattern + ordering: the controller
+// rebuilds its QP every tick with an unchanged pattern (main.cpp:1649), so after
+// the first tick setup is a hash lookup instead of AMD + symbolic + JIT.
+std::mutex g_cache_mu;
+std::map<std::string, PlanPtr> g_cache;
+constexpr size_t kCacheMax = 256;
+
+void key_append(std::string &k, const long *v, long n) {
+    if (n > 0 && v) k.append(reinterpret_cast<const char *>(v), sizeof(long) * (size_t)n);
+    k.push_back('|');
+}
+
+struct Priv {
+    PlanPtr plan;
+    std::string err;
+    bool dense = false;
+    // owned host storage (pointers in the public structs point here)
+    std::vector<long> Pjc, Pir, Ajc, Air, Gjc, Gir;
+    std::vector<double> Ppr, Apr, Gpr;
+    std::vector<long> Atjc, Atir, Gtjc, Gtir;
+    std::vector<double> Atpr, Gtpr;
+    std::vector<long> Kjc, Kir;
+    std::vector<double> Kpr;
+    std::vector<long> perm, pinv, parent, lnzc, Lp, Li, Lti, Ltp, kflag, pattern, upattern;
+    std::vector<double> kb, Y, Lx, D;
+    std::vector<double> x, y, z, s, rx, ry, rz, delta, dx, dy, dz, dsv, ds, lambda, temp;
+    smat Ps{}, As{}, Gs{}, Ats{}, Gts{}, Ks{};
+    kkt K{};
+    settings opt{};
+    stats st{};
+    // device state (allocated on the first QP_SOLVE)
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    double *dmem = nullptr;   // tiled inputs/outputs + packed staging
+    double *hmem = nullptr;   // pinned host staging: packed inputs, packed outputs
+    long nP = 0, nA = 0, nG = 0, nin = 0, nout = 0;
+    long oP = 0, oA = 0, oG = 0, oc = 0, oh = 0, ob = 0, ox = 0, oy = 0, oz = 0, os = 0, ost = 0, ofv = 0,
+         oin = 0, oout = 0, ototal = 0;
+};
+
+// Public struct first so that a QP* is also a Handle*.
+struct Handle {
+    QP qp;
+    Priv *priv;
+};
+
+Handle *handle_of(QP *q) { return reinterpret_cast<Handle *>(q); }
+
+// Auxilary.c:1154-1273: dense (column- or row-major) -> CSC, dropping exact zeros.
+void dense_to_csc(long rows, long cols, const double *a, bool rowmajor, std::vector<long> &jc,
+                  std::vector<long> &ir, std::vector<double> &pr) {
+    jc.assign((size_t)cols + 1, 0);
+    ir.clear();
+    pr.clear();
+    for (long j = 0; j < cols; j++) {
+        for (long i = 0; i < rows; i++) {
+            const double v = rowmajor ? a[i * cols + j] : a[j * rows + i];
+            if (v != 0.0) {
+                ir.push_back(i);
+                pr.push_back(v);
+            }
+        }
+        jc[(size_t)j + 1] = (long)ir.size();
+    }
+}
+
+// Counting-sort transpose (Auxilary.c:901-951 computes the same result).
+void csc_transpose(long rows, long cols, const long *jc, const long *ir, const double *pr, std::vector<long> &tjc,
+                   std::vector<long> &tir, std::vector<double> &tpr) {
+    const long nnz = jc[cols];
+    tjc.assign((size_t)rows + 1, 0);
+    tir.assign((size_t)nnz, 0);
+    tpr.assign((size_t)nnz, 0.0);
+    for (long k = 0; k < nnz; k++) tjc[(size_t)ir[k] + 1]++;
+    for (long i = 0; i < rows; i++) tjc[(size_t)i + 1] += tjc[(size_t)i];
+    std::vector<long> next(tjc.begin(), tjc.end() - 1);
+    for (long j = 0; j < cols; j++)
+        for (long k = jc[j]; k < jc[j + 1]; k++) {
+            const long d = next[(size_t)ir[k]]++;
+            tir[(size_t)d] = j;
+            tpr[(size_t)d] = pr ? pr[k] : 0.0;
+        }
+}
+
+void set_smat(smat &s, long rows, long cols, long *jc, long *ir, double *pr) {
+    s.jc = jc;
+    s.ir = ir;
+    s.pr = pr;
+    s.m = rows;
+    s.n = cols;
+    s.nnz = jc ? jc[cols] : 0;
+}
+
+double kkt_slot_value(const qpb::Slot &sl, const double *P, const double *A, const double *G, const double *s,
+                      const double *z) {
+    switch (sl.kind) {
+        case qpb::Src::P: return P[sl.idx];
+        case qpb::Src::A: return A[sl.idx];
+        case qpb::Src::G: return G[sl.idx];
+        case qpb::Src::NegOne: return -1.0;
+        case qpb::Src::ZDiag: return (s && z) ? -s[sl.idx] / z[sl.idx] : -1.0;
+    }
+    return 0.0;
+}
+
+PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const long *Ajc, const long *Air,
+                 const long *Gjc, const long *Gir, const long *perm, bool exact, std::string &err) {
+    std::string key;
+    const long hdr[5] = {n, m, p, exact ? 1L : 0L, perm ? 1L : 0L};
+    key_append(key, hdr, 5);
+    key_append(key, Pjc, n + 1);
+    key_append(key, Pir, Pjc[n]);
+    if (p > 0) {
+        key_append(key, Ajc, n + 1);
+        key_append(key, Air, Ajc[n]);
+    }
+    key_append(key, Gjc, n + 1);
+    key_append(key, Gir, Gjc[n]);
+    if (perm) key_append(key, perm, n + m + p);
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        auto it = g_cache.find(key);
+        if (it != g_cache.end()) return it->second;
+    }
+    qpb_plan *raw = nullptr;
+    int rc = qpb_plan_create(&raw, n, m, p, QPB_P_FULL | (exact ? QPB_EXACT : 0), Pjc, Pir, p > 0 ? Ajc : nullptr,
+                             p > 0 ? Air : nullptr, Gjc, Gir, perm);
+    if (rc) {
+        err = qpb_last_error();
+        return nullptr;
+    }
+    PlanPtr plan(raw, PlanDeleter());
+    if ((rc = qpb_plan_compile(raw)) != 0) {
+        err = qpb_last_error();
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    if (g_cache.size() >= kCacheMax) g_cache.clear();
+    g_cache.emplace(key, plan);
+    return plan;
+}
+
+// Everything of setup except the input conversion: transposes, plan, KKT
+// mirror, work vectors, public pointers.
+QP *finish_setup(Handle *hd, long *Permut, clk::time_point t0) {
+    QP &q = hd->qp;
+    Priv &v = *hd->priv;
+    const long n = q.n, m = q.m, p = q.p, N = n + m + p;
+
+    q.options = &v.opt;
+    q.stats = &v.st;
+    v.opt.maxit = MAXIT;
+    v.opt.reltol = RELTOL;
+    v.opt.abstol = ABSTOL;
+    v.opt.sigma = SIGMA;
+    v.opt.verbose = VERBOSE;
+    v.st.Flag = QP_FATAL;
+
+    csc_transpose(m, n, q.G->jc, q.G->ir, q.G->pr, v.Gtjc, v.Gtir, v.Gtpr);
+    set_smat(v.Gts, n, m, v.Gtjc.data(), v.Gtir.data(), v.Gtpr.data());
+    q.Gt = &v.Gts;
+    if (p > 0) {
+        csc_transpose(p, n, q.A->jc, q.A->ir, q.A->pr, v.Atjc, v.Atir, v.Atpr);
+        set_smat(v.Ats, n, p, v.Atjc.data(), v.Atir.data(), v.Atpr.data());
+        q.At = &v.Ats;
+    }
+
+    auto vec = [](std::vector<double> &b, long k) {
+        b.assign((size_t)std::max(k, 1L), 0.0);
+        return b.data();
+    };
+    q.x = vec(v.x, n);
+    q.y = p > 0 ? vec(v.y, p) : nullptr;
+    q.z = vec(v.z, m);
+    q.s = vec(v.s, m);
+    q.rx = vec(v.rx, n);
+    q.ry = p > 0 ? vec(v.ry, p) : nullptr;
+    q.rz = vec(v.rz, m);
+    q.delta = vec(v.delta, N);
+    q.delta_x = vec(v.dx, n);
+    q.delta_y = p > 0 ? vec(v.dy, p) : nullptr;
+    q.delta_z = vec(v.dz, m);
+    q.delta_s = vec(v.dsv, m);
+    q.ds = vec(v.ds, m);
+    q.lambda = vec(v.lambda, m);
+    q.temp = vec(v.temp, n);
+
+    const char *fast = getenv("QPSWIFT_HIP_FAST");
+    const bool exact = !(fast && *fast && *fast != '0');
+    v.plan = get_plan(n, m, p, q.P->jc, q.P->ir, p > 0 ? q.A->jc : nullptr, p > 0 ? q.A->ir : nullptr, q.G->jc,
+                      q.G->ir, Permut, exact, v.err);
+
+    q.kkt = &v.K;
+    v.st.AMD_RESULT = Permut ? -3 : 0;
+    if (v.plan) {
+        const qpb::Plan &pl = v.plan->pl;
+        v.Kjc.assign(pl.K.jc.begin(), pl.K.jc.end());
+        v.Kir.assign(pl.K.ir.begin(), pl.K.ir.end());
+        v.Kpr.resize(pl.K_init.size());
+        const double *Av = p > 0 ? q.A->pr : nullptr;
+        for (size_t k = 0; k < pl.K_init.size(); k++)
+            v.Kpr[k] = kkt_slot_value(pl.K_init[k], q.P->pr, Av, q.G->pr, nullptr, nullptr);
+        set_smat(v.Ks, N, N, v.Kjc.data(), v.Kir.data(), v.Kpr.data());
+        v.K.kktmatrix = &v.Ks;
+        v.perm.assign(pl.perm.begin(), pl.perm.end());
+        v.pinv.assign(pl.pinv.begin(), pl.pinv.end());
+        v.parent.assign(pl.parent.begin(), pl.parent.end());
+        v.Lp.assign(pl.Lp.begin(), pl.Lp.end());
+        v.Li.assign(pl.Li.begin(), pl.Li.end());
+        v.lnzc.assign((size_t)N, 0);
+        for (long k = 0; k < N; k++) v.lnzc[(size_t)k] = pl.Lp[(size_t)k + 1] - pl.Lp[(size_t)k];
+        v.K.P = Permut ? Permut : v.perm.data();
+        v.K.Pinv = v.pinv.data();
+        v.K.Parent = v.parent.data();
+        v.K.Lp = v.Lp.data();
+        v.K.Li = v.Li.data();
+        v.K.Lnz = v.lnzc.data();
+        const long lnz = std::max(pl.lnz, 1L);
+        v.Lx.assign((size_t)lnz, 0.0);
+        v.Lti.assign((size_t)lnz, 0);
+        v.Ltp.assign((size_t)N + 1, 0);
+        v.K.Lx = v.Lx.data();
+        v.K.Lti = v.Lti.data();
+        v.K.Ltp = v.Ltp.data();
+    }
+    v.kb.assign((size_t)N, 0.0);
+    v.Y.assign((size_t)N, 0.0);
+    v.D.assign((size_t)N, 0.0);
+    v.kflag.assign((size_t)N, 0);
+    v.pattern.assign((size_t)N, 0);
+    v.upattern.assign((size_t)N, 0);
+    v.K.b = v.kb.data();
+    v.K.Y = v.Y.data();
+    v.K.D = v.D.data();
+    v.K.Flag = v.kflag.data();
+    v.K.Pattern = v.pattern.data();
+    v.K.UPattern = v.upattern.data();
+    v.st.tsetup = seconds_since(t0);
+    return &q;
+}
+
+Handle *new_handle(long n, long m) {
+    Handle *hd = static_cast<Handle *>(std::calloc(1, sizeof(Handle)));
+    if (!hd) return nullptr;
+    hd->priv = new (std::nothrow) Priv();
+    if (!hd->priv) {
+        std::free(hd);
+        return nullptr;
+    }
+    hd->qp.n = n;
+    hd->qp.m = m;
+    return hd;
+}
+
+int ensure_device(Priv &v, const QP &q) {
+    if (v.dmem) return QPB_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return qpb::set_error(QPB_EHIP, "QP_SOLVE: no HIP device available (the drop-in has no CPU path)");
+    if (hipGetDevice(&v.dev) != hipSuccess) return qpb::set_error(QPB_EHIP, "hipGetDevice failed");
+    const long T = 64;   // one tile holds the single QP (lane 0)
+    v.nP = q.P->nnz;
+    v.nA = q.p > 0 ? q.A->nnz : 0;
+    v.nG = q.G->nnz;
+    long o = 0;
+    auto take = [&o](long k) { long r = o; o += std::max(k, 1L); return r; };
+    v.oP = take(v.nP * T); v.oA = take(v.nA * T); v.oG = take(v.nG * T);
+    v.oc = take(q.n * T); v.oh = take(q.m * T); v.ob = take(q.p * T);
+    v.ox = take(q.n * T); v.oy = take(q.p * T); v.oz = take(q.m * T); v.os = take(q.m * T);
+    v.ost = take(6 * T);
+    v.nin = v.nP + v.nA + v.nG + q.n + q.m + q.p;
+    v.nout = q.n + q.p + 2 * q.m + 6 + 1;   // x y z s stats fval
+    v.oin = take(v.nin);
+    v.oout = take(v.nout + 1);              // + flag, iters (two ints in one double slot)
+    v.ofv = v.oout + v.nout - 1;
+    v.ototal = o;
+    if (hipMalloc((void **)&v.dmem, sizeof(double) * (size_t)o) != hipSuccess) {
+        v.dmem = nullptr;
+        return qpb::set_error(QPB_ENOMEM, "QP_SOLVE: device allocation failed");
+    }
+    if (hipHostMalloc((void **)&v.hmem, sizeof(double) * (size_t)(v.nin + v.nout + 1), hipHostMallocDefault) !=
+        hipSuccess) {
+        v.hmem = nullptr;
+        return qpb::set_error(QPB_ENOMEM, "QP_SOLVE: pinned host allocation failed");
+    }
+    if (hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking) != hipSuccess)
+        return qpb::set_error(QPB_EHIP, "QP_SOLVE: stream creation failed");
+    return QPB_OK;
+}
+
+int solve_on_device(Priv &v, QP &q) {
+    int rc = ensure_device(v, q);
+    if (rc) return rc;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != v.dev) (void)hipSetDevice(v.dev);
+    const long n = q.n, m = q.m, p = q.p;
+    double *hin = v.hmem, *hout = v.hmem + v.nin;
+    double *w = hin;
+    auto put = [&w](const double *src, long k) {
+        if (k > 0) std::memcpy(w, src, sizeof(double) * (size_t)k);
+        w += k;
+    };
+    put(q.P->pr, v.nP);
+    if (p > 0) put(q.A->pr, v.nA);
+    put(q.G->pr, v.nG);
+    put(q.c, n);
+    put(q.h, m);
+    if (p > 0) put(q.b, p);
+    double *d = v.dmem;
+    hipError_t e = hipMemcpyAsync(d + v.oin, hin, sizeof(double) * (size_t)v.nin, hipMemcpyHostToDevice, v.stream);
+    qpb::CopySegs sc{};
+    long po = v.oin;
+    auto scatter = [&](long dst, long k) {
+        if (k <= 0) return;
+        sc.seg[sc.nseg++] = {d + po, d + dst, k, 1, 64};
+        po += k;
+    };
+    scatter(v.oP, v.nP);
+    scatter(v.oA, v.nA);
+    scatter(v.oG, v.nG);
+    scatter(v.oc, n);
+    scatter(v.oh, m);
+    scatter(v.ob, p);
+    if (e == hipSuccess) rc = qpb::strided_copy(sc, v.stream);
+    else rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: upload failed");
+    qpb_settings st;
+    st.maxit = q.options->maxit;
+    st.reltol = q.options->reltol;
+    st.abstol = q.options->abstol;
+    st.sigma_d = q.sigma_d;
+    int *fl = reinterpret_cast<int *>(d + v.oout + v.nout);
+    if (!rc)
+        rc = qpb_solve(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
+                       p > 0 ? d + v.ob : nullptr, &st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz, d + v.os,
+                       fl, fl + 1, d + v.ofv, d + v.ost, v.stream);
+    qpb::CopySegs gc{};
+    long qo = v.oout;
+    auto gather = [&](long src, long k, long ss) {
+        if (k <= 0) return;
+        gc.seg[gc.nseg++] = {d + src, d + qo, k, ss, 1};
+        qo += k;
+    };
+    gather(v.ox, n, 64);
+    gather(v.oy, p, 64);
+    gather(v.oz, m, 64);
+    gather(v.os, m, 64);
+    gather(v.ost, 6, 64);
+    if (!rc) rc = qpb::strided_copy(gc, v.stream);
+    if (!rc && hipMemcpyAsync(hout, d + v.oout, sizeof(double) * (size_t)(v.nout + 1), hipMemcpyDeviceToHost,
+                              v.stream) != hipSuccess)
+        rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: download failed");
+    if (hipStreamSynchronize(v.stream) != hipSuccess && !rc) rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: kernel failed");
+    if (cur != v.dev && cur >= 0) (void)hipSetDevice(cur);
+    if (rc) return rc;
+    const double *r = hout;
+    std::memcpy(q.x, r, sizeof(double) * (size_t)n); r += n;
+    if (p > 0) { std::memcpy(q.y, r, sizeof(double) * (size_t)p); r += p; }
+    std::memcpy(q.z, r, sizeof(double) * (size_t)m); r += m;
+    std::memcpy(q.s, r, sizeof(double) * (size_t)m); r += m;
+    v.st.n_rx = r[0]; v.st.n_ry = r[1]; v.st.n_rz = r[2]; v.st.n_mu = r[3];
+    v.st.alpha_p = r[4]; v.st.alpha_d = r[5];
+    r += 6;
+    v.st.fval = r[0];
+    int iv[2];
+    std::memcpy(iv, hout + v.nout, sizeof(iv));
+    v.st.Flag = iv[0];
+    v.st.IterationCount = iv[1];
+    q.mu = v.st.n_mu;
+    // KKT mirror: z-block diagonal as the last updatekktmatrix left it (Auxilary.c:205-233)
+    const qpb::Plan &pl = v.plan->pl;
+    const double *Av = p > 0 ? q.A->pr : nullptr;
+    for (size_t k = 0; k < pl.K_loop.size() && k < v.Kpr.size(); k++)
+        if (pl.K_loop[k].kind == qpb::Src::ZDiag && v.st.IterationCount > 0)
+            v.Kpr[k] = kkt_slot_value(pl.K_loop[k], q.P->pr, Av, q.G->pr, q.s, q.z);
+    return QPB_OK;
+}
+
+void release(QP *q) {
+    if (!q) return;
+    Handle *hd = handle_of(q);
+    Priv *v = hd->priv;
+    if (v) {
+        if (v->dmem || v->stream) {
+            int cur = -1;
+            (void)hipGetDevice(&cur);
+            if (v->dev >= 0 && cur != v->dev) (void)hipSetDevice(v->dev);
+            if (v->stream) (void)hipStreamSynchronize(v->stream);
+            if (v->dmem) (void)hipFree(v->dmem);
+            if (v->hmem) (void)hipHostFree(v->hmem);
+            if (v->stream) (void)hipStreamDestroy(v->stream);
+            if (cur >= 0 && cur != v->dev) (void)hipSetDevice(cur);
+        }
+        delete v;
+    }
+    std::free(hd);
+}
+
+}  // namespace
+
+extern "C" {
+
+QP *QP_SETUP(qp_int n, qp_int m, qp_int p, qp_int *Pjc, qp_int *Pir, qp_real *Ppr, qp_int *Ajc, qp_int *Air,
+             qp_real *Apr, qp_int *Gjc, qp_int *Gir, qp_real *Gpr, qp_real *c, qp_real *h, qp_real *b,
+             qp_real sigma_d, qp_int *Permut) {
+    const auto t0 = clk::now();
+    Handle *hd = new_handle(n, m);
+    if (!hd) return nullptr;
+    QP &q = hd->qp;
+    Priv &v = *hd->priv;
+    // qpSWIFT.c:91-104: the equality block exists only with all of A and b
+    if (Apr && Ajc && Air && b && p != 0) {
+        q.p = p;
+        set_smat(v.As, p, n, Ajc, Air, Apr);
+        q.A = &v.As;
+        q.b = b;
+    }
+    set_smat(v.Ps, n, n, Pjc, Pir, Ppr);
+    set_smat(v.Gs, m, n, Gjc, Gir, Gpr);
+    q.P = &v.Ps;
+    q.G = &v.Gs;
+    q.c = c;
+    q.h = h;
+    q.sigma_d = sigma_d;
+    return finish_setup(hd, Permut, t0);
+}
+
+QP *QP_SETUP_dense(qp_int n, qp_int m, qp_int p, qp_real *Ppr, qp_real *Apr, qp_real *Gpr, qp_real *c,
+                   qp_real *h, qp_real *b, qp_int *Permut, int ordering) {
+    const auto t0 = clk::now();
+    Handle *hd = new_handle(n, m);
+    if (!hd) return nullptr;
+    QP &q = hd->qp;
+    Priv &v = *hd->priv;
+    v.dense = true;
+    const bool rowmajor = ordering != COLUMN_MAJOR_ORDERING;   // qpSWIFT.c:296-303
+    if (Apr && b && p != 0) {
+        q.p = p;
+        dense_to_csc(p, n, Apr, rowmajor, v.Ajc, v.Air, v.Apr);
+        set_smat(v.As, p, n, v.Ajc.data(), v.Air.data(), v.Apr.data());
+        q.A = &v.As;
+        q.b = b;
+    }
+    dense_to_csc(n, n, Ppr, rowmajor, v.Pjc, v.Pir, v.Ppr);
+    dense_to_csc(m, n, Gpr, rowmajor, v.Gjc, v.Gir, v.Gpr);
+    set_smat(v.Ps, n, n, v.Pjc.data(), v.Pir.data(), v.Ppr.data());
+    set_smat(v.Gs, m, n, v.Gjc.data(), v.Gir.data(), v.Gpr.data());
+    q.P = &v.Ps;
+    q.G = &v.Gs;
+    q.c = c;
+    q.h = h;
+    q.sigma_d = 0.0;   // qpSWIFT.c:334
+    return finish_setup(hd, Permut, t0);
+}
+
+qp_int QP_SOLVE(QP *myQP) {
+    if (!myQP) return QP_FATAL;
+    const auto t0 = clk::now();
+    Priv &v = *handle_of(myQP)->priv;
+    int rc;
+    if (!v.plan) {
+        rc = qpb::set_error(QPB_ECOMPILE, ("QP_SOLVE: no kernel for this QP: " + v.err).c_str());
+    } else {
+        rc = solve_on_device(v, *myQP);
+    }
+    if (rc) v.st.Flag = QP_FATAL;
+    v.st.tsolve = seconds_since(t0);
+    return v.st.Flag;
+}
+
+void QP_CLEANUP(QP *myQP) { release(myQP); }
+void QP_CLEANUP_dense(QP *myQP) { release(myQP); }
+
+}  // extern "C"

@@ -1,0 +1,177 @@
+/*
+ * qpSWIFT.h -- source- and ABI-compatible replacement for qpSWIFT's public
+ * header, backed by the gfx950 interior-point kernel of libqpswift_hip.so.
+ *
+ * dogbot_controller includes "qpSWIFT/qpSWIFT.h" (src/client/main.cpp:12) and
+ * calls QP_SETUP_dense -> options override -> QP_SOLVE -> reads myQP->x
+ * (main.cpp:1649-1663).  This header declares the same five entry points
+ * (reference include/qpSWIFT/qpSWIFT.h:14-26) and the same structs with the same
+ * field order and types (reference include/qpSWIFT/Auxilary.h:18-151,
+ * qp_int = long and qp_real = double as in GlobalOptions.h:36-43), so the
+ * controller can be rebuilt against this header, or relinked against
+ * libqpswift_hip.so without recompiling.
+ *
+ * Behaviour (see INTEGRATION.md for the full list of differences):
+ *   QP_SETUP / QP_SETUP_dense  build the pattern plan (KKT layout, ordering,
+ *       elimination tree, generated kernel) on the host and cache it by sparsity
+ *       pattern; the matrices are converted exactly as the reference does
+ *       (dense -> CSC drops exact zeros).  No GPU work happens here.
+ *   QP_SOLVE  uploads the values, runs setup's initial point + the Mehrotra
+ *       loop in ONE kernel launch on the current HIP device, and copies x, y,
+ *       z, s and the statistics back.  There is no CPU fallback: without a
+ *       usable GPU it returns QP_FATAL and qpb_last_error() says why.
+ *   Arithmetic is the reference's operation order with IEEE division and no
+ *   FMA contraction (QPB_EXACT), so with the same permutation the results are
+ *   bit-identical to qpSWIFT.  With Permut == NULL the ordering is this
+ *   library's own minimum-degree ordering instead of SuiteSparse AMD (results
+ *   then agree to rounding, ~1e-12 relative).  Set QPSWIFT_HIP_FAST=1 in the
+ *   environment to use the FMA/reciprocal kernels instead.
+ */
+#ifndef QPSWIFT_HIP_DROPIN_H
+#define QPSWIFT_HIP_DROPIN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef qp_real
+#define qp_real double
+#endif
+#ifndef qp_int
+#define qp_int long
+#endif
+
+/* defaults (GlobalOptions.h:46-50) */
+#define MAXIT (100)
+#define RELTOL (1e-6)
+#define ABSTOL (1e-6)
+#define SIGMA (100)
+#define VERBOSE (0)
+
+/* exit flags (GlobalOptions.h:54-57) */
+#define QP_OPTIMAL (0)
+#define QP_KKTFAIL (1)
+#define QP_MAXIT (2)
+#define QP_FATAL (3)
+
+/* dense input storage order for QP_SETUP_dense (GlobalOptions.h:59-60) */
+#define ROW_MAJOR_ORDERING (20)
+#define COLUMN_MAJOR_ORDERING (30)
+
+/* compressed sparse column matrix: m rows, n columns (Auxilary.h:18-26) */
+typedef struct smat {
+    qp_int *jc;
+    qp_int *ir;
+    qp_real *pr;
+    qp_int n;
+    qp_int m;
+    qp_int nnz;
+} smat;
+
+/* KKT system (Auxilary.h:31-50).  Here the symbolic members (kktmatrix pattern
+ * and setup-time values, Parent, Lnz, Lp, Li, P, Pinv) are filled from the plan;
+ * the numeric factor lives on the GPU only, so Lx, D, Y, b are zero-filled
+ * buffers of the reference's sizes. */
+typedef struct kkt {
+    smat *kktmatrix;
+    qp_real *b;
+    qp_int *Parent;
+    qp_int *Flag;
+    qp_int *Lnz;
+    qp_int *Li;
+    qp_int *Lp;
+    qp_int *Lti;
+    qp_int *Ltp;
+    qp_int *Pattern;
+    qp_int *UPattern;
+    qp_real *Y;
+    qp_real *Lx;
+    qp_real *D;
+    qp_int *P;
+    qp_int *Pinv;
+} kkt;
+
+/* statistics (Auxilary.h:55-84) */
+typedef struct stats {
+    qp_real tsetup;
+    qp_real tsolve;
+    qp_real kkt_time;
+    qp_real ldl_numeric;
+    qp_int IterationCount;
+    qp_real n_rx;
+    qp_real n_ry;
+    qp_real n_rz;
+    qp_real n_mu;
+    qp_real alpha_p;
+    qp_real alpha_d;
+    qp_real fval;
+    qp_int Flag;
+    qp_int AMD_RESULT;
+    qp_int resolve_kkt;
+} stats;
+
+/* settings (Auxilary.h:89-100); verbose is accepted and ignored */
+typedef struct settings {
+    qp_int maxit;
+    qp_real reltol;
+    qp_real abstol;
+    qp_real sigma;
+    qp_int verbose;
+} settings;
+
+/* solver object (Auxilary.h:106-151) */
+typedef struct QP {
+    qp_int n;
+    qp_int m;
+    qp_int p;
+    qp_real sigma_d;
+    qp_real mu;
+    qp_real rho;
+    qp_real *x;
+    qp_real *y;
+    qp_real *z;
+    qp_real *s;
+    qp_real *rx;
+    qp_real *ry;
+    qp_real *rz;
+    qp_real *delta;
+    qp_real *delta_x;
+    qp_real *delta_y;
+    qp_real *delta_z;
+    qp_real *delta_s;
+    qp_real *ds;
+    qp_real *lambda;
+    qp_real *temp;
+    smat *P;
+    qp_real *c;
+    smat *G;
+    qp_real *h;
+    smat *A;
+    qp_real *b;
+    smat *At;
+    smat *Gt;
+    kkt *kkt;
+    settings *options;
+    stats *stats;
+} QP;
+
+/* qpSWIFT.h:14 -- CSC inputs (P full, both triangles), all borrowed */
+QP *QP_SETUP(qp_int n, qp_int m, qp_int p, qp_int *Pjc, qp_int *Pir, qp_real *Ppr,
+             qp_int *Ajc, qp_int *Air, qp_real *Apr, qp_int *Gjc, qp_int *Gir, qp_real *Gpr,
+             qp_real *c, qp_real *h, qp_real *b, qp_real sigma_d, qp_int *Permut);
+
+/* qpSWIFT.h:17 -- dense inputs (copied); c, h, b borrowed */
+QP *QP_SETUP_dense(qp_int n, qp_int m, qp_int p, qp_real *Ppr, qp_real *Apr, qp_real *Gpr,
+                   qp_real *c, qp_real *h, qp_real *b, qp_int *Permut, int ordering);
+
+/* qpSWIFT.h:20 */
+qp_int QP_SOLVE(QP *myQP);
+
+/* qpSWIFT.h:23,26 */
+void QP_CLEANUP(QP *myQP);
+void QP_CLEANUP_dense(QP *myQP);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

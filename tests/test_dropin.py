@@ -1,0 +1,219 @@
+"""The qpSWIFT drop-in (include/qpSWIFT.h): struct ABI, setup-side host logic and
+GPU parity through QP_SETUP_dense / QP_SETUP -> QP_SOLVE (the controller's call
+sequence, dogbot_controller/src/client/main.cpp:1649-1663).
+
+CPU tests: struct layout identical to the reference header, the KKT / ordering /
+elimination-tree mirror that setup fills in equals what reference qpSWIFT's own
+setup produces (oracle/_ref, only where /root/reference was available to build
+it), and QP_SOLVE fails loudly (QP_FATAL) when there is no GPU.
+GPU tests: given the reference's permutation the drop-in is BIT-IDENTICAL to the
+golden vectors; with Permut = NULL (own ordering) it is within 1e-6.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+
+from apf_quadruped_amd import _lib, dropin, qpswift_abi as abi
+
+REF_INC = "/root/reference/dogbot_controller/include"
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libqpswift_ref.so")
+
+LAYOUT_PROBE = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include HEADER
+#define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("QP %zu\nsettings %zu\nstats %zu\nkkt %zu\nsmat %zu\n", sizeof(QP), sizeof(settings),
+         sizeof(stats), sizeof(kkt), sizeof(smat));
+  F(QP, x) F(QP, y) F(QP, z) F(QP, s) F(QP, P) F(QP, c) F(QP, kkt) F(QP, options) F(QP, stats)
+  F(stats, IterationCount) F(stats, fval) F(stats, Flag) F(stats, AMD_RESULT) F(stats, resolve_kkt)
+  F(settings, reltol) F(settings, abstol) F(settings, verbose)
+  F(kkt, kktmatrix) F(kkt, Lp) F(kkt, P) F(kkt, Pinv) F(smat, nnz)
+  return 0;
+}
+"""
+
+
+def _layout(tmp_path, header, incdirs):
+    src = tmp_path / "probe.c"
+    src.write_text(LAYOUT_PROBE.replace("HEADER", f'"{header}"'))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-o", str(exe), str(src)] + [f"-I{d}" for d in incdirs], check=True)
+    return subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+
+
+def test_struct_layout_matches_ctypes_mirror(tmp_path):
+    got = dict(l.split() for l in _layout(tmp_path, os.path.join(ROOT, "include", "qpSWIFT.h"), []).splitlines())
+    assert int(got["QP"]) == C.sizeof(abi.QP)
+    assert int(got["stats"]) == C.sizeof(abi.stats)
+    assert int(got["settings"]) == C.sizeof(abi.settings)
+    assert int(got["kkt"]) == C.sizeof(abi.kkt)
+    for key, val in got.items():
+        if "." in key:
+            t, f = key.split(".")
+            assert getattr(getattr(abi, t), f).offset == int(val), key
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_INC), reason="reference headers not present (GPU box)")
+def test_struct_layout_matches_reference_header(tmp_path):
+    ours = _layout(tmp_path, os.path.join(ROOT, "include", "qpSWIFT.h"), [])
+    ref = _layout(tmp_path, "qpSWIFT/qpSWIFT.h", [REF_INC, os.path.join(REF_INC, "qpSWIFT")])
+    assert ours == ref
+
+
+def _golden_dense_args(g, q):
+    n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
+    return (n, m, p, g["P"][q], g["A"][q] if p else None, g["G"][q], g["c"][q], g["h"][q],
+            g["b"][q] if p else None)
+
+
+def _arr(ptr, k, dt=np.int64):
+    return np.ctypeslib.as_array(ptr, (k,)).astype(dt).copy()
+
+
+def _setup_mirror(L, qp, n, m, p):
+    q = qp.contents
+    k = q.kkt.contents
+    N = n + m + q.p
+    K = k.kktmatrix.contents
+    nnz = int(K.jc[N])
+    out = dict(p=q.p, Kjc=_arr(K.jc, N + 1), Kir=_arr(K.ir, nnz), Kpr=_arr(K.pr, nnz, np.float64),
+               perm=_arr(k.P, N), Pinv=_arr(k.Pinv, N), Parent=_arr(k.Parent, N), Lp=_arr(k.Lp, N + 1),
+               Pjc=_arr(q.P.contents.jc, n + 1), Gjc=_arr(q.G.contents.jc, n + 1),
+               Gtjc=_arr(q.Gt.contents.jc, m + 1), amd=int(q.stats.contents.AMD_RESULT),
+               flag=int(q.stats.contents.Flag), maxit=int(q.options.contents.maxit),
+               reltol=float(q.options.contents.reltol), sigma=float(q.options.contents.sigma))
+    nG = int(out["Gjc"][-1])
+    out["Gtir"] = _arr(q.Gt.contents.ir, nG)
+    out["Gtpr"] = _arr(q.Gt.contents.pr, nG, np.float64)
+    if q.p:
+        out["Atjc"] = _arr(q.At.contents.jc, q.p + 1)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_rowmajor", "c1_noeq", "mixed_trot_blfr", "edge_zero_g_row"])
+def test_setup_mirror_equals_reference_setup(name):
+    """Our QP_SETUP_dense fills the KKT CSC (values as assembled), ordering, Pinv,
+    elimination tree, Lp and the transposes exactly as the reference's setup does."""
+    g = golden(name)
+    args = _golden_dense_args(g, 0)
+    n, m, p = args[:3]
+    keep = [None if a is None else np.ascontiguousarray(a, dtype=np.float64) for a in args[3:]]
+    perm = np.ascontiguousarray(g["perm"][0], dtype=np.int64)
+    ordering = int(g["ordering"])
+    R = abi.bind_qpswift(C.CDLL(REF_SO))
+    L = _lib.lib()
+    mirrors = []
+    for lib in (R, L):
+        qp = lib.QP_SETUP_dense(n, m, p, *[abi.dptr(a) for a in keep], abi.lptr(perm), ordering)
+        mirrors.append(_setup_mirror(lib, qp, n, m, p))
+        lib.QP_CLEANUP_dense(qp)
+    ref, ours = mirrors
+    assert ref.keys() == ours.keys()
+    for key in ref:
+        assert np.array_equal(np.asarray(ref[key]), np.asarray(ours[key])), key
+
+
+def test_setup_own_ordering_fills_perm_and_amd_result():
+    g = golden("c1_tol1e-6")
+    qp, keep = dropin.setup_dense(*_golden_dense_args(g, 0))
+    q = qp.contents
+    N = 38
+    perm = _arr(q.kkt.contents.P, N)
+    assert sorted(perm.tolist()) == list(range(N))
+    assert q.stats.contents.AMD_RESULT == 0 and q.stats.contents.Flag == abi.QP_FATAL
+    assert int(q.kkt.contents.Lp[N]) > 0
+    _lib.lib().QP_CLEANUP_dense(qp)
+
+
+def _no_gpu():
+    try:
+        import torch
+        return not torch.cuda.is_available()
+    except Exception:
+        return True
+
+
+@pytest.mark.skipif(not _no_gpu(), reason="checks the no-GPU failure mode")
+def test_solve_without_gpu_fails_loudly():
+    g = golden("c1_tol1e-6")
+    r = dropin.solve_dense(*_golden_dense_args(g, 0), perm=g["perm"][0])
+    assert r["flag"] == abi.QP_FATAL
+    assert "no HIP device" in r["error"]
+
+
+# ---------------------------------------------------------------- GPU parity
+
+DENSE = ["c1_tol1e-6", "c1_tol1e-2", "c1_rowmajor", "c1_noeq", "edge_zero_g_row", "mixed_stance4",
+         "mixed_trot_blfr", "mixed_crawl_blflfr", "c1_maxit0", "c1_maxit2", "c1_maxit5"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", DENSE)
+def test_dropin_dense_bit_identical_to_reference(name):
+    g = golden(name)
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    for q in range(0, g["x"].shape[0], 7):
+        r = dropin.solve_dense(*_golden_dense_args(g, q), perm=g["perm"][q], ordering=int(g["ordering"]),
+                               reltol=tol, abstol=tol, maxit=maxit)
+        assert r["flag"] == int(g["flag"][q]), r["error"]
+        assert r["iters"] == int(g["iters"][q])
+        for k in ("x", "z", "s"):
+            assert np.array_equal(r[k], g[k][q]), (name, q, k)
+        if int(g["p"]):
+            assert np.array_equal(r["y"], g["y"][q]), (name, q, "y")
+        assert r["fval"] == float(g["fval"][q])
+        assert r["amd_result"] == -3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["csc_sigma0", "csc_sigma0.05"])
+def test_dropin_csc_bit_identical_to_reference(name):
+    g = golden(name)
+    n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    for q in range(g["x"].shape[0]):
+        r = dropin.solve_csc(n, m, p, g["Pjc"], g["Pir"], g["Ppr"][q], g["Ajc"], g["Air"], g["Apr"][q],
+                             g["Gjc"], g["Gir"], g["Gpr"][q], g["c"][q], g["h"][q], g["b"][q],
+                             sigma_d=float(g["sigma_d"]), perm=g["perm"][q], reltol=tol, abstol=tol, maxit=maxit)
+        assert r["flag"] == int(g["flag"][q]), r["error"]
+        assert r["iters"] == int(g["iters"][q])
+        for k in ("x", "y", "z", "s"):
+            assert np.array_equal(r[k], g[k][q]), (name, q, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "mixed_trot_brfl"])
+def test_dropin_controller_call_own_ordering(name):
+    """Permut = NULL as main.cpp:1649 passes it: own ordering, within 1e-6."""
+    g = golden(name)
+    tol = float(g["tol"])
+    for q in range(0, g["x"].shape[0], 5):
+        r = dropin.solve_dense(*_golden_dense_args(g, q), ordering=int(g["ordering"]), reltol=tol, abstol=tol)
+        assert r["flag"] == int(g["flag"][q]), r["error"]
+        scale = max(1.0, float(np.abs(g["x"][q]).max()))
+        assert np.abs(r["x"] - g["x"][q]).max() <= 1e-6 * scale
+        assert np.abs(r["z"] - g["z"][q]).max() <= 1e-6 * max(1.0, float(np.abs(g["z"][q]).max()))
+
+
+@pytest.mark.gpu
+def test_dropin_reuses_qp_and_plan_cache():
+    """Solving the same QP object twice and many QPs of one pattern (plan cache)."""
+    g = golden("c1_tol1e-6")
+    L = _lib.lib()
+    qp, keep = dropin.setup_dense(*_golden_dense_args(g, 3), perm=g["perm"][3])
+    f1 = L.QP_SOLVE(qp)
+    x1 = np.ctypeslib.as_array(qp.contents.x, (12,)).copy()
+    f2 = L.QP_SOLVE(qp)
+    x2 = np.ctypeslib.as_array(qp.contents.x, (12,)).copy()
+    L.QP_CLEANUP_dense(qp)
+    assert f1 == f2 == 0 and np.array_equal(x1, x2) and np.array_equal(x1, g["x"][3])
+    t = [dropin.solve_dense(*_golden_dense_args(g, q), perm=g["perm"][q])["tsetup"] for q in range(8)]
+    assert max(t[1:]) < 0.05   # cached plan: no ordering / JIT after the first setup
