@@ -21,6 +21,8 @@ from . import _lib
 from ._lib import QpbPlanInfo, QpbSettings, check
 
 QPB_P_FULL, QPB_P_UPPER, QPB_EXACT = 0x0, 0x1, 0x10
+QPB_KERNEL_LANE, QPB_KERNEL_WAVE = 0x100, 0x200
+KERNEL_FLAGS = {"auto": 0, "lane": QPB_KERNEL_LANE, "wave": QPB_KERNEL_WAVE}
 QP_OPTIMAL, QP_KKTFAIL, QP_MAXIT, QP_FATAL = 0, 1, 2, 3
 
 
@@ -83,7 +85,7 @@ class Patterns:
 class Plan:
     """One sparsity pattern (+ KKT ordering) and its generated gfx950 kernel."""
 
-    def __init__(self, n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=None, p_upper=True, exact=False):
+    def __init__(self, n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=None, p_upper=True, exact=False, kernel="auto"):
         L = _lib.lib()
         self.n, self.m, self.p = int(n), int(m), int(p)
         self.p_upper, self.exact = bool(p_upper), bool(exact)
@@ -93,7 +95,8 @@ class Plan:
         self.patterns = Patterns((Pjc, Pir), (Ajc, Air), (Gjc, Gir))
         lp = lambda a: None if a is None else a.ctypes.data_as(C.POINTER(C.c_long))
         h = C.c_void_p()
-        flags = (QPB_P_UPPER if p_upper else QPB_P_FULL) | (QPB_EXACT if exact else 0)
+        flags = (QPB_P_UPPER if p_upper else QPB_P_FULL) | (QPB_EXACT if exact else 0) | KERNEL_FLAGS[kernel]
+        self.kernel = kernel
         check(L.qpb_plan_create(C.byref(h), self.n, self.m, self.p, flags, lp(Pjc), lp(Pir),
                                 lp(Ajc) if self.p else None, lp(Air) if self.p else None,
                                 lp(Gjc), lp(Gir), lp(perm)), "qpb_plan_create")
@@ -111,12 +114,13 @@ class Plan:
             self._h = None
 
     @classmethod
-    def from_dense(cls, n, m, p, P, A, G, perm=None, p_upper=True, exact=False):
-        """Plan for the non-zero pattern of one dense QP (P [n,n], A [p,n], G [m,n])."""
+    def from_dense(cls, n, m, p, P, A, G, perm=None, p_upper=True, exact=False, kernel="auto"):
+        """Plan for the non-zero pattern of one dense QP (P [n,n], A [p,n], G [m,n]).
+        kernel: "auto" (wave kernel for small batches when eligible), "lane", "wave"."""
         Pjc, Pir = dense_pattern(P, upper=p_upper)
         Ajc, Air = dense_pattern(A) if p else (None, None)
         Gjc, Gir = dense_pattern(G)
-        return cls(n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=perm, p_upper=p_upper, exact=exact)
+        return cls(n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=perm, p_upper=p_upper, exact=exact, kernel=kernel)
 
     # -- inspection ---------------------------------------------------------
     def source(self) -> str:
@@ -124,6 +128,32 @@ class Plan:
         size = L.qpb_plan_source(self._h, None, 0)
         buf = C.create_string_buffer(size + 1)
         L.qpb_plan_source(self._h, buf, size + 1)
+        return buf.value.decode()
+
+    def wave_perm(self) -> np.ndarray:
+        """KKT elimination order of the wave kernel: all z rows, all y rows, then x
+        (KKT index order x, y, z as in Auxilary.c:71-181).  The oracle run with
+        this permutation is the wave kernel's arithmetic reference."""
+        n, m, p = self.n, self.m, self.p
+        return np.concatenate([np.arange(n + p, n + p + m), np.arange(n, n + p), np.arange(n)]).astype(np.int64)
+
+    def kernel_for(self, B: int) -> str:
+        """Which kernel qpb_solve runs for a batch of B ("wave" or "lane")."""
+        i = self.info
+        if i.wave_ok and (i.wave_max_batch < 0 or B <= i.wave_max_batch):
+            return "wave"
+        return "lane"
+
+    def oracle_perm(self, B: int) -> np.ndarray:
+        """The elimination order the kernel used for a batch of B runs in."""
+        return self.wave_perm() if self.kernel_for(B) == "wave" else self.perm
+
+    def wave_source(self) -> str:
+        L = _lib.lib()
+        size = L.qpb_plan_wave_source(self._h, None, 0)
+        check(0 if size >= 0 else int(size), "qpb_plan_wave_source")
+        buf = C.create_string_buffer(size + 1)
+        L.qpb_plan_wave_source(self._h, buf, size + 1)
         return buf.value.decode()
 
     def compile(self) -> None:
@@ -216,6 +246,56 @@ class Plan:
                                    ptr(out["flag"]), ptr(out["iters"]), ptr(out["fval"]),
                                    ptr(out.get("stats")), C.c_void_p(stream.cuda_stream)), "qpb_solve")
         return out
+
+
+    def launcher(self, vals, out, B, reltol=1e-6, abstol=1e-6, maxit=100, sigma_d=0.0, stream=None):
+        """A zero-argument callable that launches qpb_solve on fixed device buffers
+        with every C argument pre-built: one ctypes call per launch, so a Python
+        loop of launches stays GPU-bound even for small batches."""
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        ptr = lambda a: None if a is None else C.c_void_p(a.data_ptr())
+        st = QpbSettings(int(maxit), float(reltol), float(abstol), float(sigma_d))
+        args = (self._h, int(B), ptr(vals["P"]), ptr(vals.get("A")) if self.p else None, ptr(vals["G"]),
+                ptr(vals["c"]), ptr(vals["h"]), ptr(vals.get("b")) if self.p else None, C.byref(st),
+                ptr(out["x"]), ptr(out["y"]) if self.p else None, ptr(out["z"]), ptr(out["s"]),
+                ptr(out["flag"]), ptr(out["iters"]), ptr(out["fval"]), ptr(out.get("stats")),
+                C.c_void_p(stream.cuda_stream))
+        fn = _lib.lib().qpb_solve
+        keep = (vals, out, st)
+
+        def go():
+            rc = fn(*args)
+            if rc:
+                check(rc, "qpb_solve")
+        go.keep = keep
+        return go
+
+    def kernel_name(self, B: int) -> str:
+        """Name of the kernel qpb_solve launches for a batch of B."""
+        src = self.wave_source() if self.kernel_for(B) == "wave" else self.source()
+        for line in src.splitlines():
+            if line.startswith("#define QPB_KERNEL_NAME "):
+                return line.split()[-1]
+        return src.split("(qpb_args")[0].split()[-1]
+
+
+def argmin_launcher(fval, flag, out, stream=None):
+    """Pre-built qpb_argmin launch (see Plan.launcher)."""
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream(fval.device)
+    fn = _lib.lib().qpb_argmin
+    args = (int(fval.numel()), C.c_void_p(fval.data_ptr()), C.c_void_p(flag.data_ptr()),
+            C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream))
+
+    def go():
+        rc = fn(*args)
+        if rc:
+            check(rc, "qpb_argmin")
+    go.keep = (fval, flag, out)
+    return go
 
 
 def argmin(fval, flag, out=None, stream=None):

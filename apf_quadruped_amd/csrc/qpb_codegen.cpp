@@ -55,9 +55,8 @@ struct Gen {
             for (long e = 0; e < pl.lnz; e++) leaf[pl.Li[e]] = 0;     // row Li[e] has an entry
             leaf_slot.assign(pl.lnz, -1);
             std::vector<long> scat(N, -1);
-            long k = 0;
             for (const FacStep &st : pl.fac) {
-                if (st.op == FacOp::RowBegin) { k = st.a; std::fill(scat.begin(), scat.end(), -1); }
+                if (st.op == FacOp::RowBegin) std::fill(scat.begin(), scat.end(), -1);
                 else if (st.op == FacOp::Scatter) scat[st.a] = st.b;
                 else if (st.op == FacOp::NewL && leaf[st.a]) leaf_slot[st.b] = scat[st.a];
             }

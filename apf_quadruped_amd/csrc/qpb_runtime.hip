@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -21,6 +22,7 @@
 #include "qpb_codegen.hpp"
 #include "qpb_plan.hpp"
 #include "qpb_runtime.hpp"
+#include "qpb_wave.hpp"
 
 namespace {
 
@@ -125,25 +127,27 @@ __global__ void __launch_bounds__(256) qpb_strided_copy(qpb::CopySegs t) {
 
 namespace qpb {
 
-int compile_plan(qpb_plan *plan) {
-    if (plan->code) return QPB_OK;
+// Compile (hiprtc, gfx950) or fetch from the memory / disk cache.
+int compile_kernel(const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
+                   std::shared_ptr<std::vector<char>> *out) {
+    if (*out) return QPB_OK;
     std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_code.find(plan->kname);
-    if (it != g_code.end()) { plan->code = it->second; return QPB_OK; }
+    auto it = g_code.find(kname);
+    if (it != g_code.end()) { *out = it->second; return QPB_OK; }
     const std::string dir = cache_dir();
-    const std::string path = dir + "/" + plan->kname + ".hsaco";
+    const std::string path = dir + "/" + kname + ".hsaco";
     auto code = std::make_shared<std::vector<char>>();
     if (!getenv("QPB_NO_DISK_CACHE") && read_file(path, *code)) {
-        g_code[plan->kname] = code;
-        plan->code = code;
+        g_code[kname] = code;
+        *out = code;
         return QPB_OK;
     }
-    std::string src = generate_kernel(plan->pl, plan->gen);
+    std::string src = gen_src();
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), (plan->kname + ".hip").c_str(), 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+    if (hiprtcCreateProgram(&prog, src.c_str(), (kname + ".hip").c_str(), 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         return fail(QPB_ECOMPILE, "hiprtcCreateProgram failed");
     std::vector<const char *> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    if (plan->gen.exact) opts.push_back("-ffp-contract=off");
+    if (exact) opts.push_back("-ffp-contract=off");
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t ls = 0;
@@ -160,25 +164,35 @@ int compile_plan(qpb_plan *plan) {
     hiprtcDestroyProgram(&prog);
     mkdir(dir.c_str(), 0755);
     write_file(path, *code);
-    g_code[plan->kname] = code;
-    plan->code = code;
+    g_code[kname] = code;
+    *out = code;
     return QPB_OK;
 }
 
-int get_function(qpb_plan *plan, hipFunction_t *fn) {
-    int rc = compile_plan(plan);
-    if (rc) return rc;
+int compile_plan(qpb_plan *plan) {
+    return compile_kernel(plan->kname, [plan] { return generate_kernel(plan->pl, plan->gen); }, plan->gen.exact,
+                          &plan->code);
+}
+
+int compile_wave(qpb_plan *plan) {
+    if (!plan->wave_ok) return fail(QPB_EINVAL, "plan is not eligible for the wave kernel");
+    return compile_kernel(plan->wave_kname,
+                          [plan] { return generate_wave_kernel(plan->pl, plan->wave_wg, nullptr); }, false,
+                          &plan->wave_code);
+}
+
+int load_function(const std::string &kname, const std::shared_ptr<std::vector<char>> &code, hipFunction_t *fn) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return fail(QPB_EHIP, "hipGetDevice failed (no GPU?)");
     std::lock_guard<std::mutex> lk(g_mu);
-    auto key = std::make_pair(dev, plan->kname);
+    auto key = std::make_pair(dev, kname);
     auto it = g_funcs.find(key);
     if (it != g_funcs.end()) { *fn = it->second.second; return QPB_OK; }
     hipModule_t mod;
-    hipError_t e = hipModuleLoadData(&mod, plan->code->data());
+    hipError_t e = hipModuleLoadData(&mod, code->data());
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("hipModuleLoadData: ") + hipGetErrorString(e));
     hipFunction_t f;
-    e = hipModuleGetFunction(&f, mod, plan->kname.c_str());
+    e = hipModuleGetFunction(&f, mod, kname.c_str());
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
     g_funcs[key] = {mod, f};
     *fn = f;
@@ -229,6 +243,16 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     if (const char *e = getenv("QPB_LDS")) plan->gen.lds_mode = atoi(e);
     if (const char *e = getenv("QPB_PARKZ")) plan->gen.park_z = atoi(e);
     plan->kname = qpb::kernel_name_of(qpb::generate_kernel(plan->pl, plan->gen));
+    // wave-cooperative kernel: fast mode only (its elimination order differs
+    // from the reference's), for plans whose KKT has the z/y-leaf structure
+    std::string why;
+    plan->wave_ok = !plan->gen.exact && qpb::wave_eligible(plan->pl, &why);
+    plan->kernel_pref = (flags & QPB_KERNEL_WAVE) ? 2 : (flags & QPB_KERNEL_LANE) ? 1 : 0;
+    if (plan->kernel_pref == 2 && !plan->wave_ok)
+        return fail(QPB_EINVAL, "QPB_KERNEL_WAVE: " + (plan->gen.exact ? std::string("exact plans use the lane kernel") : why));
+    plan->wave_max_batch = 4096;   // measured crossover vs the lane kernel
+    if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
+    if (plan->wave_ok) qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
     *out = plan.release();
     return QPB_OK;
 }
@@ -244,6 +268,8 @@ int qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info) {
     info->fac_updates = pl.fac_updates; info->fac_divs = pl.fac_divs;
     info->ordering = pl.ordering_kind; info->exact = plan->gen.exact ? 1 : 0;
     info->hash = pl.hash;
+    info->wave_ok = plan->wave_ok ? 1 : 0;
+    info->wave_max_batch = plan->kernel_pref == 1 ? 0 : plan->kernel_pref == 2 ? -1 : plan->wave_max_batch;
     return QPB_OK;
 }
 
@@ -264,9 +290,23 @@ long qpb_plan_source(const qpb_plan *plan, char *buf, long cap) {
     return (long)s.size();
 }
 
+long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    if (!plan->wave_ok) return fail(QPB_EINVAL, "plan is not eligible for the wave kernel");
+    std::string s = qpb::generate_wave_kernel(plan->pl, plan->wave_wg, nullptr);
+    if (buf && cap > 0) {
+        long k = std::min<long>(cap - 1, (long)s.size());
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (long)s.size();
+}
+
 int qpb_plan_compile(qpb_plan *plan) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
-    return qpb::compile_plan(plan);
+    int rc = plan->kernel_pref == 2 ? QPB_OK : qpb::compile_plan(plan);
+    if (!rc && plan->wave_ok && plan->kernel_pref != 1) rc = qpb::compile_wave(plan);
+    return rc;
 }
 
 int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
@@ -280,8 +320,13 @@ int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const do
     if (!P || !G || !c || !h || !x || !z || !s || !flag || !iters || !fval)
         return fail(QPB_EINVAL, "NULL data pointer");
     if (pl.p > 0 && (!A || !b || !y)) return fail(QPB_EINVAL, "p > 0 needs A, b and y");
+    // kernel choice: the wave kernel (one QP per wavefront) has the lower latency
+    // and wins while the batch does not fill the GPU with lane-kernel waves
+    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 || (plan->kernel_pref == 0 && B <= plan->wave_max_batch));
     hipFunction_t fn;
-    int rc = qpb::get_function(plan, &fn);
+    int rc = wave ? qpb::compile_wave(plan) : qpb::compile_plan(plan);
+    if (!rc) rc = wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
+                       : qpb::load_function(plan->kname, plan->code, &fn);
     if (rc) return rc;
     qpb_settings def;
     qpb_default_settings(&def);
@@ -296,8 +341,9 @@ int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const do
     a.sigma_d = st->sigma_d;
     a.maxit = st->maxit;
     void *params[] = {&a};
-    const unsigned wg = (unsigned)plan->gen.wg;
-    const unsigned grid = (unsigned)((B + wg - 1) / wg);
+    const unsigned wg = (unsigned)(wave ? plan->wave_wg : plan->gen.wg);
+    const long per_block = wave ? wg / 64 : wg;    // QPs per workgroup
+    const unsigned grid = (unsigned)((B + per_block - 1) / per_block);
     hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, wg, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("launch: ") + hipGetErrorString(e));
     return QPB_OK;

@@ -11,8 +11,14 @@
 struct qpb_plan {
     qpb::Plan pl;
     qpb::GenOptions gen;
-    std::string kname;
+    std::string kname;                          // lane kernel (one QP per lane)
     std::shared_ptr<std::vector<char>> code;
+    bool wave_ok = false;                       // wave kernel (one QP per wavefront)
+    int wave_wg = 256;
+    long wave_max_batch = 0;                    // auto: wave kernel for B <= this
+    int kernel_pref = 0;                        // 0 auto, 1 lane only, 2 wave only
+    std::string wave_kname;
+    std::shared_ptr<std::vector<char>> wave_code;
 };
 
 namespace qpb {
@@ -28,5 +34,6 @@ struct CopySegs {
 // Device-side strided copies on `stream` (one launch for all segments).
 int strided_copy(const CopySegs &t, void *stream);
 int compile_plan(qpb_plan *plan);
+int compile_wave(qpb_plan *plan);
 int set_error(int code, const char *msg);
 }  // namespace qpb

@@ -1,0 +1,508 @@
+// qpb_wave.hip -- wave-cooperative IPM kernel: ONE wavefront per QP.
+//
+// Template source: compiled at run time with hiprtc after the host prepends the
+// plan's sizes (QPB_NX = n, QPB_NZ = m, QPB_NY = p), its sparsity tables and the
+// kernel name (qpb_wave.cpp).  Algorithm = qpSWIFT's Mehrotra predictor-corrector
+// (qpSWIFT.c:473-644, kkt_initialize Auxilary.c:992-1089) with the KKT LDL'
+// (ldl.c:253-326, same regularisation) in the elimination order
+//     [ all z rows | all y rows | x rows ]
+// z and y rows are leaves: their pivots are the diagonal (-s/z, and 0 -> -1e-7
+// for y, exactly the reference's regularisation), and their elimination adds
+//     H = P + G' diag(z/s) G + 1e7 A'A
+// onto the x block, which is factored densely.  Lanes own rows: lane i holds
+// x_i and row i of H (then of L), lane r holds s_r, z_r, lane l holds y_l.
+// Cross-lane traffic: whole vectors are all-gathered through LDS (one store,
+// wide same-address loads); the sequential dense factor / triangular solves
+// broadcast with DPP row_newbcast (x block within one 16-lane row) or
+// v_readlane beyond 16 rows; reductions are DPP row reductions.  Results agree
+// with the reference to rounding (fast mode: FMA contraction, reciprocal pivots).
+#pragma clang fp contract(fast)
+
+template <int V> struct qpb_ic { static constexpr int value = V; };
+
+struct qpb_args {
+    const double *P, *A, *G, *c, *h, *b;
+    double *x, *y, *z, *s;
+    int *flag, *iters;
+    double *fval;
+    double *stats;
+    long B;
+    double tol, abstol, sigma_d;
+    long maxit;
+};
+
+// tuning knobs (defaults = measured best; scripts/sweep.py "wave:KNOB=V,...")
+#ifndef QPB_W_GG
+#define QPB_W_GG 1        // 1: G(r,i)G(r,j) products in registers; 0: recompute from LDS
+#endif
+#ifndef QPB_W_PROW
+#define QPB_W_PROW 1      // 1: this lane's row of P in registers; 0: read from LDS
+#endif
+#ifndef QPB_W_TIMING
+#define QPB_W_TIMING 0    // 1: phase timestamps (s_memtime) of QP 0 of each tile into stats (debug)
+#endif
+#ifndef QPB_W_SPLIT
+#define QPB_W_SPLIT 1     // independent partial sums per long accumulation (ILP)
+#endif
+
+#define NX QPB_NX
+#define NZ QPB_NZ
+#define NY QPB_NY
+#define NY1 (NY > 0 ? NY : 1)
+#define WPB (QPB_WG / 64)
+#define NV (NX + NZ + NY)
+#define NV2 ((NV + 1) & ~1)
+// per-wave LDS (doubles): Pd[NX*NX] Ad[NY*NX] Gd[NZ*NX] c[NX] h[NZ] b[NY] | Tx[NX*NX] | V[NV2]
+#define OFF_A (NX * NX)
+#define OFF_G (OFF_A + NY * NX)
+#define OFF_C (OFF_G + NZ * NX)
+#define OFF_H (OFF_C + NX)
+#define OFF_B (OFF_H + NZ)
+#define OFF_T (((OFF_B + NY) + 1) & ~1)
+#define OFF_V (OFF_T + ((NX * NX + 1) & ~1))
+#define LDS_WAVE (OFF_V + NV2)
+#define ROWS_X ((NX + 15) / 16)
+#define ROWS_Z ((NZ + 15) / 16)
+#define ROWS_Y ((NY1 + 15) / 16)
+
+static __device__ __forceinline__ double qpb_rcp(double v) {
+    double r = __builtin_amdgcn_rcp(v);
+    double e = __builtin_fma(-v, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-v, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+// value of lane l (l wave-uniform) in every lane, through an SGPR pair
+static __device__ __forceinline__ double qpb_bc(double v, int l) {
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// value of lane J of the x block in every lane that uses it: one DPP
+// row_newbcast when the x block fits one 16-lane row, else v_readlane
+template <int J> static __device__ __forceinline__ double qpb_xb(double v) {
+    if constexpr (NX <= 16) return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
+    else return qpb_bc(v, J);
+}
+
+template <int CTRL> static __device__ __forceinline__ double qpb_dpp(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, CTRL, 0xf, 0xf, true);
+}
+
+// sums / maxima over the first R 16-lane rows (result wave-uniform); lanes
+// outside the data range must contribute 0 (sum) or a neutral value (max)
+template <int R> static __device__ __forceinline__ double qpb_rsum(double v) {
+    v += qpb_dpp<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += qpb_dpp<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += qpb_dpp<0x141>(v);   // row_half_mirror
+    v += qpb_dpp<0x140>(v);   // row_mirror
+    double r = qpb_bc(v, 0);
+#pragma unroll
+    for (int k = 1; k < R; k++) r += qpb_bc(v, 16 * k);
+    return r;
+}
+template <int R> static __device__ __forceinline__ double qpb_rmax(double v) {
+    v = __builtin_fmax(v, qpb_dpp<0xB1>(v));
+    v = __builtin_fmax(v, qpb_dpp<0x4E>(v));
+    v = __builtin_fmax(v, qpb_dpp<0x141>(v));
+    v = __builtin_fmax(v, qpb_dpp<0x140>(v));
+    double r = qpb_bc(v, 0);
+#pragma unroll
+    for (int k = 1; k < R; k++) r = __builtin_fmax(r, qpb_bc(v, 16 * k));
+    return r;
+}
+
+// LDS is shared by the lanes of one wave only: in-order per wave, so a compiler
+// fence is all that is needed between a store by one lane and a load by another.
+static __device__ __forceinline__ void qpb_wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ldl.c:273-274, 319-320
+static __device__ __forceinline__ double qpb_regularise(double d) {
+    const double sg = d <= 0.0 ? -1.0 : 1.0;
+    return sg * d <= 1e-14 ? sg * 1e-7 : d;
+}
+
+// 1 / regularise(d): v_rcp_f64 + one Newton step, computed unconditionally (the
+// asm keeps the compiler from turning the rare regularised case into a branch);
+// |d| <= 1e-14 -> 1/(+-1e-7), sign as ldl.c:273 (d <= 0 -> negative, NaN kept)
+static __device__ __forceinline__ double qpb_rcp_reg(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    asm volatile("" : "+v"(r));
+    const double reg = d > 0.0 ? 1e7 : -1e7;
+    return __builtin_fabs(d) <= 1e-14 ? reg : r;
+}
+
+template <int J0, int J1, class F> static __device__ __forceinline__ void qpb_for(F &&f) {
+    if constexpr (J0 < J1) {
+        f(qpb_ic<J0>{});
+        qpb_for<J0 + 1, J1>(f);
+    }
+}
+
+#if QPB_W_TIMING
+#define QPB_TS(k)                                                                      \
+    do {                                                                               \
+        if (ql == 0 && a.stats && (k) < 384) {                                         \
+            const double t_ = (double)__builtin_readcyclecounter();                    \
+            if (lane == 0) a.stats[tile * 384 + (k)] = t_;                             \
+        }                                                                              \
+    } while (0)
+#else
+#define QPB_TS(k) do { } while (0)
+#endif
+
+extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
+    __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * LDS_WAVE];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long q = (long)blockIdx.x * WPB + wv;
+    if (q >= a.B) return;                    // wave-uniform
+    double *__restrict__ Ls = qpb_lds + wv * LDS_WAVE;
+    const long tile = q >> 6;
+    const int ql = (int)(q & 63);
+    const bool isx = lane < NX, isz = lane < NZ, isy = lane < NY;
+    const int ix = isx ? lane : NX - 1;
+    const int iz = isz ? lane : NZ - 1;
+    const int iy = isy ? lane : (NY > 0 ? NY - 1 : 0);
+    constexpr double RDY = 1.0 / -1e-7;      // y pivots: D = 0 regularised to -1e-7
+
+    QPB_TS(0);
+    // ---- stage this QP's inputs as dense matrices in LDS (tiled SoA -> dense):
+    // every global load is issued before the first LDS store
+    constexpr int NPL = (QPB_NNZP + 63) / 64, NGL = (QPB_NNZG + 63) / 64, NAL = (QPB_NNZA + 63) / 64;
+    double vP[NPL], vG[NGL], vA[NAL > 0 ? NAL : 1];
+    int iP[NPL], iP2[NPL], iG[NGL], iA[NAL > 0 ? NAL : 1];
+    {
+        const double *tP = a.P + tile * (QPB_NNZP * 64) + ql;
+        const double *tG = a.G + tile * (QPB_NNZG * 64) + ql;
+#pragma unroll
+        for (int u = 0; u < NPL; u++) {
+            const int k = lane + 64 * u;
+            const bool ok = k < QPB_NNZP;
+            vP[u] = ok ? tP[k * 64] : 0.0;
+            iP[u] = ok ? qpb_scP[k] : -1;
+            iP2[u] = ok ? qpb_scP2[k] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < NGL; u++) {
+            const int k = lane + 64 * u;
+            const bool ok = k < QPB_NNZG;
+            vG[u] = ok ? tG[k * 64] : 0.0;
+            iG[u] = ok ? qpb_scG[k] : -1;
+        }
+#if NY > 0
+        const double *tA = a.A + tile * (QPB_NNZA * 64) + ql;
+#pragma unroll
+        for (int u = 0; u < NAL; u++) {
+            const int k = lane + 64 * u;
+            const bool ok = k < QPB_NNZA;
+            vA[u] = ok ? tA[k * 64] : 0.0;
+            iA[u] = ok ? qpb_scA[k] : -1;
+        }
+#endif
+    }
+    const double cx0 = isx ? a.c[tile * (NX * 64) + lane * 64 + ql] : 0.0;
+    const double hz0 = isz ? a.h[tile * (NZ * 64) + lane * 64 + ql] : 0.0;
+#if NY > 0
+    const double by0 = isy ? a.b[tile * (NY * 64) + lane * 64 + ql] : 0.0;
+#endif
+#pragma unroll
+    for (int k = lane; k < OFF_C; k += 64) Ls[k] = 0.0;
+    qpb_wsync();
+#pragma unroll
+    for (int u = 0; u < NPL; u++) {
+        if (iP[u] >= 0) Ls[iP[u]] = vP[u];
+        if (iP2[u] >= 0) Ls[iP2[u]] = vP[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NGL; u++)
+        if (iG[u] >= 0) Ls[OFF_G + iG[u]] = vG[u];
+#pragma unroll
+    for (int u = 0; u < NAL; u++)
+        if (iA[u] >= 0) Ls[OFF_A + iA[u]] = vA[u];
+    qpb_wsync();
+    const double *Pd = Ls, *Ad = Ls + OFF_A, *Gd = Ls + OFF_G;
+    double *Tx = Ls + OFF_T, *Vb = Ls + OFF_V;
+    // Pd[j*NX+i] = P(i,j) as given; Ad[j*NY+l] = A(l,j); Gd[j*NZ+r] = G(r,j)
+    const double cx = cx0, hz = hz0;
+#if NY > 0
+    const double by = by0;
+#else
+    const double by = 0.0;
+#endif
+    // this lane's slices of the (constant) matrices, kept in registers
+    double Prow[NX], Grow[NX], Arow[NX], Gcol[NZ], Acol[NY1], H0[NX];
+#pragma unroll
+    for (int j = 0; j < NX; j++) {
+        Prow[j] = QPB_W_PROW ? Pd[j * NX + ix] : 0.0;      // P(i, j), residual (full P)
+        Grow[j] = Gd[j * NZ + iz];                         // G(r, j)
+        Arow[j] = NY > 0 ? Ad[j * NY + iy] : 0.0;          // A(l, j)
+    }
+#pragma unroll
+    for (int r = 0; r < NZ; r++) Gcol[r] = Gd[ix * NZ + r];   // G(r, i)
+#pragma unroll
+    for (int l = 0; l < NY1; l++) Acol[l] = NY > 0 ? Ad[ix * NY + l] : 0.0;   // A(l, i)
+    // H0 = P(upper, symmetrised) + 1e7 A'A: the y leaves (ldl.c:303-318 for x rows)
+#pragma unroll
+    for (int j = 0; j < NX; j++) {
+        double v = ix <= j ? Pd[j * NX + ix] : Pd[ix * NX + j];
+#pragma unroll
+        for (int l = 0; l < NY; l++) v = __builtin_fma(Acol[l], -RDY * Ad[j * NY + l], v);
+        H0[j] = v;
+    }
+    // G(r,i) G(r,j) for every structural G(r,j): the z leaves' updates of row i
+    double GG[QPB_W_GG ? QPB_NNZG : 1];
+    if (QPB_W_GG) {
+        int e = 0;
+#pragma unroll
+        for (int r = 0; r < NZ; r++)
+#pragma unroll
+            for (int j = 0; j < NX; j++)
+                if (qpb_Gnz[r][j]) GG[QPB_W_GG ? e++ : 0] = Gcol[r] * Gd[j * NZ + r];
+    }
+
+    // every lane gets the vector held by lanes 0..K-1 (one LDS store, wide loads)
+    auto gather = [&](double v, auto kc, int off, double *out) {
+        constexpr int K = decltype(kc)::value;
+        if (lane < K) Vb[off + lane] = v;
+        qpb_wsync();
+#pragma unroll
+        for (int k = 0; k < K; k++) out[k] = Vb[off + k];
+        qpb_wsync();
+    };
+
+    double H[NX], Lt[NX], rDx = 0.0, w = 0.0;
+    // factor: H = H0 + G' diag(w) G, then dense LDL' of H (right-looking)
+    auto factor = [&](double wz) {
+        w = wz;
+        double wb[NZ];
+        gather(wz, qpb_ic<NZ>{}, 0, wb);
+#pragma unroll
+        for (int j = 0; j < NX; j++) H[j] = H0[j];
+        {
+            int e = 0;
+#pragma unroll
+            for (int r = 0; r < NZ; r++)
+#pragma unroll
+                for (int j = 0; j < NX; j++)
+                    if (qpb_Gnz[r][j]) {
+                        if (QPB_W_GG) H[j] = __builtin_fma(GG[e], wb[r], H[j]);
+                        else H[j] = __builtin_fma(Gcol[r] * wb[r], Gd[j * NZ + r], H[j]);
+                        e++;
+                    }
+        }
+        qpb_for<0, NX>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const double rd = qpb_rcp_reg(qpb_xb<k>(H[k]));
+            rDx = lane == k ? rd : rDx;
+            const double l = H[k] * rd;
+            qpb_for<k + 1, NX>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                H[j] = __builtin_fma(-l, qpb_xb<j>(H[k]), H[j]);
+            });
+            H[k] = lane > k ? l : 0.0;        // L(i,k) below the diagonal, 0 elsewhere
+        });
+        // transpose L through LDS: lane j gets column j (0 on and above the diagonal)
+        if (isx) {
+#pragma unroll
+            for (int j = 0; j < NX; j++) Tx[lane * NX + j] = H[j];
+        }
+        qpb_wsync();
+#pragma unroll
+        for (int k = 0; k < NX; k++) Lt[k] = Tx[k * NX + ix];
+        qpb_wsync();
+    };
+
+    // solve K [dx; dy; dz] = [bx; byv; bz] with the current factor
+    auto solve = [&](double bx, double byv, double bz, double &dx, double &dy, double &dz) {
+        double vb[NZ + NY1];
+        if (lane < NZ) Vb[lane] = w * bz;             // -bz / D_z
+        if (lane < NY) Vb[NZ + lane] = -RDY * byv;    // -by / D_y
+        qpb_wsync();
+#pragma unroll
+        for (int k = 0; k < NZ + NY; k++) vb[k] = Vb[k];
+        qpb_wsync();
+        double ta[QPB_W_SPLIT];
+#pragma unroll
+        for (int k = 0; k < QPB_W_SPLIT; k++) ta[k] = k ? 0.0 : bx;
+#pragma unroll
+        for (int r = 0; r < NZ; r++) ta[r % QPB_W_SPLIT] = __builtin_fma(Gcol[r], vb[r], ta[r % QPB_W_SPLIT]);
+#pragma unroll
+        for (int l = 0; l < NY; l++)
+            ta[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(Acol[l], vb[NZ + l], ta[(NZ + l) % QPB_W_SPLIT]);
+        double t = ta[0];
+#pragma unroll
+        for (int k = 1; k < QPB_W_SPLIT; k++) t += ta[k];
+        qpb_for<0, NX>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            t = __builtin_fma(-H[k], qpb_xb<k>(t), t);
+        });
+        t *= rDx;
+        qpb_for<0, NX>([&](auto kc) {
+            constexpr int k = NX - 1 - decltype(kc)::value;
+            t = __builtin_fma(-Lt[k], qpb_xb<k>(t), t);
+        });
+        dx = t;
+        double xb[NX];
+        gather(t, qpb_ic<NX>{}, 0, xb);
+        double gza[QPB_W_SPLIT], gya[QPB_W_SPLIT];
+#pragma unroll
+        for (int k = 0; k < QPB_W_SPLIT; k++) gza[k] = gya[k] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; j++) {
+            gza[j % QPB_W_SPLIT] = __builtin_fma(Grow[j], xb[j], gza[j % QPB_W_SPLIT]);
+            gya[j % QPB_W_SPLIT] = __builtin_fma(Arow[j], xb[j], gya[j % QPB_W_SPLIT]);
+        }
+        double gz = gza[0], gy = gya[0];
+#pragma unroll
+        for (int k = 1; k < QPB_W_SPLIT; k++) { gz += gza[k]; gy += gya[k]; }
+        dz = -w * (bz - gz);
+        dy = RDY * (byv - gy);
+    };
+
+    QPB_TS(1);
+    // ---- kkt_initialize (Auxilary.c:992-1089): K with -I, rhs [-c; b; h]
+    factor(1.0);
+    QPB_TS(2);
+    double x, y, s, z;
+    {
+        double dzi;
+        solve(-cx, by, hz, x, y, dzi);
+        QPB_TS(3);
+        double xb[NX];
+        gather(x, qpb_ic<NX>{}, 0, xb);
+        double gx = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; j++) gx = __builtin_fma(Grow[j], xb[j], gx);
+        const double zi = hz - gx;
+        const double lo = -qpb_rmax<ROWS_Z>(isz ? -zi : -1e300);
+        const double hi = qpb_rmax<ROWS_Z>(isz ? zi : -1e300);
+        const double sh = -lo;
+        s = sh < 0 ? zi : zi + (1 + sh);
+        z = hi < 0 ? -zi : -zi + (1 + hi);
+        if (!isz) { s = 1.0; z = 1.0; }
+        if (!isx) x = 0.0;
+        if (!isy) y = 0.0;
+    }
+
+    // ---- QP_SOLVE loop (qpSWIFT.c:502-602)
+    long it = 0;
+    int flag = 3;
+    double fval = 0.0, st_rx = 0.0, st_ry = 0.0, st_rz = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;
+    double sigma = 100.0;
+    QPB_TS(4);
+    for (;;) {
+        if (it >= a.maxit) { flag = 2; break; }
+        QPB_TS(8 + 8 * it);
+        // residuals (Auxilary.c:745-786), objective (Auxilary.c:1133-1141)
+        double vb[NV];
+        if (lane < NX) Vb[lane] = x;
+        if (lane < NZ) Vb[NX + lane] = z;
+        if (lane < NY) Vb[NX + NZ + lane] = y;
+        qpb_wsync();
+#pragma unroll
+        for (int k = 0; k < NV; k++) vb[k] = Vb[k];
+        qpb_wsync();
+        double tp = 0.0, ry = by, rz = hz - s, rx = -cx;
+#pragma unroll
+        for (int j = 0; j < NX; j++) {
+            tp = __builtin_fma(-(QPB_W_PROW ? Prow[j] : Pd[j * NX + ix]), vb[j], tp);
+            rz = __builtin_fma(-Grow[j], vb[j], rz);
+            ry = __builtin_fma(-Arow[j], vb[j], ry);
+        }
+        {
+            double ra[QPB_W_SPLIT];
+#pragma unroll
+            for (int k = 0; k < QPB_W_SPLIT; k++) ra[k] = k ? 0.0 : rx;
+#pragma unroll
+            for (int r = 0; r < NZ; r++) ra[r % QPB_W_SPLIT] = __builtin_fma(-Gcol[r], vb[NX + r], ra[r % QPB_W_SPLIT]);
+#pragma unroll
+            for (int l = 0; l < NY; l++)
+                ra[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(-Acol[l], vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
+            rx = ra[0];
+#pragma unroll
+            for (int k = 1; k < QPB_W_SPLIT; k++) rx += ra[k];
+        }
+        rx += tp;
+        fval = qpb_rsum<ROWS_X>(isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0);
+        st_rx = __builtin_sqrt(qpb_rsum<ROWS_X>(isx ? rx * rx : 0.0));
+        st_ry = NY > 0 ? __builtin_sqrt(qpb_rsum<ROWS_Y>(isy ? ry * ry : 0.0)) : 0.0;
+        st_rz = __builtin_sqrt(qpb_rsum<ROWS_Z>(isz ? rz * rz : 0.0));
+        const double sz = qpb_rsum<ROWS_Z>(isz ? s * z : 0.0);
+        st_mu = sz * (1.0 / NZ);
+        if (st_rx < a.tol && st_rz < a.tol && (NY == 0 || st_ry < a.tol) && st_mu < a.abstol) { flag = 0; break; }
+        QPB_TS(9 + 8 * it);
+        const double mu = st_mu;
+        const bool pc = sigma > a.sigma_d;
+        const double rzi = qpb_rcp(z);
+        // updatekktmatrix (Auxilary.c:211-215): z pivot -s/z, regularised (ldl.c:319-320)
+        factor(isz ? -qpb_rcp_reg(-s * rzi) : 0.0);
+        QPB_TS(10 + 8 * it);
+        if (!pc) sigma = a.sigma_d;
+        double cc = sigma * mu;
+        double dx, dy, dz, dsl;
+        auto step_length = [&]() {
+            // alpha = min over d < 0 of v/(-d) == 1 / max(-d/v); 1 if none (Auxilary.c:359-393)
+            const double bp = qpb_rmax<ROWS_Z>(isz ? -dsl * __builtin_amdgcn_rcp(s) : 0.0);
+            const double bd = qpb_rmax<ROWS_Z>(isz ? -dz * rzi : 0.0);
+            ap = bp > 1e-10 ? __builtin_amdgcn_rcp(bp) : 1.0;
+            ad = bd > 1e-10 ? __builtin_amdgcn_rcp(bd) : 1.0;
+        };
+        if (pc) {
+            // predictor (kktsolve_1, Auxilary.c:471-515): ds = -s.*z
+            solve(rx, ry, rz + s, dx, dy, dz);
+            QPB_TS(11 + 8 * it);
+            dsl = -s * __builtin_fma(dz, rzi, 1.0);
+            step_length();
+            const double rho = qpb_rsum<ROWS_Z>(isz ? (s + ap * dsl) * (z + ad * dz) : 0.0) * qpb_rcp(sz);   // formrho
+            const double r1 = 1 > rho ? rho : 1;
+            const double cube = r1 * r1 * r1;
+            sigma = a.sigma_d < cube ? cube : a.sigma_d;
+            cc = __builtin_fma(-dsl, dz, sigma * mu);
+            QPB_TS(12 + 8 * it);
+        }
+        // corrector / centering (kktsolve_2, Auxilary.c:524-564)
+        solve(rx, ry, __builtin_fma(-cc, rzi, rz + s), dx, dy, dz);
+        QPB_TS(13 + 8 * it);
+        dsl = __builtin_fma(__builtin_fma(-s, dz, cc), rzi, -s);
+        step_length();
+        QPB_TS(14 + 8 * it);
+        ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
+        ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
+        if (isx) x = __builtin_fma(dx, ap, x);
+        if (isy) y = __builtin_fma(dy, ad, y);
+        if (isz) {
+            s = __builtin_fma(dsl, ap, s);
+            z = __builtin_fma(dz, ad, z);
+        }
+        it++;
+    }
+    QPB_TS(370);
+    // ---- outputs (tiled SoA)
+    if (isx) a.x[tile * (NX * 64) + lane * 64 + ql] = x;
+#if NY > 0
+    if (isy) a.y[tile * (NY * 64) + lane * 64 + ql] = y;
+#endif
+    if (isz) {
+        a.z[tile * (NZ * 64) + lane * 64 + ql] = z;
+        a.s[tile * (NZ * 64) + lane * 64 + ql] = s;
+    }
+    if (lane == 0) {
+        a.flag[q] = flag;
+        a.iters[q] = (int)it;
+        a.fval[q] = fval;
+        if (a.stats && !QPB_W_TIMING) {
+            double *o = a.stats + tile * 384 + ql;
+            o[0] = st_rx; o[64] = st_ry; o[128] = st_rz; o[192] = st_mu; o[256] = ap; o[320] = ad;
+        }
+    }
+    QPB_TS(371);
+}

@@ -2,16 +2,19 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 
-One step = one batched IPM solve (kkt_initialize + QP_SOLVE) of
-this rank's resident batch of synthetic contact-force QPs (12 vars / 20 ineq /
-6 eq) followed by the device-side argmin; for N > 1 the per-rank
+Workload = BASELINE.json configs[1]: a batch of 1 024 identical-sparsity C1
+contact-force QPs (12 vars / 20 ineq / 6 eq) per GPU.  One step =
+one batched IPM solve (kkt_initialize + QP_SOLVE) of this rank's
+resident batch followed by the device-side argmin; for N > 1 the per-rank
 winners are exchanged with one RCCL all_gather (config 5's argmin gather).
-Shards are independent (weak scaling): rank r owns QP ids [r*B, (r+1)*B).
+Shards are independent (weak scaling): rank r owns QP ids [r*B, (r+1)*B);
+config 5 (65 536 QPs over 8 GPUs) is `--gpus 8 --batch 8192`.
 
-The default per-GPU batch (2^20 QPs, ~2 GB of inputs) keeps the working set far
-above the 256 MB Infinity Cache, as SURVEY §8d asks for HBM-roofline numbers; the
-BASELINE configs[1] shape (1 024 QPs per launch) is reported beside it as
-`batch1024` (latency-bound).  Rank 0 prints one JSON line.
+At this batch size qpb_solve runs the wave-cooperative kernel (one QP per
+wavefront).  Beside the headline, rank 0 of a 1-GPU run also measures a 2^20-QP
+batch (lane kernel, one QP per lane; working set ~2 GB, far above the 256 MB
+Infinity Cache) as `large_batch`, the HBM-scale throughput figure.
+Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -34,14 +37,17 @@ FP64_PEAK_TFLOPS = 78.6        # MI355X FP64 vector
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="QPs per GPU per step")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1024, help="QPs per GPU per step (configs[1]: 1024)")
+    ap.add_argument("--large-batch", type=int, default=1 << 20,
+                    help="QPs of the secondary large-batch leg (1-GPU runs; 0 = skip)")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave"])
     ap.add_argument("--tol", type=float, default=1e-6)
     ap.add_argument("--exact", action="store_true", help="bench the bit-faithful kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-sample", type=int, default=65536)
-    ap.add_argument("--cpu-passes", type=int, default=4)
+    ap.add_argument("--cpu-passes", type=int, default=10)
     return ap.parse_args()
 
 
@@ -106,6 +112,65 @@ def cpu_baseline(seed, sample, passes, tol):
                 mean_iters=float(iters.mean()), optimal_frac=float((flags == 0).mean()))
 
 
+def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True):
+    """Timed loop of `steps` steps (solve + argmin [+ all_gather]) on resident
+    inputs.  Returns (wall seconds max over ranks, mean kernel ms max over
+    ranks, outputs, gathered winners)."""
+    import torch
+    import torch.distributed as dist
+    from apf_quadruped_amd.batch import argmin_launcher
+    host = make_shard(plan, seed, rank * B, B)
+    vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
+    del host
+    out = plan.alloc_outputs(B, device=dev)
+    best = torch.empty(2, dtype=torch.float64, device=dev)
+    gathered = torch.empty(2 * world, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream)
+    amin = argmin_launcher(out["fval"], out["flag"], best, stream=stream)
+    coll = gather and world > 1
+
+    for _ in range(warmup):
+        solve()
+        amin()
+        if coll:
+            dist.all_gather_into_tensor(gathered, best)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    # kernel duration: HIP events on the launch stream, around every solve
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        solve()
+        ev[i][1].record(stream)
+        amin()
+        if coll:
+            dist.all_gather_into_tensor(gathered, best)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    return elapsed, kern_ms, out, gathered
+
+
+def traffic_for(kname, B):
+    tfile = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        t = json.load(open(tfile)).get(kname)
+        if t and int(t.get("batch", -1)) == B:
+            return float(t["hbm_bytes_per_launch"])
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -119,66 +184,19 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from apf_quadruped_amd.batch import Plan, argmin, ntiles
+    from apf_quadruped_amd.batch import Plan
     from apf_quadruped_amd import plans
 
     seed = plans.SEED + 1
     d0 = plans.standard_qp("c1")
-    plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=args.exact)
+    plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=args.exact, kernel=args.kernel)
     plan.compile()
     B = args.batch
-    host = make_shard(plan, seed, rank * B, B)
-    vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
-    del host
-    out = plan.alloc_outputs(B, device=dev)
-    best = torch.empty(2, dtype=torch.float64, device=dev)
-    gathered = torch.empty(2 * world, dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-
-    def step():
-        plan.solve(**vals, B=B, reltol=args.tol, abstol=args.tol, out=out, stream=stream)
-        argmin(out["fval"], out["flag"], out=best, stream=stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, best)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        plan.solve(**vals, B=B, reltol=args.tol, abstol=args.tol, out=out, stream=stream)
-        ev[i][1].record(stream)
-        argmin(out["fval"], out["flag"], out=best, stream=stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, best)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
-
-    traffic = None
-    kname = plan.source().split("(qpb_args")[0].split()[-1]
-    tfile = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tfile):
-        t = json.load(open(tfile)).get(kname)
-        if t and int(t.get("batch", -1)) == B:
-            traffic = float(t["hbm_bytes_per_launch"])
+    elapsed, kern_ms, out, gathered = run_leg(plan, B, args.steps, args.warmup, args.tol, dev, rank, world, seed)
+    kname = plan.kernel_name(B)
     flags = out["flag"].cpu().numpy()
     iters = out["iters"].cpu().numpy()
     mean_it = float(iters.mean())
-    if world > 1:
-        g = gathered.cpu().numpy().reshape(world, 2)
     ms_step = elapsed * 1e3 / args.steps
     value = world * B * args.steps / elapsed
     bpq = plan.bytes_per_qp()
@@ -186,22 +204,21 @@ def main():
     fpq = flops_per_qp(plan.info, mean_it)
     fp64_tf = fpq * B / (kern_ms * 1e-3) / 1e12
 
-    # configs[1]: one batch of 1 024 QPs per launch (latency-bound)
-    small = None
-    if rank == 0:
-        Bs = 1024
-        sv = {k: v[: ntiles(Bs) * 64 * (v.numel() // (ntiles(B) * 64))] for k, v in vals.items()}
-        so = plan.alloc_outputs(Bs, device=dev)
-        for _ in range(5):
-            plan.solve(**sv, B=Bs, reltol=args.tol, abstol=args.tol, out=so, stream=stream)
-        torch.cuda.synchronize()
-        n_small = 200
-        t1 = time.perf_counter()
-        for _ in range(n_small):
-            plan.solve(**sv, B=Bs, reltol=args.tol, abstol=args.tol, out=so, stream=stream)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t1
-        small = dict(batch=Bs, launches=n_small, us_per_launch=dt * 1e6 / n_small, qps=Bs * n_small / dt)
+    # secondary leg: one large batch per launch (lane kernel), HBM-scale numbers
+    large = None
+    if rank == 0 and world == 1 and args.large_batch > 0:
+        BL = args.large_batch
+        el, km, outl, _ = run_leg(plan, BL, 10, 2, args.tol, dev, 0, 1, seed, gather=False)
+        kl = plan.kernel_name(BL)
+        itl = float(outl["iters"].float().mean().item())
+        achl = bpq * BL / (km * 1e-3) / 1e9
+        large = {"batch": BL, "value": BL * 10 / el, "ms_per_step": el * 1e3 / 10, "kernel": kl,
+                 "kernel_ms": km, "kernel_qps": BL / (km * 1e-3),
+                 "roofline": {"bound": "hbm", "achieved": achl, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": achl / HBM_PEAK_GBS, "traffic": traffic_for(kl, BL)},
+                 "fp64_tflops": flops_per_qp(plan.info, itl) * BL / (km * 1e-3) / 1e12,
+                 "mean_iters": itl, "optimal_frac": float((outl["flag"] == 0).float().mean().item())}
+        del outl
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -221,23 +238,24 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (counter-based RNG, SURVEY §8d contact-force QPs, resident in HBM)",
-            "config": {"workload": "c1_contact_force_12v_20ineq_6eq", "qps_per_gpu": B,
-                       "global_batch": B * world, "tol": args.tol,
-                       "kernel": "exact" if args.exact else "fast",
-                       "ordering": "own min-degree", "kkt_N": plan.info.N, "nnz_L": plan.info.lnz,
-                       "parallelism": f"shard{world}"},
+            "config": {"workload": "configs[1]: batch of 1024 identical-sparsity C1 contact-force QPs per GPU"
+                                   if B == 1024 else f"batch of {B} identical-sparsity C1 contact-force QPs per GPU",
+                       "qps_per_gpu": B, "global_batch": B * world, "tol": args.tol,
+                       "kernel": kname, "arith": "exact" if args.exact else "fast",
+                       "kkt_N": plan.info.N, "nnz_L": plan.info.lnz, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(kname, B),
                          "algorithmic_bytes_per_launch": bpq * B, "bytes_per_qp": bpq,
                          "kernel_ms": kern_ms, "kernel": kname},
             "fp64": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
                      "frac": fp64_tf / FP64_PEAK_TFLOPS, "flops_per_qp": fpq},
             "mean_iters": mean_it,
             "optimal_frac": float((flags == 0).mean()),
-            "batch1024": small,
+            "large_batch": large,
             "cpu_baseline": cpu,
         }
         if world > 1:
+            g = gathered.cpu().numpy().reshape(world, 2)
             k = int(np.argmin(np.where(g[:, 1] >= 0, g[:, 0], np.inf)))
             line["argmin"] = {"fval": float(g[k, 0]), "rank": k, "index": int(g[k, 1]) + k * B}
         print(json.dumps(line))

@@ -50,6 +50,8 @@ typedef struct qpb_plan qpb_plan;
 #define QPB_P_FULL   0x0   /* P pattern holds both triangles (QP_SETUP semantics) */
 #define QPB_P_UPPER  0x1   /* P pattern is the upper triangle (symmetric P)        */
 #define QPB_EXACT    0x10  /* bit-faithful arithmetic: IEEE division, no FMA       */
+#define QPB_KERNEL_LANE 0x100  /* always the lane kernel (one QP per lane)         */
+#define QPB_KERNEL_WAVE 0x200  /* always the wave kernel (one QP per wavefront)    */
 
 /* error codes */
 #define QPB_OK        0
@@ -74,6 +76,8 @@ typedef struct qpb_plan_info {
     int  ordering;               /* 0 caller permutation, 1 own minimum degree */
     int  exact;
     uint64_t hash;               /* pattern + permutation hash */
+    int  wave_ok;                /* plan can use the wave-cooperative kernel */
+    long wave_max_batch;         /* qpb_solve uses it for B <= this (-1: always) */
 } qpb_plan_info;
 
 void qpb_default_settings(qpb_settings *st);
@@ -89,8 +93,9 @@ int  qpb_plan_get_perm(const qpb_plan *plan, long *perm /* [N] */);
 /* Generated HIP source of the plan's kernel; returns its length (copies at most
  * cap-1 bytes plus a NUL when buf is non-NULL). */
 long qpb_plan_source(const qpb_plan *plan, char *buf, long cap);
-/* Compile the plan's kernel for gfx950 (hiprtc) or fetch it from the code-object
- * cache; needs no GPU.  qpb_solve calls this implicitly. */
+long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap);
+/* Compile the plan's kernels for gfx950 (hiprtc) or fetch them from the
+ * code-object cache; needs no GPU.  qpb_solve calls this implicitly. */
 int  qpb_plan_compile(qpb_plan *plan);
 
 int  qpb_solve(qpb_plan *plan, long B,

@@ -13,6 +13,7 @@ def main():
     ap.add_argument("--batch", type=int, default=262144)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--exact", action="store_true")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave"])
     a = ap.parse_args()
     import torch
     from apf_quadruped_amd import plans
@@ -20,7 +21,7 @@ def main():
     import bench
     torch.cuda.set_device(0)
     d0 = plans.standard_qp("c1")
-    plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=a.exact)
+    plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=a.exact, kernel=a.kernel)
     vals = {k: torch.from_numpy(v).cuda() for k, v in bench.make_shard(plan, plans.SEED + 1, 0, a.batch).items()}
     out = plan.solve(**vals, B=a.batch)
     for _ in range(a.reps):

@@ -1,7 +1,7 @@
 """A/B kernel variants in one process on one GPU (cdna guide rule 24).
 
     python scripts/sweep.py [--batch B] [--reps R] VARIANT...
-VARIANT = "wg:lds" (fast kernel) or "exact".  Prints one JSON line per variant.
+VARIANT = "wg:lds" (fast lane kernel), "exact" (lane) or "wave" (wave-cooperative).  Prints one JSON line per variant.
 """
 import argparse
 import json
@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--maxit", type=int, default=100)
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -38,11 +39,18 @@ def main():
         if v == "exact":
             os.environ.pop("QPB_WG", None); os.environ.pop("QPB_LDS", None)
             plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=True)
+        elif v.startswith("wave"):
+            # "wave" or "wave:KNOB=V,KNOB=V" (QPB_W_* knobs of qpb_wave.hip)
+            opts = v.split(":", 1)[1].replace(",", " ") if ":" in v else ""
+            os.environ["QPB_WAVE_OPTS"] = " ".join("QPB_W_" + o for o in opts.split())
+            plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], kernel="wave")
+            plans_[v].compile()
+            os.environ.pop("QPB_WAVE_OPTS", None)
         else:
             parts = v.split(":")
             os.environ["QPB_WG"], os.environ["QPB_LDS"] = parts[0], parts[1]
             os.environ["QPB_PARKZ"] = parts[2] if len(parts) > 2 else "1"
-            plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0])
+            plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], kernel="lane")
         t0 = time.time(); plans_[v].compile(); ct = time.time() - t0
         print(f"compiled {v} in {ct:.1f}s", file=sys.stderr)
     for k in ("QPB_WG", "QPB_LDS", "QPB_PARKZ"):
@@ -57,19 +65,36 @@ def main():
     for r in range(a.rounds):
         for v in a.variants:
             pl = plans_[v]
-            out = pl.solve(**vals, B=a.batch)
+            out = pl.solve(**vals, B=a.batch, maxit=a.maxit)
             torch.cuda.synchronize()
             for _ in range(a.reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(); pl.solve(**vals, B=a.batch, out=out); e1.record(); torch.cuda.synchronize()
+                e0.record(); pl.solve(**vals, B=a.batch, out=out, maxit=a.maxit); e1.record(); torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1))
             outs[v] = out
     for v in a.variants:
         pl = plans_[v]
+        if "TIMING=1" in v:      # phase timestamps of QP 0 of tile 0 (s_memtime cycles)
+            t = outs[v]["stats"][:384].cpu().numpy()
+            base = t[0]
+            ph = {"stage": t[1] - t[0], "init_factor": t[2] - t[1], "init_solve": t[3] - t[2],
+                  "init_sz": t[4] - t[3]}
+            its = []
+            for it in range(int(outs[v]["iters"][0].item())):
+                r = t[8 + 8 * it: 16 + 8 * it]
+                its.append(dict(resid=r[1] - r[0], factor=r[2] - r[1], pred_solve=r[3] - r[2], pred_step=r[4] - r[3],
+                                corr_solve=r[5] - r[4], corr_step=r[6] - r[5],
+                                update=(t[16 + 8 * it] if t[16 + 8 * it] > 0 else t[370]) - r[6]))
+            ph["out"] = t[371] - t[370]
+            ph["total"] = t[371] - base
+            print(json.dumps(dict(variant=v, phases=ph, iterations=its)))
+            continue
         res = pl.unpack(outs[v], a.batch)
         err = 0.0
         for k, q in enumerate(ids):
-            ref = o.solve_dense(12, 20, 6, Pc[k], Ac[k], Gc[k], dd["c"][k], dd["h"][k], dd["b"][k], perm=pl.perm)
+            perm = pl.wave_perm() if v.startswith("wave") else pl.perm
+            ref = o.solve_dense(12, 20, 6, Pc[k], Ac[k], Gc[k], dd["c"][k], dd["h"][k], dd["b"][k], perm=perm,
+                                maxit=a.maxit)
             err = max(err, float(np.max(np.abs(ref["x"] - res["x"][q]))))
         ms = float(np.median(times[v]))
         print(json.dumps(dict(variant=v, kernel=pl.info.hash, ms_median=ms, ms_min=float(np.min(times[v])),

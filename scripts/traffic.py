@@ -6,7 +6,11 @@ FETCH_SIZE reads 1/2 of the bytes of 512-B-per-wave coalesced reads on gfx950
 byte count is known exactly (2 * FETCH_SIZE == algorithmic input bytes within
 2 %); WRITE_SIZE matched the output bytes exactly.
 
-    python scripts/traffic.py FETCH_CSV WRITE_CSV BATCH
+    python scripts/traffic.py FETCH_CSV WRITE_CSV BATCH [BATCH ...]
+
+The wave kernel (qpb_wave_*, one QP per wavefront) reads its inputs with 8-B
+per-lane loads, an access width the guide leaves uncalibrated; its entry is
+recorded with the same formula and marked "calibrated": false.
 """
 import csv
 import json
@@ -15,31 +19,38 @@ import sys
 from collections import defaultdict
 
 
+def grid_for(kname, wg, batch):
+    """Grid size (threads) of a launch of `batch` QPs."""
+    per_block = wg // 64 if kname.startswith("qpb_wave_") else wg
+    return (batch + per_block - 1) // per_block * wg
+
+
 def per_kernel(path, counter, batch):
-    """Mean counter value over the dispatches of `batch` QPs (grid == batch
-    rounded up to whole workgroups)."""
+    """Mean counter value over the dispatches of `batch` QPs."""
     vals = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "qpb_ipm" not in r["Kernel_Name"]:
+        k = r["Kernel_Name"]
+        if r["Counter_Name"] != counter or not (k.startswith("qpb_ipm") or k.startswith("qpb_wave")):
             continue
-        wg = int(r["Workgroup_Size"])
-        if int(r["Grid_Size"]) != (batch + wg - 1) // wg * wg:
+        if int(r["Grid_Size"]) != grid_for(k, int(r["Workgroup_Size"]), batch):
             continue
-        vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        vals[k].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
 def main():
-    fetch, write, batch = sys.argv[1], sys.argv[2], int(sys.argv[3])
-    f = per_kernel(fetch, "FETCH_SIZE", batch)
-    w = per_kernel(write, "WRITE_SIZE", batch)
+    fetch, write = sys.argv[1], sys.argv[2]
     out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
     data = json.load(open(out_path)) if os.path.exists(out_path) else {}
-    for k in f:
-        if k in w:
-            data[k] = dict(batch=batch, fetch_kb=f[k], write_kb=w[k],
-                           hbm_bytes_per_launch=(2 * f[k] + w[k]) * 1024.0)
-            print(k, data[k])
+    for batch in map(int, sys.argv[3:]):
+        f = per_kernel(fetch, "FETCH_SIZE", batch)
+        w = per_kernel(write, "WRITE_SIZE", batch)
+        for k in f:
+            if k in w:
+                data[k] = dict(batch=batch, fetch_kb=f[k], write_kb=w[k],
+                               hbm_bytes_per_launch=(2 * f[k] + w[k]) * 1024.0,
+                               calibrated=not k.startswith("qpb_wave_"))
+                print(k, data[k])
     json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
 
 

@@ -169,7 +169,8 @@ def test_dropin_dense_bit_identical_to_reference(name):
             assert np.array_equal(r[k], g[k][q]), (name, q, k)
         if int(g["p"]):
             assert np.array_equal(r["y"], g["y"][q]), (name, q, "y")
-        assert r["fval"] == float(g["fval"][q])
+        if maxit > 0:   # with maxit = 0 the reference never writes stats->fval (qpSWIFT.c:511)
+            assert r["fval"] == float(g["fval"][q])
         assert r["amd_result"] == -3
 
 

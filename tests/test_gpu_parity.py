@@ -33,11 +33,12 @@ def _dense(g):
     return n, m, p, P, A, G
 
 
-def _solve(g, perm, exact, p_upper=False):
+def _solve(g, perm, exact, p_upper=False, kernel="lane"):
     from apf_quadruped_amd.batch import Plan
     n, m, p, P, A, G = _dense(g)
     B = P.shape[0]
-    plan = Plan.from_dense(n, m, p, P[0], A[0] if p else None, G[0], perm=perm, p_upper=p_upper, exact=exact)
+    plan = Plan.from_dense(n, m, p, P[0], A[0] if p else None, G[0], perm=perm, p_upper=p_upper, exact=exact,
+                           kernel=kernel)
     vals = plan.pack(P, A, G, g["c"], g["h"], g["b"] if p else None)
     tol = float(g["tol"])
     out = plan.solve(**vals, B=B, reltol=tol, abstol=tol, maxit=int(g["maxit"]))
@@ -61,9 +62,11 @@ def test_exact_kernel_bit_identical_to_reference(name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", DENSE_CASES)
-@pytest.mark.parametrize("exact,own_order", [(False, False), (False, True), (True, True)])
-def test_kernel_within_tolerance_of_reference(name, exact, own_order):
+@pytest.mark.parametrize("exact,own_order,kernel", [(False, False, "lane"), (False, True, "lane"),
+                                                    (True, True, "lane"), (False, True, "wave")])
+def test_kernel_within_tolerance_of_reference(name, exact, own_order, kernel):
     """Fast kernel and/or own ordering vs the reference: |.|_inf <= 1e-6 * max(1, |ref|).
+    The wave kernel always eliminates in its own order [z | y | x].
 
     With another KKT ordering the dynamic regularisation (ldl.c:319-320) lands on
     other pivots; where A has a row-rank defect (2-foot trot: rank 5) the dual y
@@ -73,7 +76,7 @@ def test_kernel_within_tolerance_of_reference(name, exact, own_order):
     truncated = int(g["maxit"]) < 100
     if own_order and (name == "edge_zero_g_row" or truncated):
         pytest.skip("depends on the reference's own KKT order")
-    _, r = _solve(g, perm=None if own_order else g["perm"][0], exact=exact, p_upper=True)
+    _, r = _solve(g, perm=None if own_order else g["perm"][0], exact=exact, p_upper=True, kernel=kernel)
     n, m, p, P, A, G = _dense(g)
     sel = slice(None) if truncated else (g["flag"] == 0)
     if not truncated:
@@ -110,23 +113,58 @@ def test_exact_kernel_matches_oracle_with_own_ordering(oracle):
         assert r["iters"][q] == o["iters"] and r["fval"][q] == o["fval"]
 
 
+def _oracle_perm(plan):
+    return plan.wave_perm() if plan.kernel == "wave" else plan.perm
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "c1_noeq", "mixed_stance4", "mixed_trot_blfr",
+                                  "mixed_trot_brfl", "mixed_crawl_blflfr", "c1_maxit3"])
+def test_wave_kernel_matches_oracle_in_its_order(name, oracle):
+    """Wave kernel vs the oracle run with the wave kernel's elimination order:
+    same factorisation, so agreement is at rounding level (1e-9 relative)."""
+    g = golden(name)
+    plan, r = _solve(g, perm=None, exact=False, p_upper=True, kernel="wave")
+    n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
+    tol = float(g["tol"])
+    for q in range(0, g["x"].shape[0], 3):
+        o = oracle.solve_dense(n, m, p, g["P"][q], g["A"][q] if p else None, g["G"][q], g["c"][q], g["h"][q],
+                               g["b"][q] if p else None, perm=plan.wave_perm(), ordering=int(g["ordering"]),
+                               reltol=tol, abstol=tol, maxit=int(g["maxit"]))
+        assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (name, q)
+        got, ref = {k: r[k][q] for k in ("x", "z", "s")}, {k: o[k] for k in ("x", "z", "s")}
+        if p:
+            # y is unique only modulo null(A^T) when A is rank deficient (2-foot trot)
+            Aq = _dense(g)[4][q]
+            if np.linalg.matrix_rank(Aq) < p:
+                got["Aty"], ref["Aty"] = Aq.T @ r["y"][q], Aq.T @ o["y"]
+            else:
+                got["y"], ref["y"] = r["y"][q], o["y"]
+        for k in got:
+            scale = max(1.0, float(np.abs(ref[k]).max()))
+            assert np.abs(got[k] - ref[k]).max() <= 1e-9 * scale, (name, q, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["lane", "wave"])
 @pytest.mark.parametrize("B", [1, 63, 65, 1000])
-def test_ragged_batches(B, oracle):
+def test_ragged_batches(B, kernel, oracle):
     from apf_quadruped_amd import workloads as W
     from apf_quadruped_amd.batch import Plan
     d = W.contact_force_qp(0xD06B07 + 11, np.arange(B))
-    plan = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0])
+    plan = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0], kernel=kernel)
     out = plan.solve(**plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]), B=B)
     r = plan.unpack(out, B)
     Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
     for q in sorted({0, B // 2, B - 1}):
-        o = oracle.solve_dense(12, 20, 6, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm)
+        o = oracle.solve_dense(12, 20, 6, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q],
+                               perm=_oracle_perm(plan))
         assert np.max(np.abs(o["x"] - r["x"][q])) <= TOL * max(1, np.max(np.abs(o["x"])))
 
 
 @pytest.mark.gpu
-def test_large_batch_properties(oracle):
+@pytest.mark.parametrize("kernel", ["lane", "wave"])
+def test_large_batch_properties(kernel, oracle):
     """B = 65536 (config 5's global batch on one GPU): all optimal, KKT residuals
     small, deterministic, each QP independent of its neighbours."""
     import torch
@@ -134,7 +172,7 @@ def test_large_batch_properties(oracle):
     from apf_quadruped_amd.batch import Plan
     B = 65536
     d = W.contact_force_qp(0xD06B07 + 5, np.arange(B))
-    plan = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0])
+    plan = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0], kernel=kernel)
     vals = plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"])
     vals = {k: torch.from_numpy(v).cuda() for k, v in vals.items()}
     r1 = plan.unpack(plan.solve(**vals, B=B), B)
@@ -156,7 +194,8 @@ def test_large_batch_properties(oracle):
     np.testing.assert_array_equal(r3["x"], r1["x"][perm])
     Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
     for q in range(0, B, 4099):
-        o = oracle.solve_dense(12, 20, 6, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm)
+        o = oracle.solve_dense(12, 20, 6, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q],
+                               perm=_oracle_perm(plan))
         assert np.max(np.abs(o["x"] - r1["x"][q])) <= TOL * max(1, np.max(np.abs(o["x"])))
 
 
