@@ -119,7 +119,8 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True):
     import torch
     import torch.distributed as dist
     from apf_quadruped_amd.batch import argmin_launcher
-    host = make_shard(plan, seed, rank * B, B)
+    from apf_quadruped_amd.shard import shard_range
+    host = make_shard(plan, seed, shard_range(rank, world, B)[0], B)
     vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
     del host
     out = plan.alloc_outputs(B, device=dev)
@@ -255,9 +256,9 @@ def main():
             "cpu_baseline": cpu,
         }
         if world > 1:
-            g = gathered.cpu().numpy().reshape(world, 2)
-            k = int(np.argmin(np.where(g[:, 1] >= 0, g[:, 0], np.inf)))
-            line["argmin"] = {"fval": float(g[k, 0]), "rank": k, "index": int(g[k, 1]) + k * B}
+            from apf_quadruped_amd.shard import global_winner, shard_range
+            fv, gi, rk = global_winner(gathered.cpu().numpy(), [shard_range(r, world, B)[0] for r in range(world)])
+            line["argmin"] = {"fval": fv, "rank": rk, "index": gi}
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

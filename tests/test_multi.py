@@ -1,0 +1,95 @@
+"""N > 1 path on CPU: world-size-2 gloo run of the shard / argmin-gather logic
+(apf_quadruped_amd/shard.py) that bench.py uses with RCCL on the GPUs.
+
+Each rank solves its own contiguous shard (here with the oracle, the CPU
+checker), reduces it to (fval, local index) with the qpb_argmin rule, and the
+ranks exchange 16 B each; the gathered winner must equal the single-process
+argmin over the whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+PER_RANK = 12
+SEED = 0xD06B07 + 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _solve_fvals(ids):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle_py import Oracle
+    from apf_quadruped_amd import workloads as W
+    o = Oracle()
+    d = W.contact_force_qp(SEED, ids)
+    Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    fv, fl = [], []
+    for k in range(len(ids)):
+        r = o.solve_dense(12, 20, 6, Pc[k], Ac[k], Gc[k], d["c"][k], d["h"][k], d["b"][k])
+        fv.append(r["fval"])
+        fl.append(r["flag"])
+    return np.array(fv), np.array(fl)
+
+
+def _local_argmin(fv, fl):
+    best = (np.inf, -1)
+    for i, (v, f) in enumerate(zip(fv, fl)):
+        if f == 0 and (best[1] < 0 or v < best[0]):
+            best = (v, i)
+    return best
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from apf_quadruped_amd.shard import all_gather_winner, global_winner, shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(rank, world, PER_RANK)
+    fv, fl = _solve_fvals(np.arange(lo, hi))
+    v, i = _local_argmin(fv, fl)
+    g = all_gather_winner(torch.tensor([v, float(i)], dtype=torch.float64), world)
+    offsets = [shard_range(r, world, PER_RANK)[0] for r in range(world)]
+    q.put((rank, global_winner(g.numpy(), offsets)))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_argmin_gather():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fv, fl = _solve_fvals(np.arange(world * PER_RANK))
+    v, i = _local_argmin(fv, fl)
+    for r in range(world):
+        assert res[r][0] == v and res[r][1] == i, (r, res[r], (v, i))
+
+
+def test_shard_helpers():
+    from apf_quadruped_amd.shard import global_winner, shard_range, split_even
+    assert shard_range(3, 8, 8192) == (24576, 32768)
+    assert [split_even(10, 3, r) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
+    with pytest.raises(ValueError):
+        shard_range(2, 2, 1)
+    # ties -> lowest global index; ranks without an optimal QP (-1) are skipped
+    g = [[1.0, 5], [1.0, 0], [np.inf, -1]]
+    assert global_winner(g, [0, 100, 200]) == (1.0, 5, 0)
+    assert global_winner([[np.inf, -1]], [0]) == (np.inf, -1, -1)
