@@ -248,10 +248,12 @@ class Plan:
         return out
 
 
-    def launcher(self, vals, out, B, reltol=1e-6, abstol=1e-6, maxit=100, sigma_d=0.0, stream=None):
+    def launcher(self, vals, out, B, reltol=1e-6, abstol=1e-6, maxit=100, sigma_d=0.0, stream=None, best=None):
         """A zero-argument callable that launches qpb_solve on fixed device buffers
         with every C argument pre-built: one ctypes call per launch, so a Python
-        loop of launches stays GPU-bound even for small batches."""
+        loop of launches stays GPU-bound even for small batches.  With `best` (a
+        float64 device tensor of >= 2) it calls qpb_solve_best: the batch's
+        argmin {fval, index} lands in best[0:2]."""
         import torch
         if stream is None:
             stream = torch.cuda.current_stream()
@@ -260,10 +262,16 @@ class Plan:
         args = (self._h, int(B), ptr(vals["P"]), ptr(vals.get("A")) if self.p else None, ptr(vals["G"]),
                 ptr(vals["c"]), ptr(vals["h"]), ptr(vals.get("b")) if self.p else None, C.byref(st),
                 ptr(out["x"]), ptr(out["y"]) if self.p else None, ptr(out["z"]), ptr(out["s"]),
-                ptr(out["flag"]), ptr(out["iters"]), ptr(out["fval"]), ptr(out.get("stats")),
-                C.c_void_p(stream.cuda_stream))
-        fn = _lib.lib().qpb_solve
-        keep = (vals, out, st)
+                ptr(out["flag"]), ptr(out["iters"]), ptr(out["fval"]), ptr(out.get("stats")))
+        if best is not None:
+            if best.numel() < 2 or best.dtype != torch.float64:
+                raise ValueError("best must be a float64 device tensor of >= 2 elements")
+            args = args + (ptr(best), C.c_void_p(stream.cuda_stream))
+            fn = _lib.lib().qpb_solve_best
+        else:
+            args = args + (C.c_void_p(stream.cuda_stream),)
+            fn = _lib.lib().qpb_solve
+        keep = (vals, out, st, best)
 
         def go():
             rc = fn(*args)

@@ -114,6 +114,16 @@ __global__ void __launch_bounds__(1024) qpb_argmin_final(long nb, const double *
     if (threadIdx.x == 0) { out[0] = bv; out[1] = (double)bi; }
 }
 
+__global__ void __launch_bounds__(1024) qpb_argmin_single(long B, const double *__restrict__ fval,
+                                                          const int *__restrict__ flag, double *__restrict__ out) {
+    double bv = INFINITY;
+    long bi = -1;
+    for (long q = threadIdx.x; q < B; q += blockDim.x)
+        if (flag[q] == 0 && qpb_better(fval[q], q, bv, bi)) { bv = fval[q]; bi = q; }
+    qpb_block_argmin(bv, bi);
+    if (threadIdx.x == 0) { out[0] = bv; out[1] = (double)bi; }
+}
+
 // Strided segment copies dst[i * ds] = src[i * ss]; blockIdx.y selects the
 // segment.  Used by the single-QP drop-in to move packed host-order vectors in
 // and out of the tiled SoA layout with one H2D and one D2H transfer.
@@ -309,10 +319,10 @@ int qpb_plan_compile(qpb_plan *plan) {
     return rc;
 }
 
-int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
-              const double *c, const double *h, const double *b, const qpb_settings *st,
-              double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
-              double *stats, void *stream) {
+static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
+                      const double *c, const double *h, const double *b, const qpb_settings *st,
+                      double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
+                      double *stats, double *best, void *stream) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     if (B < 0) return fail(QPB_EINVAL, "need B >= 0");
     if (B == 0) return QPB_OK;
@@ -346,7 +356,25 @@ int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const do
     const unsigned grid = (unsigned)((B + per_block - 1) / per_block);
     hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, wg, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("launch: ") + hipGetErrorString(e));
+    // an in-kernel "last wave reduces" argmin was measured slower than this
+    // separate single-block launch (agent-coherent stores + counter tail), DESIGN.md
+    if (best) return qpb_argmin(B, fval, flag, best, stream);
     return QPB_OK;
+}
+
+int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
+              const double *c, const double *h, const double *b, const qpb_settings *st,
+              double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
+              double *stats, void *stream) {
+    return solve_impl(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, nullptr, stream);
+}
+
+int qpb_solve_best(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
+                   const double *c, const double *h, const double *b, const qpb_settings *st,
+                   double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
+                   double *stats, double *best, void *stream) {
+    if (!best) return fail(QPB_EINVAL, "qpb_solve_best: best is NULL");
+    return solve_impl(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, best, stream);
 }
 
 int qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *stream) {
@@ -365,9 +393,13 @@ int qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *
     }
     double *pv = (double *)buf.first;
     long *pi = (long *)((char *)buf.first + nb * 8);
-    hipLaunchKernelGGL(qpb_argmin_partial, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, B, chunk, fval, flag,
-                       pv, pi);
-    hipLaunchKernelGGL(qpb_argmin_final, dim3(1), dim3(1024), 0, (hipStream_t)stream, nb, pv, pi, out2);
+    if (nb == 1) {   // one block covers the batch: a single launch writes the result
+        hipLaunchKernelGGL(qpb_argmin_single, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, fval, flag, out2);
+    } else {
+        hipLaunchKernelGGL(qpb_argmin_partial, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, B, chunk, fval,
+                           flag, pv, pi);
+        hipLaunchKernelGGL(qpb_argmin_final, dim3(1), dim3(1024), 0, (hipStream_t)stream, nb, pv, pi, out2);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("argmin: ") + hipGetErrorString(e));
     return QPB_OK;

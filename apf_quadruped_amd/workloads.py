@@ -171,3 +171,91 @@ def mpc_qp(seed: int, qp_ids, horizon: int = 10, mu: float = MU):
 def to_colmajor(M: np.ndarray) -> np.ndarray:
     """[B, r, c] row-major -> [B, r*c] column-major (QP_SETUP_dense, ordering 30)."""
     return np.ascontiguousarray(np.transpose(M, (0, 2, 1))).reshape(M.shape[0], -1)
+
+
+def controller_qp(seed: int, qp_ids):
+    """Controller-shape stance QP "C30" (30 vars / 68 ineq / 18 eq), following
+    dogbot_controller/src/client/main.cpp:1471-1647 (SURVEY §8a shape table):
+
+    x = [ddx_com (6); ddq (12); f (12)], Sigma_st selects f (main.cpp:496-497)
+      Q = 50 T_s' T_s + I, T_s = Jc' Sigma_st          (main.cpp:1476-1480)
+      c = -50 T_s' W_des                                (main.cpp:1573)
+      A = [M_com 0 -Jc'; Jc J_j 0], b = [-bias_com; -Jdqd] (main.cpp:1579-1588)
+      D rows: friction 0-19 on f, tau_max 20-31 = [0 M_jj -J_j'],
+              tau_min 32-43 = -(same), ddq_max 44-55 = [0 I 0], ddq_min 56-67 = [0 -I 0]
+      C: 0, 60 - bias_j, 60 + bias_j, ddq_max, -ddq_min  (main.cpp:1627-1647, deltat 0.025)
+    Synthetic robot terms (no rigid-body model here): M_com = blkdiag(m I3, I_c),
+    dense SPD M_jj, leg-dominant dense J_j, bias ~ U(-2, 2), q ~ U(-0.5, 0.5),
+    dq ~ U(-0.2, 0.2), joint limits +-1.5 rad.  The equality right-hand side is
+    made consistent with a random state (ddx*, ddq*, f* inside the friction
+    pyramids) so every QP is feasible.  Returns the same dict layout as
+    contact_force_qp (dense row-major [B, r, c])."""
+    qp_ids = np.atleast_1d(np.asarray(qp_ids, dtype=np.int64))
+    B = len(qp_ids)
+    Jc, W = contact_terms(seed, qp_ids)
+    u = uniforms(seed ^ 0xC30C30, qp_ids, 3 + 3 + 144 + 144 + 12 + 12 + 12 + 12 + 6 + 12 + 12)
+    k = 0
+
+    def take(cnt):
+        nonlocal k
+        v = u[:, k:k + cnt]
+        k += cnt
+        return v
+    Ic = np.zeros((B, 3, 3))
+    Ic[:, [0, 1, 2], [0, 1, 2]] = np.array([0.35, 0.85, 0.95]) * (1.0 + 0.2 * take(3))
+    off = 0.02 * take(3) - 0.01
+    Ic[:, 0, 1] = Ic[:, 1, 0] = off[:, 0]
+    Ic[:, 0, 2] = Ic[:, 2, 0] = off[:, 1]
+    Ic[:, 1, 2] = Ic[:, 2, 1] = off[:, 2]
+    Mcom = np.zeros((B, 6, 6))
+    Mcom[:, [0, 1, 2], [0, 1, 2]] = ROBOT_MASS
+    Mcom[:, 3:, 3:] = Ic
+    Lm = 0.02 * take(144).reshape(B, 12, 12) - 0.01 + 0.25 * np.eye(12)[None]
+    Mjj = np.einsum("bij,bkj->bik", Lm, Lm)                       # dense SPD
+    Jj = 0.004 * take(144).reshape(B, 12, 12) - 0.002               # weak off-block coupling
+    jb = 0.7 * take(12).reshape(B, 4, 3) - 0.35
+    for leg in range(4):                                            # leg-dominant 3x3 blocks
+        blk = np.einsum("bi,ij->bij", jb[:, leg], np.ones((3, 3))) * np.array([[1, .5, .3], [.4, 1, .6], [.2, .5, 1]])
+        Jj[:, 3 * leg:3 * leg + 3, 3 * leg:3 * leg + 3] += blk + 0.3 * np.eye(3)[None]
+    bias_j = 4.0 * take(12) - 2.0
+    q = take(12) - 0.5
+    dq = 0.4 * take(12) - 0.2
+    ddx = 2.0 * take(6) - 1.0
+    ddq = 2.0 * take(12) - 1.0
+    uf = take(12).reshape(B, 4, 3)
+    fz = 40.0 + 60.0 * uf[..., 2]
+    f = np.stack([(0.8 * uf[..., 0] - 0.4) * MU * fz, (0.8 * uf[..., 1] - 0.4) * MU * fz, fz], -1).reshape(B, 12)
+
+    n, m, p = 30, 68, 18
+    Ts = np.zeros((B, 6, n))
+    Ts[:, :, 18:30] = np.transpose(Jc, (0, 2, 1))
+    P = 50.0 * np.einsum("bki,bkj->bij", Ts, Ts) + np.eye(n)[None]
+    c = -50.0 * np.einsum("bki,bk->bi", Ts, W)
+    A = np.zeros((B, p, n))
+    A[:, 0:6, 0:6] = Mcom
+    A[:, 0:6, 18:30] = -np.transpose(Jc, (0, 2, 1))
+    A[:, 6:18, 0:6] = Jc
+    A[:, 6:18, 6:18] = Jj
+    xs = np.concatenate([ddx, ddq, f], 1)
+    b = np.einsum("bij,bj->bi", A, xs)                              # consistent with (ddx*, ddq*, f*)
+    G = np.zeros((B, m, n))
+    cfr = friction_block(MU)
+    for i in range(4):
+        G[:, 5 * i:5 * i + 5, 18 + 3 * i:18 + 3 * i + 3] = cfr
+    JjT = np.transpose(Jj, (0, 2, 1))
+    G[:, 20:32, 6:18] = Mjj
+    G[:, 20:32, 18:30] = -JjT
+    G[:, 32:44, 6:18] = -Mjj
+    G[:, 32:44, 18:30] = JjT
+    G[:, 44:56, 6:18] = np.eye(12)[None]
+    G[:, 56:68, 6:18] = -np.eye(12)[None]
+    dt = 0.025
+    qmax, qmin = 1.5, -1.5
+    ddq_max = (2 / dt ** 2) * (qmax - q - dt * dq)
+    ddq_min = (2 / dt ** 2) * (qmin - q - dt * dq)
+    h = np.zeros((B, m))
+    h[:, 20:32] = 60.0 - bias_j
+    h[:, 32:44] = -(-60.0 - bias_j)
+    h[:, 44:56] = ddq_max
+    h[:, 56:68] = -ddq_min
+    return dict(n=n, m=m, p=p, P=P, c=c, A=A, b=b, G=G, h=h)

@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--large-batch", type=int, default=1 << 20,
                     help="QPs of the secondary large-batch leg (1-GPU runs; 0 = skip)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave"])
+    ap.add_argument("--argmin", default="separate", choices=["fused", "separate"],
+                    help="fused: one qpb_solve_best call per step; separate: qpb_solve + qpb_argmin calls")
     ap.add_argument("--tol", type=float, default=1e-6)
     ap.add_argument("--exact", action="store_true", help="bench the bit-faithful kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -112,30 +114,39 @@ def cpu_baseline(seed, sample, passes, tol):
                 mean_iters=float(iters.mean()), optimal_frac=float((flags == 0).mean()))
 
 
-def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True):
+def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, argmin="fused"):
     """Timed loop of `steps` steps (solve + argmin [+ all_gather]) on resident
     inputs.  Returns (wall seconds max over ranks, mean kernel ms max over
     ranks, outputs, gathered winners)."""
     import torch
     import torch.distributed as dist
-    from apf_quadruped_amd.batch import argmin_launcher
     from apf_quadruped_amd.shard import shard_range
     host = make_shard(plan, seed, shard_range(rank, world, B)[0], B)
     vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
     del host
     out = plan.alloc_outputs(B, device=dev)
-    best = torch.empty(2, dtype=torch.float64, device=dev)
+    best = torch.zeros(2, dtype=torch.float64, device=dev)     # {fval, index}
     gathered = torch.empty(2 * world, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
-    solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream)
-    amin = argmin_launcher(out["fval"], out["flag"], best, stream=stream)
+    # one step = solve + argmin (HIP events time the solve kernel alone)
+    if argmin == "fused":
+        solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream, best=best)
+        post = lambda: None
+    else:
+        from apf_quadruped_amd.batch import argmin_launcher
+        solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream)
+        post = argmin_launcher(out["fval"], out["flag"], best, stream=stream)
     coll = gather and world > 1
+
+    def exchange():
+        # 16 B per rank; async so step i's gather overlaps step i+1's solve
+        return dist.all_gather_into_tensor(gathered, best, async_op=True)
 
     for _ in range(warmup):
         solve()
-        amin()
+        post()
         if coll:
-            dist.all_gather_into_tensor(gathered, best)
+            exchange().wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -143,13 +154,16 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True):
     # kernel duration: HIP events on the launch stream, around every solve
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
+    work = None
     for i in range(steps):
         ev[i][0].record(stream)
         solve()
         ev[i][1].record(stream)
-        amin()
+        post()
         if coll:
-            dist.all_gather_into_tensor(gathered, best)
+            work = exchange()
+    if work is not None:
+        work.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -160,7 +174,7 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True):
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-    return elapsed, kern_ms, out, gathered
+    return elapsed, kern_ms, out, (gathered if coll else best.reshape(1, 2))
 
 
 def traffic_for(kname, B):
@@ -193,7 +207,8 @@ def main():
     plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=args.exact, kernel=args.kernel)
     plan.compile()
     B = args.batch
-    elapsed, kern_ms, out, gathered = run_leg(plan, B, args.steps, args.warmup, args.tol, dev, rank, world, seed)
+    elapsed, kern_ms, out, gathered = run_leg(plan, B, args.steps, args.warmup, args.tol, dev, rank, world, seed,
+                                              argmin=args.argmin)
     kname = plan.kernel_name(B)
     flags = out["flag"].cpu().numpy()
     iters = out["iters"].cpu().numpy()

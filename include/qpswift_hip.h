@@ -106,6 +106,16 @@ int  qpb_solve(qpb_plan *plan, long B,
                int *flag, int *iters, double *fval, double *stats,
                void *stream);
 
+/* qpb_solve followed by qpb_argmin into best (DEVICE, >= 2 doubles; receives
+ * {fval, index}): one call per control step. */
+int  qpb_solve_best(qpb_plan *plan, long B,
+                    const double *P, const double *A, const double *G,
+                    const double *c, const double *h, const double *b,
+                    const qpb_settings *st,
+                    double *x, double *y, double *z, double *s,
+                    int *flag, int *iters, double *fval, double *stats,
+                    double *best, void *stream);
+
 /* Lowest-fval optimal QP of a batch (device-side reduction): writes
  * {fval, index} of the minimum over q with flag[q] == 0 (ties -> lowest index;
  * none -> {+inf, -1}) to out2 (device, 2 doubles; the index as a double). */

@@ -211,3 +211,28 @@ def test_argmin_device_reduction():
     flg = torch.zeros(100003, dtype=torch.int32, device="cuda")
     r = argmin(big, flg).cpu().numpy()
     assert r[1] == float(torch.argmin(big).item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["lane", "wave"])
+def test_solve_best_fused_argmin(kernel):
+    """qpb_solve_best == qpb_solve + qpb_argmin, repeatedly, for ragged batch sizes
+    (1 and 1024 take the single-block argmin, 3000 too; 100003 the two-stage one)."""
+    import torch
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan, argmin
+    for B in (1, 100, 1024, 3000):
+        d = W.contact_force_qp(0xD06B07 + 13, np.arange(B))
+        plan = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0], kernel=kernel)
+        vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"],
+                                                                    d["b"]).items()}
+        out = plan.alloc_outputs(B)
+        best = torch.zeros(4, dtype=torch.float64, device="cuda")
+        go = plan.launcher(vals, out, B, best=best)
+        for _ in range(3):
+            best[:2] = -7.0
+            go()
+            torch.cuda.synchronize()
+            ref = argmin(out["fval"], out["flag"]).cpu().numpy()
+            got = best.cpu().numpy()
+            assert got[0] == ref[0] and got[1] == ref[1], (kernel, B, got, ref)
