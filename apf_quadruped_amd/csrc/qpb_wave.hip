@@ -32,11 +32,11 @@ struct qpb_args {
 };
 
 // tuning knobs (defaults = measured best; scripts/sweep.py "wave:KNOB=V,...")
-#ifndef QPB_W_GG
-#define QPB_W_GG 1        // 1: G(r,i)G(r,j) products in registers; 0: recompute from LDS
+#ifndef QPB_W_GG           // 1: G(r,i)G(r,j) products in registers; 0: recompute from LDS
+#define QPB_W_GG (QPB_NNZG <= 48)
 #endif
-#ifndef QPB_W_PROW
-#define QPB_W_PROW 1      // 1: this lane's row of P in registers; 0: read from LDS
+#ifndef QPB_W_REGS         // 1: this lane's slices of P, A, G in registers; 0: read LDS in place
+#define QPB_W_REGS (QPB_NX <= 16 && QPB_NZ <= 32)
 #endif
 #ifndef QPB_W_TIMING
 #define QPB_W_TIMING 0    // 1: phase timestamps (s_memtime) of QP 0 of each tile into stats (debug)
@@ -61,8 +61,9 @@ struct qpb_args {
 #define OFF_T (((OFF_B + NY) + 1) & ~1)
 #define OFF_V (OFF_T + ((NX * NX + 1) & ~1))
 #define LDS_WAVE (OFF_V + NV2)
+#define ZC ((NZ + 63) / 64)          // z rows per lane (lane r holds r, r + 64, ...)
 #define ROWS_X ((NX + 15) / 16)
-#define ROWS_Z ((NZ + 15) / 16)
+#define ROWS_Z (ZC > 1 ? 4 : (NZ + 15) / 16)
 #define ROWS_Y ((NY1 + 15) / 16)
 
 static __device__ __forceinline__ double qpb_rcp(double v) {
@@ -168,10 +169,16 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     double *__restrict__ Ls = qpb_lds + wv * LDS_WAVE;
     const long tile = q >> 6;
     const int ql = (int)(q & 63);
-    const bool isx = lane < NX, isz = lane < NZ, isy = lane < NY;
+    const bool isx = lane < NX, isy = lane < NY;
     const int ix = isx ? lane : NX - 1;
-    const int iz = isz ? lane : NZ - 1;
     const int iy = isy ? lane : (NY > 0 ? NY - 1 : 0);
+    bool isz[ZC];
+    int iz[ZC];
+#pragma unroll
+    for (int t = 0; t < ZC; t++) {
+        isz[t] = lane + 64 * t < NZ;
+        iz[t] = isz[t] ? lane + 64 * t : NZ - 1;
+    }
     constexpr double RDY = 1.0 / -1e-7;      // y pivots: D = 0 regularised to -1e-7
 
     QPB_TS(0);
@@ -209,12 +216,15 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         }
 #endif
     }
-    const double cx0 = isx ? a.c[tile * (NX * 64) + lane * 64 + ql] : 0.0;
-    const double hz0 = isz ? a.h[tile * (NZ * 64) + lane * 64 + ql] : 0.0;
-#if NY > 0
-    const double by0 = isy ? a.b[tile * (NY * 64) + lane * 64 + ql] : 0.0;
-#endif
+    const double cx = isx ? a.c[tile * (NX * 64) + lane * 64 + ql] : 0.0;
+    double hz[ZC];
 #pragma unroll
+    for (int t = 0; t < ZC; t++) hz[t] = isz[t] ? a.h[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql] : 0.0;
+#if NY > 0
+    const double by = isy ? a.b[tile * (NY * 64) + lane * 64 + ql] : 0.0;
+#else
+    const double by = 0.0;
+#endif
     for (int k = lane; k < OFF_C; k += 64) Ls[k] = 0.0;
     qpb_wsync();
 #pragma unroll
@@ -232,73 +242,75 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     const double *Pd = Ls, *Ad = Ls + OFF_A, *Gd = Ls + OFF_G;
     double *Tx = Ls + OFF_T, *Vb = Ls + OFF_V;
     // Pd[j*NX+i] = P(i,j) as given; Ad[j*NY+l] = A(l,j); Gd[j*NZ+r] = G(r,j)
-    const double cx = cx0, hz = hz0;
-#if NY > 0
-    const double by = by0;
-#else
-    const double by = 0.0;
-#endif
-    // this lane's slices of the (constant) matrices, kept in registers
-    double Prow[NX], Grow[NX], Arow[NX], Gcol[NZ], Acol[NY1], H0[NX];
+
+    // this lane's slices of the (constant) matrices: registers when small (REGS)
+    double Prow[QPB_W_REGS ? NX : 1], Grow[QPB_W_REGS ? ZC * NX : 1], Arow[QPB_W_REGS ? NX : 1];
+    double Gcol[QPB_W_REGS ? NZ : 1], Acol[QPB_W_REGS ? NY1 : 1];
+    if constexpr (QPB_W_REGS) {
 #pragma unroll
-    for (int j = 0; j < NX; j++) {
-        Prow[j] = QPB_W_PROW ? Pd[j * NX + ix] : 0.0;      // P(i, j), residual (full P)
-        Grow[j] = Gd[j * NZ + iz];                         // G(r, j)
-        Arow[j] = NY > 0 ? Ad[j * NY + iy] : 0.0;          // A(l, j)
+        for (int j = 0; j < NX; j++) {
+            Prow[j] = Pd[j * NX + ix];
+            Arow[j] = NY > 0 ? Ad[j * NY + iy] : 0.0;
+#pragma unroll
+            for (int t = 0; t < ZC; t++) Grow[t * NX + j] = Gd[j * NZ + iz[t]];
+        }
+#pragma unroll
+        for (int r = 0; r < NZ; r++) Gcol[r] = Gd[ix * NZ + r];
+#pragma unroll
+        for (int l = 0; l < NY1; l++) Acol[l] = NY > 0 ? Ad[ix * NY + l] : 0.0;
     }
-#pragma unroll
-    for (int r = 0; r < NZ; r++) Gcol[r] = Gd[ix * NZ + r];   // G(r, i)
-#pragma unroll
-    for (int l = 0; l < NY1; l++) Acol[l] = NY > 0 ? Ad[ix * NY + l] : 0.0;   // A(l, i)
+    auto PR = [&](int j) { if constexpr (QPB_W_REGS) return Prow[j]; else return Pd[j * NX + ix]; };   // P(i, j)
+    auto GR = [&](int t, int j) { if constexpr (QPB_W_REGS) return Grow[t * NX + j]; else return Gd[j * NZ + iz[t]]; };  // G(r, j)
+    auto AR = [&](int j) { if constexpr (QPB_W_REGS) return Arow[j]; else return Ad[j * NY + iy]; };   // A(l, j)
+    auto GC = [&](int r) { if constexpr (QPB_W_REGS) return Gcol[r]; else return Gd[ix * NZ + r]; };   // G(r, i)
+    auto AC = [&](int l) { if constexpr (QPB_W_REGS) return Acol[l]; else return Ad[ix * NY + l]; };   // A(l, i)
+
     // H0 = P(upper, symmetrised) + 1e7 A'A: the y leaves (ldl.c:303-318 for x rows)
+    double H0[NX];
 #pragma unroll
     for (int j = 0; j < NX; j++) {
         double v = ix <= j ? Pd[j * NX + ix] : Pd[ix * NX + j];
 #pragma unroll
-        for (int l = 0; l < NY; l++) v = __builtin_fma(Acol[l], -RDY * Ad[j * NY + l], v);
+        for (int l = 0; l < NY; l++) v = __builtin_fma(AC(l), -RDY * Ad[j * NY + l], v);
         H0[j] = v;
     }
     // G(r,i) G(r,j) for every structural G(r,j): the z leaves' updates of row i
     double GG[QPB_W_GG ? QPB_NNZG : 1];
-    if (QPB_W_GG) {
+    if constexpr (QPB_W_GG) {
         int e = 0;
 #pragma unroll
         for (int r = 0; r < NZ; r++)
 #pragma unroll
             for (int j = 0; j < NX; j++)
-                if (qpb_Gnz[r][j]) GG[QPB_W_GG ? e++ : 0] = Gcol[r] * Gd[j * NZ + r];
+                if (qpb_Gnz[r][j]) GG[e++] = GC(r) * Gd[j * NZ + r];
     }
 
-    // every lane gets the vector held by lanes 0..K-1 (one LDS store, wide loads)
-    auto gather = [&](double v, auto kc, int off, double *out) {
-        constexpr int K = decltype(kc)::value;
-        if (lane < K) Vb[off + lane] = v;
-        qpb_wsync();
-#pragma unroll
-        for (int k = 0; k < K; k++) out[k] = Vb[off + k];
-        qpb_wsync();
-    };
-
-    double H[NX], Lt[NX], rDx = 0.0, w = 0.0;
+    double H[NX], Lt[NX], rDx = 0.0, w[ZC];
     // factor: H = H0 + G' diag(w) G, then dense LDL' of H (right-looking)
-    auto factor = [&](double wz) {
-        w = wz;
-        double wb[NZ];
-        gather(wz, qpb_ic<NZ>{}, 0, wb);
+    auto factor = [&](const double *wz) {
+#pragma unroll
+        for (int t = 0; t < ZC; t++) {
+            w[t] = wz[t];
+            if (isz[t]) Vb[lane + 64 * t] = wz[t];
+        }
+        qpb_wsync();
 #pragma unroll
         for (int j = 0; j < NX; j++) H[j] = H0[j];
         {
             int e = 0;
 #pragma unroll
-            for (int r = 0; r < NZ; r++)
+            for (int r = 0; r < NZ; r++) {
+                const double wr = Vb[r];
 #pragma unroll
                 for (int j = 0; j < NX; j++)
                     if (qpb_Gnz[r][j]) {
-                        if (QPB_W_GG) H[j] = __builtin_fma(GG[e], wb[r], H[j]);
-                        else H[j] = __builtin_fma(Gcol[r] * wb[r], Gd[j * NZ + r], H[j]);
+                        if constexpr (QPB_W_GG) H[j] = __builtin_fma(GG[e], wr, H[j]);
+                        else H[j] = __builtin_fma(GC(r) * wr, Gd[j * NZ + r], H[j]);
                         e++;
                     }
+            }
         }
+        qpb_wsync();
         qpb_for<0, NX>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             const double rd = qpb_rcp_reg(qpb_xb<k>(H[k]));
@@ -322,22 +334,21 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     };
 
     // solve K [dx; dy; dz] = [bx; byv; bz] with the current factor
-    auto solve = [&](double bx, double byv, double bz, double &dx, double &dy, double &dz) {
-        double vb[NZ + NY1];
-        if (lane < NZ) Vb[lane] = w * bz;             // -bz / D_z
-        if (lane < NY) Vb[NZ + lane] = -RDY * byv;    // -by / D_y
-        qpb_wsync();
+    auto solve = [&](double bx, double byv, const double *bz, double &dx, double &dy, double *dz) {
 #pragma unroll
-        for (int k = 0; k < NZ + NY; k++) vb[k] = Vb[k];
+        for (int t = 0; t < ZC; t++)
+            if (isz[t]) Vb[lane + 64 * t] = w[t] * bz[t];    // -bz / D_z
+        if (lane < NY) Vb[NZ + lane] = -RDY * byv;        // -by / D_y
         qpb_wsync();
         double ta[QPB_W_SPLIT];
 #pragma unroll
         for (int k = 0; k < QPB_W_SPLIT; k++) ta[k] = k ? 0.0 : bx;
 #pragma unroll
-        for (int r = 0; r < NZ; r++) ta[r % QPB_W_SPLIT] = __builtin_fma(Gcol[r], vb[r], ta[r % QPB_W_SPLIT]);
+        for (int r = 0; r < NZ; r++) ta[r % QPB_W_SPLIT] = __builtin_fma(GC(r), Vb[r], ta[r % QPB_W_SPLIT]);
 #pragma unroll
         for (int l = 0; l < NY; l++)
-            ta[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(Acol[l], vb[NZ + l], ta[(NZ + l) % QPB_W_SPLIT]);
+            ta[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(AC(l), Vb[NZ + l], ta[(NZ + l) % QPB_W_SPLIT]);
+        qpb_wsync();
         double t = ta[0];
 #pragma unroll
         for (int k = 1; k < QPB_W_SPLIT; k++) t += ta[k];
@@ -351,44 +362,81 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             t = __builtin_fma(-Lt[k], qpb_xb<k>(t), t);
         });
         dx = t;
-        double xb[NX];
-        gather(t, qpb_ic<NX>{}, 0, xb);
-        double gza[QPB_W_SPLIT], gya[QPB_W_SPLIT];
+        if (lane < NX) Vb[lane] = t;
+        qpb_wsync();
+        double gza[ZC][QPB_W_SPLIT], gya[QPB_W_SPLIT];
 #pragma unroll
-        for (int k = 0; k < QPB_W_SPLIT; k++) gza[k] = gya[k] = 0.0;
+        for (int k = 0; k < QPB_W_SPLIT; k++) {
+            gya[k] = 0.0;
+#pragma unroll
+            for (int u = 0; u < ZC; u++) gza[u][k] = 0.0;
+        }
 #pragma unroll
         for (int j = 0; j < NX; j++) {
-            gza[j % QPB_W_SPLIT] = __builtin_fma(Grow[j], xb[j], gza[j % QPB_W_SPLIT]);
-            gya[j % QPB_W_SPLIT] = __builtin_fma(Arow[j], xb[j], gya[j % QPB_W_SPLIT]);
-        }
-        double gz = gza[0], gy = gya[0];
+            const double xj = Vb[j];
 #pragma unroll
-        for (int k = 1; k < QPB_W_SPLIT; k++) { gz += gza[k]; gy += gya[k]; }
-        dz = -w * (bz - gz);
+            for (int u = 0; u < ZC; u++) gza[u][j % QPB_W_SPLIT] = __builtin_fma(GR(u, j), xj, gza[u][j % QPB_W_SPLIT]);
+            if constexpr (NY > 0) gya[j % QPB_W_SPLIT] = __builtin_fma(AR(j), xj, gya[j % QPB_W_SPLIT]);
+        }
+        qpb_wsync();
+        double gy = gya[0];
+#pragma unroll
+        for (int k = 1; k < QPB_W_SPLIT; k++) gy += gya[k];
+#pragma unroll
+        for (int u = 0; u < ZC; u++) {
+            double gz = gza[u][0];
+#pragma unroll
+            for (int k = 1; k < QPB_W_SPLIT; k++) gz += gza[u][k];
+            dz[u] = -w[u] * (bz[u] - gz);
+        }
         dy = RDY * (byv - gy);
+    };
+
+    // lane sums / maxima over this lane's z slots (0 / neutral outside the range)
+    auto zsum = [&](auto f) {
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < ZC; t++) v += isz[t] ? f(t) : 0.0;
+        return qpb_rsum<ROWS_Z>(v);
+    };
+    auto zmax = [&](auto f, double neutral) {
+        double v = neutral;
+#pragma unroll
+        for (int t = 0; t < ZC; t++) v = __builtin_fmax(v, isz[t] ? f(t) : neutral);
+        return qpb_rmax<ROWS_Z>(v);
     };
 
     QPB_TS(1);
     // ---- kkt_initialize (Auxilary.c:992-1089): K with -I, rhs [-c; b; h]
-    factor(1.0);
-    QPB_TS(2);
-    double x, y, s, z;
+    double x, y, s[ZC], z[ZC];
     {
-        double dzi;
+        double one[ZC], dzi[ZC];
+#pragma unroll
+        for (int t = 0; t < ZC; t++) one[t] = 1.0;
+        factor(one);
+        QPB_TS(2);
         solve(-cx, by, hz, x, y, dzi);
         QPB_TS(3);
-        double xb[NX];
-        gather(x, qpb_ic<NX>{}, 0, xb);
-        double gx = 0.0;
+        if (lane < NX) Vb[lane] = x;
+        qpb_wsync();
+        double zi[ZC];
 #pragma unroll
-        for (int j = 0; j < NX; j++) gx = __builtin_fma(Grow[j], xb[j], gx);
-        const double zi = hz - gx;
-        const double lo = -qpb_rmax<ROWS_Z>(isz ? -zi : -1e300);
-        const double hi = qpb_rmax<ROWS_Z>(isz ? zi : -1e300);
+        for (int t = 0; t < ZC; t++) {
+            double gx = 0.0;
+#pragma unroll
+            for (int j = 0; j < NX; j++) gx = __builtin_fma(GR(t, j), Vb[j], gx);
+            zi[t] = hz[t] - gx;
+        }
+        qpb_wsync();
+        const double lo = -zmax([&](int t) { return -zi[t]; }, -1e300);
+        const double hi = zmax([&](int t) { return zi[t]; }, -1e300);
         const double sh = -lo;
-        s = sh < 0 ? zi : zi + (1 + sh);
-        z = hi < 0 ? -zi : -zi + (1 + hi);
-        if (!isz) { s = 1.0; z = 1.0; }
+#pragma unroll
+        for (int t = 0; t < ZC; t++) {
+            s[t] = sh < 0 ? zi[t] : zi[t] + (1 + sh);
+            z[t] = hi < 0 ? -zi[t] : -zi[t] + (1 + hi);
+            if (!isz[t]) { s[t] = 1.0; z[t] = 1.0; }
+        }
         if (!isx) x = 0.0;
         if (!isy) y = 0.0;
     }
@@ -403,86 +451,105 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         if (it >= a.maxit) { flag = 2; break; }
         QPB_TS(8 + 8 * it);
         // residuals (Auxilary.c:745-786), objective (Auxilary.c:1133-1141)
-        double vb[NV];
         if (lane < NX) Vb[lane] = x;
-        if (lane < NZ) Vb[NX + lane] = z;
+#pragma unroll
+        for (int t = 0; t < ZC; t++)
+            if (isz[t]) Vb[NX + lane + 64 * t] = z[t];
         if (lane < NY) Vb[NX + NZ + lane] = y;
         qpb_wsync();
+        double tp = 0.0, ry = by, rz[ZC], rx = -cx;
 #pragma unroll
-        for (int k = 0; k < NV; k++) vb[k] = Vb[k];
-        qpb_wsync();
-        double tp = 0.0, ry = by, rz = hz - s, rx = -cx;
+        for (int t = 0; t < ZC; t++) rz[t] = hz[t] - s[t];
 #pragma unroll
         for (int j = 0; j < NX; j++) {
-            tp = __builtin_fma(-(QPB_W_PROW ? Prow[j] : Pd[j * NX + ix]), vb[j], tp);
-            rz = __builtin_fma(-Grow[j], vb[j], rz);
-            ry = __builtin_fma(-Arow[j], vb[j], ry);
+            const double xj = Vb[j];
+            tp = __builtin_fma(-PR(j), xj, tp);
+#pragma unroll
+            for (int t = 0; t < ZC; t++) rz[t] = __builtin_fma(-GR(t, j), xj, rz[t]);
+            if constexpr (NY > 0) ry = __builtin_fma(-AR(j), xj, ry);
         }
         {
             double ra[QPB_W_SPLIT];
 #pragma unroll
             for (int k = 0; k < QPB_W_SPLIT; k++) ra[k] = k ? 0.0 : rx;
 #pragma unroll
-            for (int r = 0; r < NZ; r++) ra[r % QPB_W_SPLIT] = __builtin_fma(-Gcol[r], vb[NX + r], ra[r % QPB_W_SPLIT]);
+            for (int r = 0; r < NZ; r++) ra[r % QPB_W_SPLIT] = __builtin_fma(-GC(r), Vb[NX + r], ra[r % QPB_W_SPLIT]);
 #pragma unroll
             for (int l = 0; l < NY; l++)
-                ra[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(-Acol[l], vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
+                ra[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(-AC(l), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
             rx = ra[0];
 #pragma unroll
             for (int k = 1; k < QPB_W_SPLIT; k++) rx += ra[k];
         }
+        qpb_wsync();
         rx += tp;
         fval = qpb_rsum<ROWS_X>(isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0);
         st_rx = __builtin_sqrt(qpb_rsum<ROWS_X>(isx ? rx * rx : 0.0));
         st_ry = NY > 0 ? __builtin_sqrt(qpb_rsum<ROWS_Y>(isy ? ry * ry : 0.0)) : 0.0;
-        st_rz = __builtin_sqrt(qpb_rsum<ROWS_Z>(isz ? rz * rz : 0.0));
-        const double sz = qpb_rsum<ROWS_Z>(isz ? s * z : 0.0);
+        st_rz = __builtin_sqrt(zsum([&](int t) { return rz[t] * rz[t]; }));
+        const double sz = zsum([&](int t) { return s[t] * z[t]; });
         st_mu = sz * (1.0 / NZ);
         if (st_rx < a.tol && st_rz < a.tol && (NY == 0 || st_ry < a.tol) && st_mu < a.abstol) { flag = 0; break; }
         QPB_TS(9 + 8 * it);
         const double mu = st_mu;
         const bool pc = sigma > a.sigma_d;
-        const double rzi = qpb_rcp(z);
-        // updatekktmatrix (Auxilary.c:211-215): z pivot -s/z, regularised (ldl.c:319-320)
-        factor(isz ? -qpb_rcp_reg(-s * rzi) : 0.0);
+        double rzi[ZC], wz[ZC];
+#pragma unroll
+        for (int t = 0; t < ZC; t++) {
+            rzi[t] = qpb_rcp(z[t]);
+            // updatekktmatrix (Auxilary.c:211-215): z pivot -s/z, regularised (ldl.c:319-320)
+            wz[t] = isz[t] ? -qpb_rcp_reg(-s[t] * rzi[t]) : 0.0;
+        }
+        factor(wz);
         QPB_TS(10 + 8 * it);
         if (!pc) sigma = a.sigma_d;
-        double cc = sigma * mu;
-        double dx, dy, dz, dsl;
+        double cc[ZC];
+#pragma unroll
+        for (int t = 0; t < ZC; t++) cc[t] = sigma * mu;
+        double dx, dy, dz[ZC], dsl[ZC], bz[ZC];
         auto step_length = [&]() {
             // alpha = min over d < 0 of v/(-d) == 1 / max(-d/v); 1 if none (Auxilary.c:359-393)
-            const double bp = qpb_rmax<ROWS_Z>(isz ? -dsl * __builtin_amdgcn_rcp(s) : 0.0);
-            const double bd = qpb_rmax<ROWS_Z>(isz ? -dz * rzi : 0.0);
+            const double bp = zmax([&](int t) { return -dsl[t] * __builtin_amdgcn_rcp(s[t]); }, 0.0);
+            const double bd = zmax([&](int t) { return -dz[t] * rzi[t]; }, 0.0);
             ap = bp > 1e-10 ? __builtin_amdgcn_rcp(bp) : 1.0;
             ad = bd > 1e-10 ? __builtin_amdgcn_rcp(bd) : 1.0;
         };
         if (pc) {
             // predictor (kktsolve_1, Auxilary.c:471-515): ds = -s.*z
-            solve(rx, ry, rz + s, dx, dy, dz);
+#pragma unroll
+            for (int t = 0; t < ZC; t++) bz[t] = rz[t] + s[t];
+            solve(rx, ry, bz, dx, dy, dz);
             QPB_TS(11 + 8 * it);
-            dsl = -s * __builtin_fma(dz, rzi, 1.0);
+#pragma unroll
+            for (int t = 0; t < ZC; t++) dsl[t] = -s[t] * __builtin_fma(dz[t], rzi[t], 1.0);
             step_length();
-            const double rho = qpb_rsum<ROWS_Z>(isz ? (s + ap * dsl) * (z + ad * dz) : 0.0) * qpb_rcp(sz);   // formrho
+            const double rho = zsum([&](int t) { return (s[t] + ap * dsl[t]) * (z[t] + ad * dz[t]); }) * qpb_rcp(sz);   // formrho
             const double r1 = 1 > rho ? rho : 1;
             const double cube = r1 * r1 * r1;
             sigma = a.sigma_d < cube ? cube : a.sigma_d;
-            cc = __builtin_fma(-dsl, dz, sigma * mu);
+#pragma unroll
+            for (int t = 0; t < ZC; t++) cc[t] = __builtin_fma(-dsl[t], dz[t], sigma * mu);
             QPB_TS(12 + 8 * it);
         }
         // corrector / centering (kktsolve_2, Auxilary.c:524-564)
-        solve(rx, ry, __builtin_fma(-cc, rzi, rz + s), dx, dy, dz);
+#pragma unroll
+        for (int t = 0; t < ZC; t++) bz[t] = __builtin_fma(-cc[t], rzi[t], rz[t] + s[t]);
+        solve(rx, ry, bz, dx, dy, dz);
         QPB_TS(13 + 8 * it);
-        dsl = __builtin_fma(__builtin_fma(-s, dz, cc), rzi, -s);
+#pragma unroll
+        for (int t = 0; t < ZC; t++) dsl[t] = __builtin_fma(__builtin_fma(-s[t], dz[t], cc[t]), rzi[t], -s[t]);
         step_length();
         QPB_TS(14 + 8 * it);
         ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
         ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
         if (isx) x = __builtin_fma(dx, ap, x);
         if (isy) y = __builtin_fma(dy, ad, y);
-        if (isz) {
-            s = __builtin_fma(dsl, ap, s);
-            z = __builtin_fma(dz, ad, z);
-        }
+#pragma unroll
+        for (int t = 0; t < ZC; t++)
+            if (isz[t]) {
+                s[t] = __builtin_fma(dsl[t], ap, s[t]);
+                z[t] = __builtin_fma(dz[t], ad, z[t]);
+            }
         it++;
     }
     QPB_TS(370);
@@ -491,10 +558,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #if NY > 0
     if (isy) a.y[tile * (NY * 64) + lane * 64 + ql] = y;
 #endif
-    if (isz) {
-        a.z[tile * (NZ * 64) + lane * 64 + ql] = z;
-        a.s[tile * (NZ * 64) + lane * 64 + ql] = s;
-    }
+#pragma unroll
+    for (int t = 0; t < ZC; t++)
+        if (isz[t]) {
+            a.z[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql] = z[t];
+            a.s[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql] = s[t];
+        }
     if (lane == 0) {
         a.flag[q] = flag;
         a.iters[q] = (int)it;

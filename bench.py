@@ -53,13 +53,14 @@ def parse():
     return ap.parse_args()
 
 
-def make_shard(plan, seed, q0, B, chunk=65536):
-    """Synthetic C1 QPs [q0, q0+B) packed in the plan's tiled layout (host)."""
+def make_shard(plan, seed, q0, B, chunk=65536, gen=None):
+    """Synthetic QPs [q0, q0+B) (C1 unless `gen(ids)` is given) packed in the
+    plan's tiled layout (host)."""
     from apf_quadruped_amd import workloads as W
     parts = {k: [] for k in ("P", "A", "G", "c", "h", "b")}
     for s in range(0, B, chunk):
         ids = np.arange(q0 + s, q0 + min(B, s + chunk))
-        d = W.contact_force_qp(seed, ids)
+        d = gen(ids) if gen is not None else W.contact_force_qp(seed, ids)
         v = plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"])
         for k in parts:
             parts[k].append(v[k])

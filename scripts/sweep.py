@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--maxit", type=int, default=100)
+    ap.add_argument("--shape", default="c1", choices=["c1", "c30"])
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -29,28 +30,34 @@ def main():
     from apf_quadruped_amd.batch import Plan
     import bench
     torch.cuda.set_device(0)
-    d0 = plans.standard_qp("c1")
     seed = plans.SEED + 1
-    base = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0])
-    host = bench.make_shard(base, seed, 0, a.batch)
+    if a.shape == "c1":
+        gen = lambda ids: W.contact_force_qp(seed, ids)
+        n, m, p = 12, 20, 6
+    else:
+        gen = lambda ids: W.controller_qp(seed, ids)
+        n, m, p = 30, 68, 18
+    d0 = gen(np.arange(1))
+    base = Plan.from_dense(n, m, p, d0["P"][0], d0["A"][0], d0["G"][0], kernel="wave" if a.shape == "c30" else "auto")
+    host = bench.make_shard(base, seed, 0, a.batch, gen=gen)
     vals = {k: torch.from_numpy(v).cuda() for k, v in host.items()}
     plans_ = {}
     for v in a.variants:
         if v == "exact":
             os.environ.pop("QPB_WG", None); os.environ.pop("QPB_LDS", None)
-            plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=True)
+            plans_[v] = Plan.from_dense(n, m, p, d0["P"][0], d0["A"][0], d0["G"][0], exact=True)
         elif v.startswith("wave"):
             # "wave" or "wave:KNOB=V,KNOB=V" (QPB_W_* knobs of qpb_wave.hip)
             opts = v.split(":", 1)[1].replace(",", " ") if ":" in v else ""
             os.environ["QPB_WAVE_OPTS"] = " ".join("QPB_W_" + o for o in opts.split())
-            plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], kernel="wave")
+            plans_[v] = Plan.from_dense(n, m, p, d0["P"][0], d0["A"][0], d0["G"][0], kernel="wave")
             plans_[v].compile()
             os.environ.pop("QPB_WAVE_OPTS", None)
         else:
             parts = v.split(":")
             os.environ["QPB_WG"], os.environ["QPB_LDS"] = parts[0], parts[1]
             os.environ["QPB_PARKZ"] = parts[2] if len(parts) > 2 else "1"
-            plans_[v] = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], kernel="lane")
+            plans_[v] = Plan.from_dense(n, m, p, d0["P"][0], d0["A"][0], d0["G"][0], kernel="lane")
         t0 = time.time(); plans_[v].compile(); ct = time.time() - t0
         print(f"compiled {v} in {ct:.1f}s", file=sys.stderr)
     for k in ("QPB_WG", "QPB_LDS", "QPB_PARKZ"):
@@ -58,7 +65,7 @@ def main():
     from oracle_py import Oracle
     o = Oracle()
     ids = np.arange(0, a.batch, a.batch // 16)
-    dd = W.contact_force_qp(seed, ids)
+    dd = gen(ids)
     Pc, Ac, Gc = W.to_colmajor(dd["P"]), W.to_colmajor(dd["A"]), W.to_colmajor(dd["G"])
     times = {v: [] for v in a.variants}
     outs = {}
@@ -93,7 +100,7 @@ def main():
         err = 0.0
         for k, q in enumerate(ids):
             perm = pl.wave_perm() if v.startswith("wave") else pl.perm
-            ref = o.solve_dense(12, 20, 6, Pc[k], Ac[k], Gc[k], dd["c"][k], dd["h"][k], dd["b"][k], perm=perm,
+            ref = o.solve_dense(n, m, p, Pc[k], Ac[k], Gc[k], dd["c"][k], dd["h"][k], dd["b"][k], perm=perm,
                                 maxit=a.maxit)
             err = max(err, float(np.max(np.abs(ref["x"] - res["x"][q]))))
         ms = float(np.median(times[v]))

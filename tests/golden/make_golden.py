@@ -3,7 +3,8 @@
 Run in the build container (needs oracle/_ref/libqpswift_ref.so, which
 `make -C oracle ref` compiles from /root/reference's own C sources):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py          # every case
+    python tests/golden/make_golden.py c30      # only the controller-shape cases
 
 Every case calls the reference exactly as dogbot_controller does
 (QP_SETUP_dense -> options override -> QP_SOLVE, main.cpp:1649-1656) and records
@@ -58,8 +59,20 @@ def save(name, **arrs):
     print(f"{name}: {os.path.getsize(path) / 1024:.1f} KiB")
 
 
-def main():
+def c30_cases(ref):
+    """Controller-shape stance QP 30/68/18 (main.cpp:1471-1647),
+    at the default tolerance and at the controller's 1e-2 (main.cpp:1651-1652)."""
+    ids = np.arange(8)
+    d = W.controller_qp(SEED_BASE + 30, ids)
+    save("c30_tol1e-6", seed=SEED_BASE + 30, **dense_case(ref, d, ids, 1e-6))
+    save("c30_tol1e-2", seed=SEED_BASE + 30, **dense_case(ref, d, ids, 1e-2))
+
+
+def main(only=None):
     ref = Reference()
+    if only == "c30":
+        c30_cases(ref)
+        return
     # C1: 12-var / 20-ineq / 6-eq contact-force QP (configs 1, 2, 5).
     ids = np.arange(64)
     d = W.contact_force_qp(SEED_BASE + 1, ids)
@@ -92,6 +105,7 @@ def main():
     save("edge_zero_g_row", seed=SEED_BASE + 6, **dense_case(ref, dz, ids8, 1e-6))
     # Sparse QP_SETUP with sigma_d > 0: the pure-centering branch (qpSWIFT.c:572-579).
     sparse_cases(ref)
+    c30_cases(ref)
 
 
 def to_csc(M):
@@ -126,4 +140,4 @@ def sparse_cases(ref):
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else None)

@@ -113,13 +113,27 @@ def test_exact_kernel_matches_oracle_with_own_ordering(oracle):
         assert r["iters"][q] == o["iters"] and r["fval"][q] == o["fval"]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c30_tol1e-6"])
+def test_wave_kernel_controller_shape_vs_reference(name):
+    """Controller-shape QPs (30/68/18, N = 116: two z rows per lane, x block over
+    two 16-lane rows) on the wave kernel vs the reference golden vectors."""
+    g = golden(name)
+    _, r = _solve(g, perm=None, exact=False, p_upper=True, kernel="wave")
+    np.testing.assert_array_equal(r["flag"], g["flag"])
+    for k in ("x", "y", "z", "s"):
+        scale = max(1.0, float(np.abs(g[k]).max()))
+        err = float(np.abs(r[k] - g[k]).max())
+        assert err <= TOL * scale, (name, k, err, scale)
+
+
 def _oracle_perm(plan):
     return plan.wave_perm() if plan.kernel == "wave" else plan.perm
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "c1_noeq", "mixed_stance4", "mixed_trot_blfr",
-                                  "mixed_trot_brfl", "mixed_crawl_blflfr", "c1_maxit3"])
+                                  "mixed_trot_brfl", "mixed_crawl_blflfr", "c1_maxit3", "c30_tol1e-6", "c30_tol1e-2"])
 def test_wave_kernel_matches_oracle_in_its_order(name, oracle):
     """Wave kernel vs the oracle run with the wave kernel's elimination order:
     same factorisation, so agreement is at rounding level (1e-9 relative)."""
