@@ -130,13 +130,6 @@ class Plan:
         L.qpb_plan_source(self._h, buf, size + 1)
         return buf.value.decode()
 
-    def wave_perm(self) -> np.ndarray:
-        """KKT elimination order of the wave kernel: all z rows, all y rows, then x
-        (KKT index order x, y, z as in Auxilary.c:71-181).  The oracle run with
-        this permutation is the wave kernel's arithmetic reference."""
-        n, m, p = self.n, self.m, self.p
-        return np.concatenate([np.arange(n + p, n + p + m), np.arange(n, n + p), np.arange(n)]).astype(np.int64)
-
     def kernel_for(self, B: int) -> str:
         """Which kernel qpb_solve runs for a batch of B ("wave" or "lane")."""
         i = self.info
@@ -145,8 +138,9 @@ class Plan:
         return "lane"
 
     def oracle_perm(self, B: int) -> np.ndarray:
-        """The elimination order the kernel used for a batch of B runs in."""
-        return self.wave_perm() if self.kernel_for(B) == "wave" else self.perm
+        """The KKT permutation the kernels factor with (both kernels follow the
+        plan's permutation; the oracle run with it is their arithmetic reference)."""
+        return self.perm
 
     def wave_source(self) -> str:
         L = _lib.lib()

@@ -262,7 +262,10 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
         return fail(QPB_EINVAL, "QPB_KERNEL_WAVE: " + (plan->gen.exact ? std::string("exact plans use the lane kernel") : why));
     plan->wave_max_batch = 4096;   // measured crossover vs the lane kernel
     if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
-    if (plan->wave_ok) qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
+    if (plan->wave_ok) {
+        plan->wave_wg = qpb::wave_wg_for(plan->pl);
+        qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
+    }
     *out = plan.release();
     return QPB_OK;
 }

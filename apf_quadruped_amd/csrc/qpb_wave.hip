@@ -4,13 +4,17 @@
 // plan's sizes (QPB_NX = n, QPB_NZ = m, QPB_NY = p), its sparsity tables and the
 // kernel name (qpb_wave.cpp).  Algorithm = qpSWIFT's Mehrotra predictor-corrector
 // (qpSWIFT.c:473-644, kkt_initialize Auxilary.c:992-1089) with the KKT LDL'
-// (ldl.c:253-326, same regularisation) in the elimination order
-//     [ all z rows | all y rows | x rows ]
-// z and y rows are leaves: their pivots are the diagonal (-s/z, and 0 -> -1e-7
-// for y, exactly the reference's regularisation), and their elimination adds
-//     H = P + G' diag(z/s) G + 1e7 A'A
-// onto the x block, which is factored densely.  Lanes own rows: lane i holds
-// x_i and row i of H (then of L), lane r holds s_r, z_r, lane l holds y_l.
+// (ldl.c:253-326, same regularisation) of the PLAN'S permutation, reorganised:
+// z and y rows whose neighbours (x rows) all come later in the permutation are
+// leaves -- their row of L is empty and their pivot is the diagonal (-s/z, and
+// 0 -> -1e-7 for y, the reference's regularisation) -- so they are eliminated
+// first, all at once, adding
+//     P + G_L' diag(z/s) G_L + 1e7 A_L'A_L          (L = leaf rows)
+// onto the x block.  Every other row (x, non-leaf y and z) forms a dense block
+// factored right-looking in permutation order, so the pivots, and which of
+// them are regularised, are the reference's when it is given the same
+// permutation.  Lanes own rows: lane d holds dense row d of H (then of L);
+// lane i holds x_i, lane l holds y_l, lane r (+64, ...) holds s_r, z_r.
 // Cross-lane traffic: whole vectors are all-gathered through LDS (one store,
 // wide same-address loads); the sequential dense factor / triangular solves
 // broadcast with DPP row_newbcast (x block within one 16-lane row) or
@@ -50,18 +54,19 @@ struct qpb_args {
 #define NY QPB_NY
 #define NY1 (NY > 0 ? NY : 1)
 #define WPB (QPB_WG / 64)
+#define ND QPB_ND
 #define NV (NX + NZ + NY)
-#define NV2 ((NV + 1) & ~1)
-// per-wave LDS (doubles): Pd[NX*NX] Ad[NY*NX] Gd[NZ*NX] c[NX] h[NZ] b[NY] | Tx[NX*NX] | V[NV2]
+// vector exchange area: x | z | y  (residual gather); solve: bx | by | bz | v | out
+#define VB_SIZE (((2 * NV + NZ + NX) + 1) & ~1)
+// per-wave LDS (doubles): Pd[NX*NX] Ad[NY*NX] Gd[NZ*NX] | Tx[ND*ND] | Vb
 #define OFF_A (NX * NX)
 #define OFF_G (OFF_A + NY * NX)
 #define OFF_C (OFF_G + NZ * NX)
-#define OFF_H (OFF_C + NX)
-#define OFF_B (OFF_H + NZ)
-#define OFF_T (((OFF_B + NY) + 1) & ~1)
-#define OFF_V (OFF_T + ((NX * NX + 1) & ~1))
-#define LDS_WAVE (OFF_V + NV2)
+#define OFF_T ((OFF_C + 1) & ~1)
+#define OFF_V (OFF_T + ((ND * ND + 1) & ~1))
+#define LDS_WAVE (OFF_V + VB_SIZE)
 #define ZC ((NZ + 63) / 64)          // z rows per lane (lane r holds r, r + 64, ...)
+#define ROWS_D ((ND + 15) / 16)
 #define ROWS_X ((NX + 15) / 16)
 #define ROWS_Z (ZC > 1 ? 4 : (NZ + 15) / 16)
 #define ROWS_Y ((NY1 + 15) / 16)
@@ -82,10 +87,10 @@ static __device__ __forceinline__ double qpb_bc(double v, int l) {
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
-// value of lane J of the x block in every lane that uses it: one DPP
-// row_newbcast when the x block fits one 16-lane row, else v_readlane
+// value of lane J of the dense block in every lane that uses it: one DPP
+// row_newbcast when the dense block fits one 16-lane row, else v_readlane
 template <int J> static __device__ __forceinline__ double qpb_xb(double v) {
-    if constexpr (NX <= 16) return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
+    if constexpr (ND <= 16) return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
     else return qpb_bc(v, J);
 }
 
@@ -169,17 +174,23 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     double *__restrict__ Ls = qpb_lds + wv * LDS_WAVE;
     const long tile = q >> 6;
     const int ql = (int)(q & 63);
-    const bool isx = lane < NX, isy = lane < NY;
+    const bool isx = lane < NX, isy = lane < NY, isd = lane < ND;
     const int ix = isx ? lane : NX - 1;
     const int iy = isy ? lane : (NY > 0 ? NY - 1 : 0);
-    bool isz[ZC];
+    const int id = isd ? lane : ND - 1;
+    bool isz[ZC], zleaf[ZC];
     int iz[ZC];
 #pragma unroll
     for (int t = 0; t < ZC; t++) {
         isz[t] = lane + 64 * t < NZ;
         iz[t] = isz[t] ? lane + 64 * t : NZ - 1;
+        zleaf[t] = qpb_zleaf_d[iz[t]] != 0;
     }
-    constexpr double RDY = 1.0 / -1e-7;      // y pivots: D = 0 regularised to -1e-7
+    const bool yleaf = NY > 0 ? qpb_yleaf_d[iy] != 0 : true;
+    // this lane's dense row: kind (0 x, 1 y, 2 z) and variable index
+    const int dk = qpb_dkind_d[id], di = qpb_didx_d[id];
+    const int dvar = dk == 0 ? di : (dk == 1 ? NX + di : NX + NY + di);   // x | y | z numbering
+    constexpr double RDY = 1.0 / -1e-7;      // leaf y pivots: D = 0 regularised to -1e-7
 
     QPB_TS(0);
     // ---- stage this QP's inputs as dense matrices in LDS (tiled SoA -> dense):
@@ -245,7 +256,6 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 
     // this lane's slices of the (constant) matrices: registers when small (REGS)
     double Prow[QPB_W_REGS ? NX : 1], Grow[QPB_W_REGS ? ZC * NX : 1], Arow[QPB_W_REGS ? NX : 1];
-    double Gcol[QPB_W_REGS ? NZ : 1], Acol[QPB_W_REGS ? NY1 : 1];
     if constexpr (QPB_W_REGS) {
 #pragma unroll
         for (int j = 0; j < NX; j++) {
@@ -254,27 +264,47 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
             for (int t = 0; t < ZC; t++) Grow[t * NX + j] = Gd[j * NZ + iz[t]];
         }
-#pragma unroll
-        for (int r = 0; r < NZ; r++) Gcol[r] = Gd[ix * NZ + r];
-#pragma unroll
-        for (int l = 0; l < NY1; l++) Acol[l] = NY > 0 ? Ad[ix * NY + l] : 0.0;
     }
     auto PR = [&](int j) { if constexpr (QPB_W_REGS) return Prow[j]; else return Pd[j * NX + ix]; };   // P(i, j)
     auto GR = [&](int t, int j) { if constexpr (QPB_W_REGS) return Grow[t * NX + j]; else return Gd[j * NZ + iz[t]]; };  // G(r, j)
     auto AR = [&](int j) { if constexpr (QPB_W_REGS) return Arow[j]; else return Ad[j * NY + iy]; };   // A(l, j)
-    auto GC = [&](int r) { if constexpr (QPB_W_REGS) return Gcol[r]; else return Gd[ix * NZ + r]; };   // G(r, i)
-    auto AC = [&](int l) { if constexpr (QPB_W_REGS) return Acol[l]; else return Ad[ix * NY + l]; };   // A(l, i)
-
-    // H0 = P(upper, symmetrised) + 1e7 A'A: the y leaves (ldl.c:303-318 for x rows)
-    double H0[NX];
+    // dense-row slices: G(r, i) / A(l, i) of this lane's dense row when it is x_i, else 0
+    const int dxi = dk == 0 ? di : 0;
+    const double dxm = dk == 0 ? 1.0 : 0.0;
+    double Gcol[QPB_W_REGS ? NZ : 1], Acol[QPB_W_REGS ? NY1 : 1];
+    if constexpr (QPB_W_REGS) {
 #pragma unroll
-    for (int j = 0; j < NX; j++) {
-        double v = ix <= j ? Pd[j * NX + ix] : Pd[ix * NX + j];
+        for (int r = 0; r < NZ; r++) Gcol[r] = dxm * Gd[dxi * NZ + r];
 #pragma unroll
-        for (int l = 0; l < NY; l++) v = __builtin_fma(AC(l), -RDY * Ad[j * NY + l], v);
-        H0[j] = v;
+        for (int l = 0; l < NY1; l++) Acol[l] = NY > 0 ? dxm * Ad[dxi * NY + l] : 0.0;
     }
-    // G(r,i) G(r,j) for every structural G(r,j): the z leaves' updates of row i
+    auto GC = [&](int r) { if constexpr (QPB_W_REGS) return Gcol[r]; else return dxm * Gd[dxi * NZ + r]; };
+    auto AC = [&](int l) { if constexpr (QPB_W_REGS) return Acol[l]; else return dxm * Ad[dxi * NY + l]; };
+
+    // H0: the static part of this lane's dense row (perm order of the columns):
+    //   x_i  : P(i,j) (upper, symmetrised) + 1e7 sum_{leaf y} A(l,i)A(l,j) | A(l,i) | G(r,i)
+    //   y_l  : A(l,j) on x columns, 0 elsewhere
+    //   z_r  : G(r,j) on x columns, 0 elsewhere (the diagonal -s/z joins at pivot time)
+    double H0[ND];
+    qpb_for<0, ND>([&](auto ec) {
+        constexpr int e = decltype(ec)::value;
+        constexpr int ke = qpb_dkind[e], je = qpb_didx[e];
+        double v = 0.0;
+        if constexpr (ke == 0) {
+            const double px = dxi <= je ? Pd[je * NX + dxi] : Pd[dxi * NX + je];
+            double vx = px;
+#pragma unroll
+            for (int l = 0; l < NY; l++)
+                if (qpb_yleaf[l]) vx = __builtin_fma(Ad[dxi * NY + l], -RDY * Ad[je * NY + l], vx);
+            v = dk == 0 ? vx : (dk == 1 ? Ad[je * NY + (NY > 0 ? di : 0)] : Gd[je * NZ + di]);
+        } else if constexpr (ke == 1) {
+            v = dk == 0 ? Ad[dxi * NY + je] : 0.0;
+        } else {
+            v = dk == 0 ? Gd[dxi * NZ + je] : 0.0;
+        }
+        H0[e] = isd ? v : 0.0;
+    });
+    // G(r,i) G(r,j) for every structural G(r,j) of a leaf z row (x_i rows only)
     double GG[QPB_W_GG ? QPB_NNZG : 1];
     if constexpr (QPB_W_GG) {
         int e = 0;
@@ -285,17 +315,21 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 if (qpb_Gnz[r][j]) GG[e++] = GC(r) * Gd[j * NZ + r];
     }
 
-    double H[NX], Lt[NX], rDx = 0.0, w[ZC];
-    // factor: H = H0 + G' diag(w) G, then dense LDL' of H (right-looking)
-    auto factor = [&](const double *wz) {
+    double H[ND], Lt[ND], rDd = 0.0, w[ZC];
+    // factor with z diagonal kd (per z row): leaf z rows fold into the x block
+    // as G'diag(w)G, w = -1/regularise(kd); dense z rows take kd at their pivot
+    auto factor = [&](const double *kd) {
 #pragma unroll
         for (int t = 0; t < ZC; t++) {
-            w[t] = wz[t];
-            if (isz[t]) Vb[lane + 64 * t] = wz[t];
+            w[t] = -qpb_rcp_reg(kd[t]);
+            if (isz[t]) {
+                Vb[lane + 64 * t] = w[t];
+                if constexpr (!QPB_XID) Vb[NZ + lane + 64 * t] = kd[t];   // dense z rows' diagonals
+            }
         }
         qpb_wsync();
 #pragma unroll
-        for (int j = 0; j < NX; j++) H[j] = H0[j];
+        for (int e = 0; e < ND; e++) H[e] = H0[e];
         {
             int e = 0;
 #pragma unroll
@@ -304,66 +338,93 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
                 for (int j = 0; j < NX; j++)
                     if (qpb_Gnz[r][j]) {
-                        if constexpr (QPB_W_GG) H[j] = __builtin_fma(GG[e], wr, H[j]);
-                        else H[j] = __builtin_fma(GC(r) * wr, Gd[j * NZ + r], H[j]);
+                        const int xe = qpb_xpos[j];
+                        if constexpr (QPB_W_GG) H[xe] = __builtin_fma(GG[e], wr, H[xe]);
+                        else H[xe] = __builtin_fma(GC(r) * wr, Gd[j * NZ + r], H[xe]);
                         e++;
                     }
             }
         }
-        qpb_wsync();
-        qpb_for<0, NX>([&](auto kc) {
+        double kdz[ND];
+        qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            const double rd = qpb_rcp_reg(qpb_xb<k>(H[k]));
-            rDx = lane == k ? rd : rDx;
+            if constexpr (qpb_dkind[k] == 2) kdz[k] = Vb[NZ + qpb_didx[k]];
+        });
+        qpb_wsync();
+        qpb_for<0, ND>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            double dpiv = qpb_xb<k>(H[k]);
+            if constexpr (qpb_dkind[k] == 2) dpiv += kdz[k];
+            const double rd = qpb_rcp_reg(dpiv);
+            rDd = lane == k ? rd : rDd;
             const double l = H[k] * rd;
-            qpb_for<k + 1, NX>([&](auto jc) {
+            qpb_for<k + 1, ND>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 H[j] = __builtin_fma(-l, qpb_xb<j>(H[k]), H[j]);
             });
-            H[k] = lane > k ? l : 0.0;        // L(i,k) below the diagonal, 0 elsewhere
+            H[k] = lane > k ? l : 0.0;        // L(d,k) below the diagonal, 0 elsewhere
         });
-        // transpose L through LDS: lane j gets column j (0 on and above the diagonal)
-        if (isx) {
+        // transpose L through LDS: lane e gets column e (0 on and above the diagonal)
+        if (isd) {
 #pragma unroll
-            for (int j = 0; j < NX; j++) Tx[lane * NX + j] = H[j];
+            for (int e = 0; e < ND; e++) Tx[lane * ND + e] = H[e];
         }
         qpb_wsync();
 #pragma unroll
-        for (int k = 0; k < NX; k++) Lt[k] = Tx[k * NX + ix];
+        for (int k = 0; k < ND; k++) Lt[k] = Tx[k * ND + id];
         qpb_wsync();
     };
 
     // solve K [dx; dy; dz] = [bx; byv; bz] with the current factor
+    constexpr int VBX = 0, VBY = NX, VBZ = NX + NY, VBV = NX + NY + NZ, VBO = NX + NY + 2 * NZ;
     auto solve = [&](double bx, double byv, const double *bz, double &dx, double &dy, double *dz) {
+        if constexpr (!QPB_XID) {
+            if (lane < NX) Vb[VBX + lane] = bx;
+            if (lane < NY) Vb[VBY + lane] = byv;
+        }
 #pragma unroll
         for (int t = 0; t < ZC; t++)
-            if (isz[t]) Vb[lane + 64 * t] = w[t] * bz[t];    // -bz / D_z
-        if (lane < NY) Vb[NZ + lane] = -RDY * byv;        // -by / D_y
+            if (isz[t]) {
+                if constexpr (!QPB_XID) Vb[VBZ + lane + 64 * t] = bz[t];
+                Vb[VBV + lane + 64 * t] = w[t] * bz[t];     // -bz / D_z (read for leaf rows only)
+            }
+        if constexpr (QPB_XID)
+            if (lane < NY) Vb[VBY + lane] = byv;
         qpb_wsync();
+        // this dense row's right-hand side after the leaves' forward elimination
         double ta[QPB_W_SPLIT];
 #pragma unroll
-        for (int k = 0; k < QPB_W_SPLIT; k++) ta[k] = k ? 0.0 : bx;
+        for (int k = 0; k < QPB_W_SPLIT; k++) ta[k] = 0.0;
 #pragma unroll
-        for (int r = 0; r < NZ; r++) ta[r % QPB_W_SPLIT] = __builtin_fma(GC(r), Vb[r], ta[r % QPB_W_SPLIT]);
+        for (int r = 0; r < NZ; r++)
+            if (qpb_zleaf[r]) ta[r % QPB_W_SPLIT] = __builtin_fma(GC(r), Vb[VBV + r], ta[r % QPB_W_SPLIT]);
 #pragma unroll
         for (int l = 0; l < NY; l++)
-            ta[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(AC(l), Vb[NZ + l], ta[(NZ + l) % QPB_W_SPLIT]);
-        qpb_wsync();
-        double t = ta[0];
+            if (qpb_yleaf[l])
+                ta[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(AC(l), -RDY * Vb[VBY + l], ta[(NZ + l) % QPB_W_SPLIT]);
+        double t;
+        if constexpr (QPB_XID) t = bx;        // dense row d is x_d
+        else t = Vb[dvar];                    // bx_i | by_l | bz_r  (VBX, VBY, VBZ are contiguous)
 #pragma unroll
-        for (int k = 1; k < QPB_W_SPLIT; k++) t += ta[k];
-        qpb_for<0, NX>([&](auto kc) {
+        for (int k = 0; k < QPB_W_SPLIT; k++) t += ta[k];
+        qpb_wsync();
+        qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             t = __builtin_fma(-H[k], qpb_xb<k>(t), t);
         });
-        t *= rDx;
-        qpb_for<0, NX>([&](auto kc) {
-            constexpr int k = NX - 1 - decltype(kc)::value;
+        t *= rDd;
+        qpb_for<0, ND>([&](auto kc) {
+            constexpr int k = ND - 1 - decltype(kc)::value;
             t = __builtin_fma(-Lt[k], qpb_xb<k>(t), t);
         });
-        dx = t;
-        if (lane < NX) Vb[lane] = t;
+        if constexpr (QPB_XID) {
+            if (lane < NX) Vb[VBO + lane] = t;
+        } else if (isd) {
+            Vb[VBO + dvar] = t;               // dense solution, by variable
+        }
         qpb_wsync();
+        if constexpr (QPB_XID) dx = t;
+        else dx = Vb[VBO + ix];
         double gza[ZC][QPB_W_SPLIT], gya[QPB_W_SPLIT];
 #pragma unroll
         for (int k = 0; k < QPB_W_SPLIT; k++) {
@@ -373,12 +434,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         }
 #pragma unroll
         for (int j = 0; j < NX; j++) {
-            const double xj = Vb[j];
+            const double xj = Vb[VBO + j];
 #pragma unroll
             for (int u = 0; u < ZC; u++) gza[u][j % QPB_W_SPLIT] = __builtin_fma(GR(u, j), xj, gza[u][j % QPB_W_SPLIT]);
             if constexpr (NY > 0) gya[j % QPB_W_SPLIT] = __builtin_fma(AR(j), xj, gya[j % QPB_W_SPLIT]);
         }
-        qpb_wsync();
         double gy = gya[0];
 #pragma unroll
         for (int k = 1; k < QPB_W_SPLIT; k++) gy += gya[k];
@@ -387,9 +447,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             double gz = gza[u][0];
 #pragma unroll
             for (int k = 1; k < QPB_W_SPLIT; k++) gz += gza[u][k];
-            dz[u] = -w[u] * (bz[u] - gz);
+            if constexpr (QPB_XID) dz[u] = -w[u] * (bz[u] - gz);
+            else dz[u] = zleaf[u] ? -w[u] * (bz[u] - gz) : Vb[VBO + NX + NY + iz[u]];
         }
-        dy = RDY * (byv - gy);
+        if constexpr (QPB_XID) dy = RDY * (byv - gy);
+        else dy = yleaf ? RDY * (byv - gy) : Vb[VBO + NX + iy];
+        qpb_wsync();
     };
 
     // lane sums / maxima over this lane's z slots (0 / neutral outside the range)
@@ -410,10 +473,10 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     // ---- kkt_initialize (Auxilary.c:992-1089): K with -I, rhs [-c; b; h]
     double x, y, s[ZC], z[ZC];
     {
-        double one[ZC], dzi[ZC];
+        double m1[ZC], dzi[ZC];
 #pragma unroll
-        for (int t = 0; t < ZC; t++) one[t] = 1.0;
-        factor(one);
+        for (int t = 0; t < ZC; t++) m1[t] = -1.0;
+        factor(m1);
         QPB_TS(2);
         solve(-cx, by, hz, x, y, dzi);
         QPB_TS(3);
@@ -473,10 +536,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
             for (int k = 0; k < QPB_W_SPLIT; k++) ra[k] = k ? 0.0 : rx;
 #pragma unroll
-            for (int r = 0; r < NZ; r++) ra[r % QPB_W_SPLIT] = __builtin_fma(-GC(r), Vb[NX + r], ra[r % QPB_W_SPLIT]);
+            for (int r = 0; r < NZ; r++)   // G(r, i): the dense-row slice when dense row i is x_i
+                ra[r % QPB_W_SPLIT] = __builtin_fma(-(QPB_XID ? GC(r) : Gd[ix * NZ + r]), Vb[NX + r], ra[r % QPB_W_SPLIT]);
 #pragma unroll
             for (int l = 0; l < NY; l++)
-                ra[(NZ + l) % QPB_W_SPLIT] = __builtin_fma(-AC(l), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
+                ra[(NZ + l) % QPB_W_SPLIT] =
+                    __builtin_fma(-(QPB_XID ? AC(l) : Ad[ix * NY + l]), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
             rx = ra[0];
 #pragma unroll
             for (int k = 1; k < QPB_W_SPLIT; k++) rx += ra[k];
@@ -493,14 +558,13 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         QPB_TS(9 + 8 * it);
         const double mu = st_mu;
         const bool pc = sigma > a.sigma_d;
-        double rzi[ZC], wz[ZC];
+        double rzi[ZC], kd[ZC];
 #pragma unroll
         for (int t = 0; t < ZC; t++) {
             rzi[t] = qpb_rcp(z[t]);
-            // updatekktmatrix (Auxilary.c:211-215): z pivot -s/z, regularised (ldl.c:319-320)
-            wz[t] = isz[t] ? -qpb_rcp_reg(-s[t] * rzi[t]) : 0.0;
+            kd[t] = isz[t] ? -s[t] * rzi[t] : -1.0;   // updatekktmatrix (Auxilary.c:211-215)
         }
-        factor(wz);
+        factor(kd);
         QPB_TS(10 + 8 * it);
         if (!pc) sigma = a.sigma_d;
         double cc[ZC];

@@ -5,9 +5,22 @@
 
 #include "qpb_plan.hpp"
 
+#include <vector>
+
 namespace qpb {
-// Can the plan run on the wave kernel?  (n, m, p <= 64; no empty G row.)
+// Elimination layout of the wave kernel for the plan's permutation: z / y rows
+// whose neighbours all come later ("leaves") are eliminated first, in parallel;
+// every other KKT row forms a dense block factored in permutation order.
+struct WaveLayout {
+    std::vector<int> zleaf, yleaf;   // per z / y row: 1 = leaf
+    std::vector<long> dense;         // KKT indices of the dense block, in perm order
+};
+WaveLayout wave_layout(const Plan &pl);
+// Can the plan run on the wave kernel?  (n, p <= 64, m <= 256, <= 64 dense
+// rows, no empty G row, LDS fits.)
 bool wave_eligible(const Plan &pl, std::string *why);
+// Workgroup size: 64 x (QPs per workgroup that fit the LDS), 0 if none fits.
+int wave_wg_for(const Plan &pl);
 // Full hiprtc source; the kernel name is returned through name_out.
 std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out);
 }  // namespace qpb

@@ -99,7 +99,7 @@ def main():
         res = pl.unpack(outs[v], a.batch)
         err = 0.0
         for k, q in enumerate(ids):
-            perm = pl.wave_perm() if v.startswith("wave") else pl.perm
+            perm = pl.perm
             ref = o.solve_dense(n, m, p, Pc[k], Ac[k], Gc[k], dd["c"][k], dd["h"][k], dd["b"][k], perm=perm,
                                 maxit=a.maxit)
             err = max(err, float(np.max(np.abs(ref["x"] - res["x"][q]))))

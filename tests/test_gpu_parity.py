@@ -63,7 +63,8 @@ def test_exact_kernel_bit_identical_to_reference(name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", DENSE_CASES)
 @pytest.mark.parametrize("exact,own_order,kernel", [(False, False, "lane"), (False, True, "lane"),
-                                                    (True, True, "lane"), (False, True, "wave")])
+                                                    (True, True, "lane"), (False, True, "wave"),
+                                                    (False, False, "wave")])
 def test_kernel_within_tolerance_of_reference(name, exact, own_order, kernel):
     """Fast kernel and/or own ordering vs the reference: |.|_inf <= 1e-6 * max(1, |ref|).
     The wave kernel always eliminates in its own order [z | y | x].
@@ -76,6 +77,8 @@ def test_kernel_within_tolerance_of_reference(name, exact, own_order, kernel):
     truncated = int(g["maxit"]) < 100
     if own_order and (name == "edge_zero_g_row" or truncated):
         pytest.skip("depends on the reference's own KKT order")
+    if kernel == "wave" and name == "edge_zero_g_row":
+        pytest.skip("the wave kernel needs every G row non-empty")
     _, r = _solve(g, perm=None if own_order else g["perm"][0], exact=exact, p_upper=True, kernel=kernel)
     n, m, p, P, A, G = _dense(g)
     sel = slice(None) if truncated else (g["flag"] == 0)
@@ -114,12 +117,15 @@ def test_exact_kernel_matches_oracle_with_own_ordering(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["c30_tol1e-6"])
-def test_wave_kernel_controller_shape_vs_reference(name):
-    """Controller-shape QPs (30/68/18, N = 116: two z rows per lane, x block over
-    two 16-lane rows) on the wave kernel vs the reference golden vectors."""
+@pytest.mark.parametrize("name,ref_perm", [("c30_tol1e-6", False), ("c30_tol1e-6", True), ("c30_tol1e-2", True)])
+def test_wave_kernel_controller_shape_vs_reference(name, ref_perm):
+    """Controller-shape QPs (30/68/18, N = 116: two z rows per lane, dense block
+    of 48-51 rows over several 16-lane rows) on the wave kernel vs the reference
+    golden vectors.  Given the reference's permutation the wave kernel factors
+    with the reference's pivots (and regularisations), so even the loosely
+    converged tol-1e-2 solutions agree to 1e-6."""
     g = golden(name)
-    _, r = _solve(g, perm=None, exact=False, p_upper=True, kernel="wave")
+    _, r = _solve(g, perm=g["perm"][0] if ref_perm else None, exact=False, p_upper=True, kernel="wave")
     np.testing.assert_array_equal(r["flag"], g["flag"])
     for k in ("x", "y", "z", "s"):
         scale = max(1.0, float(np.abs(g[k]).max()))
@@ -128,7 +134,7 @@ def test_wave_kernel_controller_shape_vs_reference(name):
 
 
 def _oracle_perm(plan):
-    return plan.wave_perm() if plan.kernel == "wave" else plan.perm
+    return plan.perm if plan.kernel == "wave" else plan.perm
 
 
 @pytest.mark.gpu
@@ -143,7 +149,7 @@ def test_wave_kernel_matches_oracle_in_its_order(name, oracle):
     tol = float(g["tol"])
     for q in range(0, g["x"].shape[0], 3):
         o = oracle.solve_dense(n, m, p, g["P"][q], g["A"][q] if p else None, g["G"][q], g["c"][q], g["h"][q],
-                               g["b"][q] if p else None, perm=plan.wave_perm(), ordering=int(g["ordering"]),
+                               g["b"][q] if p else None, perm=plan.perm, ordering=int(g["ordering"]),
                                reltol=tol, abstol=tol, maxit=int(g["maxit"]))
         assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (name, q)
         got, ref = {k: r[k][q] for k in ("x", "z", "s")}, {k: o[k] for k in ("x", "z", "s")}
