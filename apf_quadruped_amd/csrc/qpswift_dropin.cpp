@@ -69,7 +69,9 @@ struct Priv {
     kkt K{};
     settings opt{};
     stats st{};
-    // device state (allocated on the first QP_SOLVE)
+    // device buffers: borrowed from the solving thread's workspace (below) for
+    // the duration of one QP_SOLVE -- the controller creates and destroys a QP
+    // every tick, so nothing device-side is allocated per QP object
     int dev = -1;
     hipStream_t stream = nullptr;
     double *dmem = nullptr;   // tiled inputs/outputs + packed staging
@@ -171,7 +173,10 @@ PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const
         return nullptr;
     }
     PlanPtr plan(raw, PlanDeleter());
-    if ((rc = qpb_plan_compile(raw)) != 0) {
+    // compile only the kernel a batch of one runs (the wave kernel when the plan
+    // is eligible, else the lane kernel): large lane kernels take minutes
+    rc = raw->wave_ok && raw->kernel_pref != 1 ? qpb::compile_wave(raw) : qpb::compile_plan(raw);
+    if (rc != 0) {
         err = qpb_last_error();
         return nullptr;
     }
@@ -226,8 +231,11 @@ QP *finish_setup(Handle *hd, long *Permut, clk::time_point t0) {
     q.lambda = vec(v.lambda, m);
     q.temp = vec(v.temp, n);
 
-    const char *fast = getenv("QPSWIFT_HIP_FAST");
-    const bool exact = !(fast && *fast && *fast != '0');
+    // default: fast arithmetic (the wave kernel where eligible: ~50 us per C1
+    // tick instead of ~250 us); QPSWIFT_HIP_EXACT=1 selects the bit-faithful
+    // lane kernel (bit-identical to qpSWIFT given the same permutation)
+    const char *ex = getenv("QPSWIFT_HIP_EXACT");
+    const bool exact = ex && *ex && *ex != '0';
     v.plan = get_plan(n, m, p, q.P->jc, q.P->ir, p > 0 ? q.A->jc : nullptr, p > 0 ? q.A->ir : nullptr, q.G->jc,
                       q.G->ir, Permut, exact, v.err);
 
@@ -293,39 +301,66 @@ Handle *new_handle(long n, long m) {
     return hd;
 }
 
+// Per-thread, per-device workspace: one stream, one device slab and one pinned
+// staging slab, grown on demand and reused by every QP the thread solves.
+struct Workspace {
+    hipStream_t stream = nullptr;
+    double *dmem = nullptr;
+    double *hmem = nullptr;
+    long dcap = 0, hcap = 0;   // doubles
+};
+thread_local std::map<int, Workspace> t_ws;
+
 int ensure_device(Priv &v, const QP &q) {
-    if (v.dmem) return QPB_OK;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return qpb::set_error(QPB_EHIP, "QP_SOLVE: no HIP device available (the drop-in has no CPU path)");
-    if (hipGetDevice(&v.dev) != hipSuccess) return qpb::set_error(QPB_EHIP, "hipGetDevice failed");
-    const long T = 64;   // one tile holds the single QP (lane 0)
-    v.nP = q.P->nnz;
-    v.nA = q.p > 0 ? q.A->nnz : 0;
-    v.nG = q.G->nnz;
-    long o = 0;
-    auto take = [&o](long k) { long r = o; o += std::max(k, 1L); return r; };
-    v.oP = take(v.nP * T); v.oA = take(v.nA * T); v.oG = take(v.nG * T);
-    v.oc = take(q.n * T); v.oh = take(q.m * T); v.ob = take(q.p * T);
-    v.ox = take(q.n * T); v.oy = take(q.p * T); v.oz = take(q.m * T); v.os = take(q.m * T);
-    v.ost = take(6 * T);
-    v.nin = v.nP + v.nA + v.nG + q.n + q.m + q.p;
-    v.nout = q.n + q.p + 2 * q.m + 6 + 1;   // x y z s stats fval
-    v.oin = take(v.nin);
-    v.oout = take(v.nout + 1);              // + flag, iters (two ints in one double slot)
-    v.ofv = v.oout + v.nout - 1;
-    v.ototal = o;
-    if (hipMalloc((void **)&v.dmem, sizeof(double) * (size_t)o) != hipSuccess) {
-        v.dmem = nullptr;
-        return qpb::set_error(QPB_ENOMEM, "QP_SOLVE: device allocation failed");
+    if (v.dev < 0 && hipGetDevice(&v.dev) != hipSuccess) return qpb::set_error(QPB_EHIP, "hipGetDevice failed");
+    if (v.ototal == 0) {   // layout of this QP in the slab (tile of 64, QP in lane 0)
+        const long T = 64;
+        v.nP = q.P->nnz;
+        v.nA = q.p > 0 ? q.A->nnz : 0;
+        v.nG = q.G->nnz;
+        long o = 0;
+        auto take = [&o](long k) { long r = o; o += std::max(k, 1L); return r; };
+        v.oP = take(v.nP * T); v.oA = take(v.nA * T); v.oG = take(v.nG * T);
+        v.oc = take(q.n * T); v.oh = take(q.m * T); v.ob = take(q.p * T);
+        v.ox = take(q.n * T); v.oy = take(q.p * T); v.oz = take(q.m * T); v.os = take(q.m * T);
+        v.ost = take(6 * T);
+        v.nin = v.nP + v.nA + v.nG + q.n + q.m + q.p;
+        v.nout = q.n + q.p + 2 * q.m + 6 + 1;   // x y z s stats fval
+        v.oin = take(v.nin);
+        v.oout = take(v.nout + 1);              // + flag, iters (two ints in one double slot)
+        v.ofv = v.oout + v.nout - 1;
+        v.ototal = o;
     }
-    if (hipHostMalloc((void **)&v.hmem, sizeof(double) * (size_t)(v.nin + v.nout + 1), hipHostMallocDefault) !=
-        hipSuccess) {
-        v.hmem = nullptr;
-        return qpb::set_error(QPB_ENOMEM, "QP_SOLVE: pinned host allocation failed");
-    }
-    if (hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking) != hipSuccess)
+    Workspace &w = t_ws[v.dev];
+    if (!w.stream && hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking) != hipSuccess) {
+        w.stream = nullptr;
         return qpb::set_error(QPB_EHIP, "QP_SOLVE: stream creation failed");
+    }
+    if (w.dcap < v.ototal) {
+        if (w.dmem) (void)hipFree(w.dmem);
+        w.dcap = 0;
+        if (hipMalloc((void **)&w.dmem, sizeof(double) * (size_t)v.ototal) != hipSuccess) {
+            w.dmem = nullptr;
+            return qpb::set_error(QPB_ENOMEM, "QP_SOLVE: device allocation failed");
+        }
+        w.dcap = v.ototal;
+    }
+    const long hneed = v.nin + v.nout + 1;
+    if (w.hcap < hneed) {
+        if (w.hmem) (void)hipHostFree(w.hmem);
+        w.hcap = 0;
+        if (hipHostMalloc((void **)&w.hmem, sizeof(double) * (size_t)hneed, hipHostMallocDefault) != hipSuccess) {
+            w.hmem = nullptr;
+            return qpb::set_error(QPB_ENOMEM, "QP_SOLVE: pinned host allocation failed");
+        }
+        w.hcap = hneed;
+    }
+    v.dmem = w.dmem;
+    v.hmem = w.hmem;
+    v.stream = w.stream;
     return QPB_OK;
 }
 
@@ -420,20 +455,7 @@ int solve_on_device(Priv &v, QP &q) {
 void release(QP *q) {
     if (!q) return;
     Handle *hd = handle_of(q);
-    Priv *v = hd->priv;
-    if (v) {
-        if (v->dmem || v->stream) {
-            int cur = -1;
-            (void)hipGetDevice(&cur);
-            if (v->dev >= 0 && cur != v->dev) (void)hipSetDevice(v->dev);
-            if (v->stream) (void)hipStreamSynchronize(v->stream);
-            if (v->dmem) (void)hipFree(v->dmem);
-            if (v->hmem) (void)hipHostFree(v->hmem);
-            if (v->stream) (void)hipStreamDestroy(v->stream);
-            if (cur >= 0 && cur != v->dev) (void)hipSetDevice(cur);
-        }
-        delete v;
-    }
+    delete hd->priv;      // device buffers belong to the thread workspace, not the QP
     std::free(hd);
 }
 

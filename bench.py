@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--large-batch", type=int, default=1 << 20,
                     help="QPs of the secondary large-batch leg (1-GPU runs; 0 = skip)")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave"])
+    ap.add_argument("--no-mixed", dest="mixed", action="store_false",
+                    help="skip the configs[2] leg (4 gait patterns x 1024 QPs)")
     ap.add_argument("--argmin", default="separate", choices=["fused", "separate"],
                     help="fused: one qpb_solve_best call per step; separate: qpb_solve + qpb_argmin calls")
     ap.add_argument("--tol", type=float, default=1e-6)
@@ -178,6 +180,57 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ar
     return elapsed, kern_ms, out, (gathered if coll else best.reshape(1, 2))
 
 
+def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
+    """configs[2]: 4 x 1024 QPs, one sparsity pattern per gait phase (stance4,
+    trot BL+FR, trot BR+FL, crawl), bucketed into one plan each and launched
+    on one stream each; a step = all four solves (+ argmins) complete."""
+    import torch
+    from apf_quadruped_amd import plans, workloads as W
+    from apf_quadruped_amd.batch import Plan, argmin_launcher
+    legs = []
+    for k, name in enumerate(("stance4", "trot_blfr", "trot_brfl", "crawl_blflfr")):
+        stance = W.STANCE_SETS[name]
+        gen = lambda ids, st=stance: W.contact_force_qp(plans.SEED + 3, ids, stance=st, feasible_wrench=True)
+        d0 = gen(np.arange(1))
+        plan = Plan.from_dense(12, d0["m"], 6, d0["P"][0], d0["A"][0], d0["G"][0])
+        plan.compile()
+        host = make_shard(plan, plans.SEED + 3, k * per_pattern, per_pattern, gen=gen)
+        vals = {kk: torch.from_numpy(v).to(dev) for kk, v in host.items()}
+        out = plan.alloc_outputs(per_pattern, device=dev)
+        best = torch.zeros(2, dtype=torch.float64, device=dev)
+        st = torch.cuda.Stream(dev)
+        legs.append(dict(name=name, plan=plan, out=out, stream=st, vals=vals,
+                         solve=plan.launcher(vals, out, per_pattern, reltol=tol, abstol=tol, stream=st),
+                         post=argmin_launcher(out["fval"], out["flag"], best, stream=st)))
+    main = torch.cuda.current_stream(dev)
+
+    def step():
+        ev = torch.cuda.Event()
+        ev.record(main)
+        for L in legs:
+            L["stream"].wait_event(ev)
+            L["solve"]()
+            L["post"]()
+        for L in legs:
+            e = torch.cuda.Event()
+            e.record(L["stream"])
+            main.wait_event(e)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    B = per_pattern * len(legs)
+    return {"batch": B, "patterns": [L["name"] for L in legs], "value": B * steps / el,
+            "ms_per_step": el * 1e3 / steps, "kernels": [L["plan"].kernel_name(per_pattern) for L in legs],
+            "kkt_N": [L["plan"].info.N for L in legs],
+            "optimal_frac": float(np.mean([(L["out"]["flag"] == 0).float().mean().item() for L in legs]))}
+
+
 def traffic_for(kname, B):
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
@@ -237,6 +290,12 @@ def main():
                  "mean_iters": itl, "optimal_frac": float((outl["flag"] == 0).float().mean().item())}
         del outl
 
+    # configs[2]: 4 096 QPs across the 4 gait contact patterns (mixed KKT sparsity):
+    # one plan per pattern, the four launches on four HIP streams
+    mixed = None
+    if rank == 0 and world == 1 and args.mixed:
+        mixed = mixed_patterns_leg(args.tol, dev)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(seed, args.cpu_sample, args.cpu_passes, args.tol)
@@ -269,6 +328,7 @@ def main():
             "mean_iters": mean_it,
             "optimal_frac": float((flags == 0).mean()),
             "large_batch": large,
+            "mixed_patterns": mixed,
             "cpu_baseline": cpu,
         }
         if world > 1:

@@ -1,0 +1,72 @@
+"""Per-tick latency of the qpSWIFT drop-in, called exactly as the controller
+does (QP_SETUP_dense -> options -> QP_SOLVE -> read x -> QP_CLEANUP_dense,
+main.cpp:1649-1663), next to the reference qpSWIFT on the host CPU (oracle/_ref,
+when present).
+
+    python scripts/dropin_latency.py [--ticks N] [--shape c1|c30] [--mode exact|fast]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ticks", type=int, default=200)
+    ap.add_argument("--shape", default="c1", choices=["c1", "c30"])
+    ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
+    ap.add_argument("--tol", type=float, default=1e-2)        # the controller's (main.cpp:1651)
+    a = ap.parse_args()
+    from apf_quadruped_amd import _lib, plans, qpswift_abi as abi, workloads as W
+    if a.mode == "exact":
+        os.environ["QPSWIFT_HIP_EXACT"] = "1"
+    else:
+        os.environ.pop("QPSWIFT_HIP_EXACT", None)
+    gen = (lambda ids: W.contact_force_qp(plans.SEED + 1, ids)) if a.shape == "c1" else \
+        (lambda ids: W.controller_qp(plans.SEED + 30, ids))
+    d = gen(np.arange(a.ticks))
+    n, m, p = d["n"], d["m"], d["p"]
+    P, A, G = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    c, h, b = (np.ascontiguousarray(d[k]) for k in ("c", "h", "b"))
+
+    def run(lib):
+        lat, flags, xs = [], [], []
+        for t in range(a.ticks):
+            t0 = time.perf_counter()
+            qp = lib.QP_SETUP_dense(n, m, p, abi.dptr(P[t]), abi.dptr(A[t]), abi.dptr(G[t]), abi.dptr(c[t]),
+                                    abi.dptr(h[t]), abi.dptr(b[t]), None, abi.COLUMN_MAJOR_ORDERING)
+            o = qp.contents.options.contents
+            o.reltol = a.tol
+            o.abstol = a.tol
+            flags.append(int(lib.QP_SOLVE(qp)))
+            xs.append(np.ctypeslib.as_array(qp.contents.x, (n,)).copy())
+            lib.QP_CLEANUP_dense(qp)
+            lat.append(time.perf_counter() - t0)
+        return np.array(lat), np.array(flags), np.array(xs)
+
+    L = _lib.lib()
+    run(L)                                   # first ticks: plan + kernel (cache) + device buffers
+    lat, flags, xs = run(L)
+    out = dict(shape=a.shape, mode=a.mode, tol=a.tol, ticks=a.ticks, optimal=float((flags == 0).mean()),
+               gpu_us_median=float(np.median(lat) * 1e6), gpu_us_p99=float(np.percentile(lat, 99) * 1e6))
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libqpswift_ref.so")
+    if os.path.exists(ref_so):
+        R = abi.bind_qpswift(C.CDLL(ref_so))
+        run(R)
+        rl, rf, rx = run(R)
+        out.update(cpu_ref_us_median=float(np.median(rl) * 1e6), cpu_ref_us_p99=float(np.percentile(rl, 99) * 1e6),
+                   max_abs_x_diff=float(np.abs(rx - xs).max()),
+                   max_rel_x_diff=float((np.abs(rx - xs).max(1) / np.maximum(1, np.abs(rx).max(1))).max()))
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

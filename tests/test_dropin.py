@@ -151,13 +151,35 @@ def test_solve_without_gpu_fails_loudly():
 
 # ---------------------------------------------------------------- GPU parity
 
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "mixed_crawl_blflfr", "c30_tol1e-6", "c30_tol1e-2"])
+def test_dropin_fast_default_with_reference_permutation(name):
+    """Default (fast) drop-in given the reference's permutation: same pivots and
+    regularisations, so x, y, z, s agree to 1e-6 even at the controller's tol 1e-2
+    on the 30/68/18 controller shape."""
+    g = golden(name)
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    for q in range(0, g["x"].shape[0], 3):
+        r = dropin.solve_dense(*_golden_dense_args(g, q), perm=g["perm"][q], ordering=int(g["ordering"]),
+                               reltol=tol, abstol=tol, maxit=maxit)
+        assert r["flag"] == int(g["flag"][q]), r["error"]
+        for k in ("x", "z", "s") + (("y",) if int(g["p"]) else ()):
+            scale = max(1.0, float(np.abs(g[k][q]).max()))
+            assert np.abs(r[k] - g[k][q]).max() <= 1e-6 * scale, (name, q, k)
+
 DENSE = ["c1_tol1e-6", "c1_tol1e-2", "c1_rowmajor", "c1_noeq", "edge_zero_g_row", "mixed_stance4",
          "mixed_trot_blfr", "mixed_crawl_blflfr", "c1_maxit0", "c1_maxit2", "c1_maxit5"]
 
 
+@pytest.fixture
+def exact_mode(monkeypatch):
+    monkeypatch.setenv("QPSWIFT_HIP_EXACT", "1")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", DENSE)
-def test_dropin_dense_bit_identical_to_reference(name):
+def test_dropin_dense_bit_identical_to_reference(name, exact_mode):
     g = golden(name)
     tol, maxit = float(g["tol"]), int(g["maxit"])
     for q in range(0, g["x"].shape[0], 7):
@@ -176,7 +198,7 @@ def test_dropin_dense_bit_identical_to_reference(name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["csc_sigma0", "csc_sigma0.05"])
-def test_dropin_csc_bit_identical_to_reference(name):
+def test_dropin_csc_bit_identical_to_reference(name, exact_mode):
     g = golden(name)
     n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
     tol, maxit = float(g["tol"]), int(g["maxit"])
@@ -193,7 +215,8 @@ def test_dropin_csc_bit_identical_to_reference(name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "mixed_trot_brfl"])
 def test_dropin_controller_call_own_ordering(name):
-    """Permut = NULL as main.cpp:1649 passes it: own ordering, within 1e-6."""
+    """Permut = NULL as main.cpp:1649 passes it, default (fast) kernels: own
+    ordering, within 1e-6."""
     g = golden(name)
     tol = float(g["tol"])
     for q in range(0, g["x"].shape[0], 5):
@@ -205,7 +228,7 @@ def test_dropin_controller_call_own_ordering(name):
 
 
 @pytest.mark.gpu
-def test_dropin_reuses_qp_and_plan_cache():
+def test_dropin_reuses_qp_and_plan_cache(exact_mode):
     """Solving the same QP object twice and many QPs of one pattern (plan cache)."""
     g = golden("c1_tol1e-6")
     L = _lib.lib()
