@@ -330,7 +330,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         qpb_wsync();
 #pragma unroll
         for (int e = 0; e < ND; e++) H[e] = H0[e];
-        {
+        if constexpr (QPB_W_GG) {      // small G: every (r, j) unrolled, products precomputed
             int e = 0;
 #pragma unroll
             for (int r = 0; r < NZ; r++) {
@@ -338,12 +338,23 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
                 for (int j = 0; j < NX; j++)
                     if (qpb_Gnz[r][j]) {
-                        const int xe = qpb_xpos[j];
-                        if constexpr (QPB_W_GG) H[xe] = __builtin_fma(GG[e], wr, H[xe]);
-                        else H[xe] = __builtin_fma(GC(r) * wr, Gd[j * NZ + r], H[xe]);
+                        H[qpb_xpos[j]] = __builtin_fma(GG[e], wr, H[qpb_xpos[j]]);
                         e++;
                     }
             }
+        } else {                       // per column-pattern group: rows looped, columns unrolled
+            qpb_for<0, QPB_NGRP>([&](auto gc) {
+                constexpr int g = decltype(gc)::value;
+#pragma nounroll
+                for (int u = qpb_goff[g]; u < qpb_goff[g + 1]; u++) {
+                    const int r = __builtin_amdgcn_readfirstlane(qpb_grow[u]);
+                    const double t = dxm * Gd[dxi * NZ + r] * Vb[r];     // G(r, i) w_r
+                    qpb_for<0, qpb_gncol[g]>([&](auto cc) {
+                        constexpr int j = qpb_gcol[g][decltype(cc)::value];
+                        H[qpb_xpos[j]] = __builtin_fma(t, Gd[j * NZ + r], H[qpb_xpos[j]]);
+                    });
+                }
+            });
         }
         double kdz[ND];
         qpb_for<0, ND>([&](auto kc) {
@@ -470,107 +481,86 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     };
 
     QPB_TS(1);
-    // ---- kkt_initialize (Auxilary.c:992-1089): K with -I, rhs [-c; b; h]
-    double x, y, s[ZC], z[ZC];
-    {
-        double m1[ZC], dzi[ZC];
+    // ---- kkt_initialize (Auxilary.c:992-1089) as iteration -1, then the
+    // QP_SOLVE loop (qpSWIFT.c:502-602).  One instance of factor() and of
+    // solve() serves the setup solve, the predictor and the corrector, which
+    // keeps the kernel's code small enough for the instruction cache.
+    double x = 0.0, y = 0.0, s[ZC], z[ZC];
 #pragma unroll
-        for (int t = 0; t < ZC; t++) m1[t] = -1.0;
-        factor(m1);
-        QPB_TS(2);
-        solve(-cx, by, hz, x, y, dzi);
-        QPB_TS(3);
-        if (lane < NX) Vb[lane] = x;
-        qpb_wsync();
-        double zi[ZC];
-#pragma unroll
-        for (int t = 0; t < ZC; t++) {
-            double gx = 0.0;
-#pragma unroll
-            for (int j = 0; j < NX; j++) gx = __builtin_fma(GR(t, j), Vb[j], gx);
-            zi[t] = hz[t] - gx;
-        }
-        qpb_wsync();
-        const double lo = -zmax([&](int t) { return -zi[t]; }, -1e300);
-        const double hi = zmax([&](int t) { return zi[t]; }, -1e300);
-        const double sh = -lo;
-#pragma unroll
-        for (int t = 0; t < ZC; t++) {
-            s[t] = sh < 0 ? zi[t] : zi[t] + (1 + sh);
-            z[t] = hi < 0 ? -zi[t] : -zi[t] + (1 + hi);
-            if (!isz[t]) { s[t] = 1.0; z[t] = 1.0; }
-        }
-        if (!isx) x = 0.0;
-        if (!isy) y = 0.0;
-    }
-
-    // ---- QP_SOLVE loop (qpSWIFT.c:502-602)
-    long it = 0;
+    for (int t = 0; t < ZC; t++) { s[t] = 1.0; z[t] = 1.0; }
+    long it = -1;
     int flag = 3;
     double fval = 0.0, st_rx = 0.0, st_ry = 0.0, st_rz = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;
     double sigma = 100.0;
-    QPB_TS(4);
     for (;;) {
-        if (it >= a.maxit) { flag = 2; break; }
-        QPB_TS(8 + 8 * it);
-        // residuals (Auxilary.c:745-786), objective (Auxilary.c:1133-1141)
-        if (lane < NX) Vb[lane] = x;
+        double rx = 0.0, ry = 0.0, rz[ZC], rzi[ZC], kd[ZC], sz = 1.0, mu = 0.0;
+        bool pc = true;
+        if (it >= 0) {
+            if (it >= a.maxit) { flag = 2; break; }
+            QPB_TS(8 + 8 * it);
+            // residuals (Auxilary.c:745-786), objective (Auxilary.c:1133-1141)
+            if (lane < NX) Vb[lane] = x;
 #pragma unroll
-        for (int t = 0; t < ZC; t++)
-            if (isz[t]) Vb[NX + lane + 64 * t] = z[t];
-        if (lane < NY) Vb[NX + NZ + lane] = y;
-        qpb_wsync();
-        double tp = 0.0, ry = by, rz[ZC], rx = -cx;
+            for (int t = 0; t < ZC; t++)
+                if (isz[t]) Vb[NX + lane + 64 * t] = z[t];
+            if (lane < NY) Vb[NX + NZ + lane] = y;
+            qpb_wsync();
+            double tp = 0.0;
+            ry = by;
+            rx = -cx;
 #pragma unroll
-        for (int t = 0; t < ZC; t++) rz[t] = hz[t] - s[t];
+            for (int t = 0; t < ZC; t++) rz[t] = hz[t] - s[t];
 #pragma unroll
-        for (int j = 0; j < NX; j++) {
-            const double xj = Vb[j];
-            tp = __builtin_fma(-PR(j), xj, tp);
+            for (int j = 0; j < NX; j++) {
+                const double xj = Vb[j];
+                tp = __builtin_fma(-PR(j), xj, tp);
 #pragma unroll
-            for (int t = 0; t < ZC; t++) rz[t] = __builtin_fma(-GR(t, j), xj, rz[t]);
-            if constexpr (NY > 0) ry = __builtin_fma(-AR(j), xj, ry);
-        }
-        {
-            double ra[QPB_W_SPLIT];
+                for (int t = 0; t < ZC; t++) rz[t] = __builtin_fma(-GR(t, j), xj, rz[t]);
+                if constexpr (NY > 0) ry = __builtin_fma(-AR(j), xj, ry);
+            }
+            {
+                double ra[QPB_W_SPLIT];
 #pragma unroll
-            for (int k = 0; k < QPB_W_SPLIT; k++) ra[k] = k ? 0.0 : rx;
+                for (int k = 0; k < QPB_W_SPLIT; k++) ra[k] = k ? 0.0 : rx;
 #pragma unroll
-            for (int r = 0; r < NZ; r++)   // G(r, i): the dense-row slice when dense row i is x_i
-                ra[r % QPB_W_SPLIT] = __builtin_fma(-(QPB_XID ? GC(r) : Gd[ix * NZ + r]), Vb[NX + r], ra[r % QPB_W_SPLIT]);
+                for (int r = 0; r < NZ; r++)   // G(r, i): the dense-row slice when dense row i is x_i
+                    ra[r % QPB_W_SPLIT] = __builtin_fma(-(QPB_XID ? GC(r) : Gd[ix * NZ + r]), Vb[NX + r], ra[r % QPB_W_SPLIT]);
 #pragma unroll
-            for (int l = 0; l < NY; l++)
-                ra[(NZ + l) % QPB_W_SPLIT] =
-                    __builtin_fma(-(QPB_XID ? AC(l) : Ad[ix * NY + l]), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
-            rx = ra[0];
+                for (int l = 0; l < NY; l++)
+                    ra[(NZ + l) % QPB_W_SPLIT] =
+                        __builtin_fma(-(QPB_XID ? AC(l) : Ad[ix * NY + l]), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
+                rx = ra[0];
 #pragma unroll
-            for (int k = 1; k < QPB_W_SPLIT; k++) rx += ra[k];
-        }
-        qpb_wsync();
-        rx += tp;
-        fval = qpb_rsum<ROWS_X>(isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0);
-        st_rx = __builtin_sqrt(qpb_rsum<ROWS_X>(isx ? rx * rx : 0.0));
-        st_ry = NY > 0 ? __builtin_sqrt(qpb_rsum<ROWS_Y>(isy ? ry * ry : 0.0)) : 0.0;
-        st_rz = __builtin_sqrt(zsum([&](int t) { return rz[t] * rz[t]; }));
-        const double sz = zsum([&](int t) { return s[t] * z[t]; });
-        st_mu = sz * (1.0 / NZ);
-        if (st_rx < a.tol && st_rz < a.tol && (NY == 0 || st_ry < a.tol) && st_mu < a.abstol) { flag = 0; break; }
-        QPB_TS(9 + 8 * it);
-        const double mu = st_mu;
-        const bool pc = sigma > a.sigma_d;
-        double rzi[ZC], kd[ZC];
+                for (int k = 1; k < QPB_W_SPLIT; k++) rx += ra[k];
+            }
+            qpb_wsync();
+            rx += tp;
+            fval = qpb_rsum<ROWS_X>(isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0);
+            st_rx = __builtin_sqrt(qpb_rsum<ROWS_X>(isx ? rx * rx : 0.0));
+            st_ry = NY > 0 ? __builtin_sqrt(qpb_rsum<ROWS_Y>(isy ? ry * ry : 0.0)) : 0.0;
+            st_rz = __builtin_sqrt(zsum([&](int t) { return rz[t] * rz[t]; }));
+            sz = zsum([&](int t) { return s[t] * z[t]; });
+            st_mu = sz * (1.0 / NZ);
+            if (st_rx < a.tol && st_rz < a.tol && (NY == 0 || st_ry < a.tol) && st_mu < a.abstol) { flag = 0; break; }
+            QPB_TS(9 + 8 * it);
+            mu = st_mu;
+            pc = sigma > a.sigma_d;
 #pragma unroll
-        for (int t = 0; t < ZC; t++) {
-            rzi[t] = qpb_rcp(z[t]);
-            kd[t] = isz[t] ? -s[t] * rzi[t] : -1.0;   // updatekktmatrix (Auxilary.c:211-215)
+            for (int t = 0; t < ZC; t++) {
+                rzi[t] = qpb_rcp(z[t]);
+                kd[t] = isz[t] ? -s[t] * rzi[t] : -1.0;   // updatekktmatrix (Auxilary.c:211-215)
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < ZC; t++) { kd[t] = -1.0; rzi[t] = 1.0; rz[t] = 0.0; }   // KKT with -I
         }
         factor(kd);
-        QPB_TS(10 + 8 * it);
+        QPB_TS(it >= 0 ? 10 + 8 * it : 2);
         if (!pc) sigma = a.sigma_d;
         double cc[ZC];
 #pragma unroll
         for (int t = 0; t < ZC; t++) cc[t] = sigma * mu;
-        double dx, dy, dz[ZC], dsl[ZC], bz[ZC];
+        double dx, dy, dz[ZC], dsl[ZC];
         auto step_length = [&]() {
             // alpha = min over d < 0 of v/(-d) == 1 / max(-d/v); 1 if none (Auxilary.c:359-393)
             const double bp = zmax([&](int t) { return -dsl[t] * __builtin_amdgcn_rcp(s[t]); }, 0.0);
@@ -578,42 +568,75 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             ap = bp > 1e-10 ? __builtin_amdgcn_rcp(bp) : 1.0;
             ad = bd > 1e-10 ? __builtin_amdgcn_rcp(bd) : 1.0;
         };
-        if (pc) {
-            // predictor (kktsolve_1, Auxilary.c:471-515): ds = -s.*z
+        // pass 2: setup solve, rhs [-c; b; h]; pass 0: predictor (kktsolve_1,
+        // Auxilary.c:471-515), ds = -s.*z; pass 1: corrector / centering
+        // (kktsolve_2, Auxilary.c:524-564)
+        int pass = it < 0 ? 2 : (pc ? 0 : 1);
+        for (;;) {
+            double bxv = rx, byv = ry, bz[ZC];
 #pragma unroll
-            for (int t = 0; t < ZC; t++) bz[t] = rz[t] + s[t];
-            solve(rx, ry, bz, dx, dy, dz);
-            QPB_TS(11 + 8 * it);
+            for (int t = 0; t < ZC; t++)
+                bz[t] = pass == 2 ? hz[t] : (pass == 0 ? rz[t] + s[t] : __builtin_fma(-cc[t], rzi[t], rz[t] + s[t]));
+            if (pass == 2) { bxv = -cx; byv = by; }
+            solve(bxv, byv, bz, dx, dy, dz);
+            QPB_TS(it >= 0 ? (pass == 0 ? 11 : 13) + 8 * it : 3);
+            if (pass == 2) {
+                // initial point: x0, y0 from the solve; s0, z0 from r = h - G x0
+                x = isx ? dx : 0.0;
+                y = isy ? dy : 0.0;
+                if (lane < NX) Vb[lane] = x;
+                qpb_wsync();
+                double zi[ZC];
 #pragma unroll
-            for (int t = 0; t < ZC; t++) dsl[t] = -s[t] * __builtin_fma(dz[t], rzi[t], 1.0);
-            step_length();
-            const double rho = zsum([&](int t) { return (s[t] + ap * dsl[t]) * (z[t] + ad * dz[t]); }) * qpb_rcp(sz);   // formrho
-            const double r1 = 1 > rho ? rho : 1;
-            const double cube = r1 * r1 * r1;
-            sigma = a.sigma_d < cube ? cube : a.sigma_d;
+                for (int t = 0; t < ZC; t++) {
+                    double gx = 0.0;
 #pragma unroll
-            for (int t = 0; t < ZC; t++) cc[t] = __builtin_fma(-dsl[t], dz[t], sigma * mu);
-            QPB_TS(12 + 8 * it);
-        }
-        // corrector / centering (kktsolve_2, Auxilary.c:524-564)
+                    for (int j = 0; j < NX; j++) gx = __builtin_fma(GR(t, j), Vb[j], gx);
+                    zi[t] = hz[t] - gx;
+                }
+                qpb_wsync();
+                const double lo = -zmax([&](int t) { return -zi[t]; }, -1e300);
+                const double hi = zmax([&](int t) { return zi[t]; }, -1e300);
+                const double sh = -lo;
 #pragma unroll
-        for (int t = 0; t < ZC; t++) bz[t] = __builtin_fma(-cc[t], rzi[t], rz[t] + s[t]);
-        solve(rx, ry, bz, dx, dy, dz);
-        QPB_TS(13 + 8 * it);
-#pragma unroll
-        for (int t = 0; t < ZC; t++) dsl[t] = __builtin_fma(__builtin_fma(-s[t], dz[t], cc[t]), rzi[t], -s[t]);
-        step_length();
-        QPB_TS(14 + 8 * it);
-        ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
-        ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
-        if (isx) x = __builtin_fma(dx, ap, x);
-        if (isy) y = __builtin_fma(dy, ad, y);
-#pragma unroll
-        for (int t = 0; t < ZC; t++)
-            if (isz[t]) {
-                s[t] = __builtin_fma(dsl[t], ap, s[t]);
-                z[t] = __builtin_fma(dz[t], ad, z[t]);
+                for (int t = 0; t < ZC; t++) {
+                    s[t] = sh < 0 ? zi[t] : zi[t] + (1 + sh);
+                    z[t] = hi < 0 ? -zi[t] : -zi[t] + (1 + hi);
+                    if (!isz[t]) { s[t] = 1.0; z[t] = 1.0; }
+                }
+                QPB_TS(4);
+                break;
             }
+            if (pass == 0) {
+#pragma unroll
+                for (int t = 0; t < ZC; t++) dsl[t] = -s[t] * __builtin_fma(dz[t], rzi[t], 1.0);
+                step_length();
+                const double rho = zsum([&](int t) { return (s[t] + ap * dsl[t]) * (z[t] + ad * dz[t]); }) * qpb_rcp(sz);   // formrho
+                const double r1 = 1 > rho ? rho : 1;
+                const double cube = r1 * r1 * r1;
+                sigma = a.sigma_d < cube ? cube : a.sigma_d;
+#pragma unroll
+                for (int t = 0; t < ZC; t++) cc[t] = __builtin_fma(-dsl[t], dz[t], sigma * mu);
+                QPB_TS(12 + 8 * it);
+                pass = 1;
+                continue;
+            }
+#pragma unroll
+            for (int t = 0; t < ZC; t++) dsl[t] = __builtin_fma(__builtin_fma(-s[t], dz[t], cc[t]), rzi[t], -s[t]);
+            step_length();
+            QPB_TS(14 + 8 * it);
+            ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
+            ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
+            if (isx) x = __builtin_fma(dx, ap, x);
+            if (isy) y = __builtin_fma(dy, ad, y);
+#pragma unroll
+            for (int t = 0; t < ZC; t++)
+                if (isz[t]) {
+                    s[t] = __builtin_fma(dsl[t], ap, s[t]);
+                    z[t] = __builtin_fma(dz[t], ad, z[t]);
+                }
+            break;
+        }
         it++;
     }
     QPB_TS(370);
