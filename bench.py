@@ -45,8 +45,6 @@ def parse():
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave"])
     ap.add_argument("--no-mixed", dest="mixed", action="store_false",
                     help="skip the configs[2] leg (4 gait patterns x 1024 QPs)")
-    ap.add_argument("--argmin", default="separate", choices=["fused", "separate"],
-                    help="fused: one qpb_solve_best call per step; separate: qpb_solve + qpb_argmin calls")
     ap.add_argument("--tol", type=float, default=1e-6)
     ap.add_argument("--exact", action="store_true", help="bench the bit-faithful kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -117,7 +115,7 @@ def cpu_baseline(seed, sample, passes, tol):
                 mean_iters=float(iters.mean()), optimal_frac=float((flags == 0).mean()))
 
 
-def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, argmin="fused"):
+def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True):
     """Timed loop of `steps` steps (solve + argmin [+ all_gather]) on resident
     inputs.  Returns (wall seconds max over ranks, mean kernel ms max over
     ranks, outputs, gathered winners)."""
@@ -131,14 +129,11 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ar
     best = torch.zeros(2, dtype=torch.float64, device=dev)     # {fval, index}
     gathered = torch.empty(2 * world, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev)
-    # one step = solve + argmin (HIP events time the solve kernel alone)
-    if argmin == "fused":
-        solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream, best=best)
-        post = lambda: None
-    else:
-        from apf_quadruped_amd.batch import argmin_launcher
-        solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream)
-        post = argmin_launcher(out["fval"], out["flag"], best, stream=stream)
+    # one step = solve + argmin, stream-ordered (an overlapped two-stream variant
+    # was CPU-bound on the per-step event calls: 65.8 vs 50.8 us per step)
+    from apf_quadruped_amd.batch import argmin_launcher
+    solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream)
+    post = argmin_launcher(out["fval"], out["flag"], best, stream=stream)
     coll = gather and world > 1
 
     def exchange():
@@ -261,8 +256,7 @@ def main():
     plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=args.exact, kernel=args.kernel)
     plan.compile()
     B = args.batch
-    elapsed, kern_ms, out, gathered = run_leg(plan, B, args.steps, args.warmup, args.tol, dev, rank, world, seed,
-                                              argmin=args.argmin)
+    elapsed, kern_ms, out, gathered = run_leg(plan, B, args.steps, args.warmup, args.tol, dev, rank, world, seed)
     kname = plan.kernel_name(B)
     flags = out["flag"].cpu().numpy()
     iters = out["iters"].cpu().numpy()
