@@ -26,7 +26,7 @@ class QpbPlanInfo(C.Structure):
                 ("nnzK", C.c_long), ("lnz", C.c_long),
                 ("fac_updates", C.c_long), ("fac_divs", C.c_long),
                 ("ordering", C.c_int), ("exact", C.c_int), ("hash", C.c_uint64),
-                ("wave_ok", C.c_int), ("wave_max_batch", C.c_long)]
+                ("wave_ok", C.c_int), ("wave_max_batch", C.c_long), ("wave_qpw", C.c_int)]
 
 
 _lib = None

@@ -21,8 +21,11 @@ from . import _lib
 from ._lib import QpbPlanInfo, QpbSettings, check
 
 QPB_P_FULL, QPB_P_UPPER, QPB_EXACT = 0x0, 0x1, 0x10
-QPB_KERNEL_LANE, QPB_KERNEL_WAVE = 0x100, 0x200
-KERNEL_FLAGS = {"auto": 0, "lane": QPB_KERNEL_LANE, "wave": QPB_KERNEL_WAVE}
+QPB_KERNEL_LANE, QPB_KERNEL_WAVE, QPB_KERNEL_NOROW = 0x100, 0x200, 0x400
+# "wave" = the wave kernel in the form the plan picks (row form: four QPs per
+# wavefront, where it fits); "wave1" = one QP per wavefront regardless
+KERNEL_FLAGS = {"auto": 0, "lane": QPB_KERNEL_LANE, "wave": QPB_KERNEL_WAVE,
+                "wave1": QPB_KERNEL_WAVE | QPB_KERNEL_NOROW, "auto1": QPB_KERNEL_NOROW}
 QP_OPTIMAL, QP_KKTFAIL, QP_MAXIT, QP_FATAL = 0, 1, 2, 3
 
 
@@ -116,7 +119,9 @@ class Plan:
     @classmethod
     def from_dense(cls, n, m, p, P, A, G, perm=None, p_upper=True, exact=False, kernel="auto"):
         """Plan for the non-zero pattern of one dense QP (P [n,n], A [p,n], G [m,n]).
-        kernel: "auto" (wave kernel for small batches when eligible), "lane", "wave"."""
+        kernel: "auto" (wave kernel for small batches when eligible), "lane", "wave"
+        (its row form -- four QPs per wavefront -- where the pattern fits a 16-lane
+        row), "wave1" / "auto1" (as "wave" / "auto" but one QP per wavefront)."""
         Pjc, Pir = dense_pattern(P, upper=p_upper)
         Ajc, Air = dense_pattern(A) if p else (None, None)
         Gjc, Gir = dense_pattern(G)
@@ -131,7 +136,8 @@ class Plan:
         return buf.value.decode()
 
     def kernel_for(self, B: int) -> str:
-        """Which kernel qpb_solve runs for a batch of B ("wave" or "lane")."""
+        """Which kernel qpb_solve runs for a batch of B ("wave" or "lane"; the wave
+        kernel's form is info.wave_qpw: 4 QPs per wavefront = row form)."""
         i = self.info
         if i.wave_ok and (i.wave_max_batch < 0 or B <= i.wave_max_batch):
             return "wave"

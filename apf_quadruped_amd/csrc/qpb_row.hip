@@ -1,0 +1,517 @@
+// qpb_row.hip -- row-cooperative IPM kernel: ONE 16-lane row per QP, four QPs
+// per wavefront.
+//
+// Template source like qpb_wave.hip (the host prepends sizes, tables and the
+// kernel name; qpb_wave.cpp generate_row_kernel).  Same algorithm and the same
+// elimination as the wave kernel's common case -- every z and y row is a leaf
+// and the x block is factored in natural order (QPB_XID) -- for plans small
+// enough that one QP fits a 16-lane DPP row: n <= 16, p <= 16, m <= 32.
+//
+// Lane c of a row holds x_c, y_c, z_c / s_c (c < 16) and z_{16+c} / s_{16+c}
+// (second register when m > 16).  Every cross-lane move is inside the row, so
+// it is a DPP row_newbcast folded into the consuming v_fmac_f64 (no LDS round
+// trips, no SGPR traffic), and every reduction is a 4-stage row butterfly that
+// leaves the result in all 16 lanes.  LDS is used once per factorisation, to
+// transpose L for the backward solve, and for the input staging.  A QP that
+// converges freezes while the other rows of its wave go on.
+//
+// Reference: qpSWIFT's Mehrotra predictor-corrector (qpSWIFT.c:473-644,
+// kkt_initialize Auxilary.c:992-1089), LDL' with dynamic regularisation
+// (ldl.c:253-326), residuals (Auxilary.c:745-786), step length
+// (Auxilary.c:359-393).  Fast mode: FMA contraction, reciprocal pivots.
+#pragma clang fp contract(fast)
+
+template <int V> struct qpb_ic { static constexpr int value = V; };
+
+struct qpb_args {
+    const double *P, *A, *G, *c, *h, *b;
+    double *x, *y, *z, *s;
+    int *flag, *iters;
+    double *fval;
+    double *stats;
+    long B;
+    double tol, abstol, sigma_d;
+    long maxit;
+};
+
+#ifndef QPB_R_TIMING
+#define QPB_R_TIMING 0    // 2: per-QP start / end (realtime, cycles), iterations, hardware ids into stats
+#endif
+
+#define NX QPB_NX
+#define NZ QPB_NZ
+#define NY QPB_NY
+#define NY1 (NY > 0 ? NY : 1)
+#define WPB (QPB_WG / 64)
+#define ZH (NZ > 16)
+// per-row LDS (doubles): staging Pd[NX*NX] Ad[NY1*NX] Gd[NZ*NX] | Tx[NX*NX]
+// (columns of -L, one contiguous run per lane) | PR[NX*NX] (-P rows) | H0s[NX*NX]
+#define EVEN(v) (((v) + 1) & ~1)
+#define OFF_A (NX * NX)
+#define OFF_G (OFF_A + NY1 * NX)
+#define OFF_T EVEN(OFF_G + NZ * NX)
+#define OFF_PR EVEN(OFF_T + NX * NX)
+#define OFF_H0 EVEN(OFF_PR + NX * NX)
+#define LDS_ROW EVEN(OFF_H0 + NX * NX)
+
+static __device__ __forceinline__ double qpb_rcp(double v) {
+    double r = __builtin_amdgcn_rcp(v);
+    double e = __builtin_fma(-v, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-v, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+// 1 / regularise(d) (ldl.c:273-274): v_rcp_f64 + one Newton step, computed
+// unconditionally; |d| <= 1e-14 -> 1/(+-1e-7), sign as ldl.c:273
+static __device__ __forceinline__ double qpb_rcp_reg(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    asm("" : "+v"(r));     // keeps the rare regularised case from becoming a branch
+    const double reg = d > 0.0 ? 1e7 : -1e7;
+    return __builtin_fabs(d) <= 1e-14 ? reg : r;
+}
+
+template <int J0, int J1, class F> static __device__ __forceinline__ void qpb_for(F &&f) {
+    if constexpr (J0 < J1) {
+        f(qpb_ic<J0>{});
+        qpb_for<J0 + 1, J1>(f);
+    }
+}
+
+// lane J of this row, in every lane of the row (compiler DPP move)
+template <int J> static __device__ __forceinline__ double qpb_nb(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
+}
+template <int CTRL> static __device__ __forceinline__ double qpb_dpp(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, CTRL, 0xf, 0xf, true);
+}
+
+// acc += (src of row lane J) * m as one v_fmac_f64 with a DPP row_newbcast
+// source.  A DPP source must not have been written by the two preceding VALU
+// instructions:
+//  - qpb_fxs: src is a static slice written in the prologue (never a hazard);
+//  - qpb_fx:  src is dynamic; the phase starts with qpb_fence(src, ...), and
+//             both are volatile so they keep their order;
+//  - qpb_fxd: the chained triangular solves (src is the accumulator itself).
+template <int J> static __device__ __forceinline__ void qpb_fxs(double &acc, double src, double m) {
+    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "+v"(acc) : "v"(src), "v"(m), "i"(J));
+}
+template <int J> static __device__ __forceinline__ void qpb_fx(double &acc, double src, double m) {
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                 : "+v"(acc) : "v"(src), "v"(m), "i"(J));
+}
+template <int J> static __device__ __forceinline__ void qpb_fxd(double &t, double m) {
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                 : "+v"(t) : "v"(m), "i"(J));
+}
+static __device__ __forceinline__ void qpb_fence(double a) { asm volatile("s_nop 1" ::"v"(a)); }
+static __device__ __forceinline__ void qpb_fence(double a, double b) { asm volatile("s_nop 1" ::"v"(a), "v"(b)); }
+static __device__ __forceinline__ void qpb_fence(double a, double b, double c) {
+    asm volatile("s_nop 1" ::"v"(a), "v"(b), "v"(c));
+}
+static __device__ __forceinline__ void qpb_fence(double a, double b, double c, double d) {
+    asm volatile("s_nop 1" ::"v"(a), "v"(b), "v"(c), "v"(d));
+}
+
+// K sums / maxima over the 16 lanes of each row, stage-major (the K chains
+// overlap); the result is in every lane of the row
+template <int K> static __device__ __forceinline__ void qpb_rsum(double (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += qpb_dpp<0xB1>(v[k]);    // quad_perm [1,0,3,2]
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += qpb_dpp<0x4E>(v[k]);    // quad_perm [2,3,0,1]
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += qpb_dpp<0x141>(v[k]);   // row_half_mirror
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += qpb_dpp<0x140>(v[k]);   // row_mirror
+}
+template <int K> static __device__ __forceinline__ void qpb_rmax(double (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_fmax(v[k], qpb_dpp<0xB1>(v[k]));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_fmax(v[k], qpb_dpp<0x4E>(v[k]));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_fmax(v[k], qpb_dpp<0x141>(v[k]));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_fmax(v[k], qpb_dpp<0x140>(v[k]));
+}
+
+// LDS of a row is touched by the lanes of one wave only: in-order per wave, so
+// a compiler fence is all that is needed between a store and another lane's load
+static __device__ __forceinline__ void qpb_wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+static __device__ __forceinline__ bool qpb_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
+
+extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
+    __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * 4 * LDS_ROW];
+    const int lane = threadIdx.x & 63, row = lane >> 4, c = lane & 15;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long q0 = ((long)blockIdx.x * WPB + wv) * 4;
+    if (q0 >= a.B) return;                     // wave-uniform
+#if QPB_R_TIMING == 2
+    const double t_rt0 = (double)__builtin_amdgcn_s_memrealtime(), t_cy0 = (double)__builtin_readcyclecounter();
+#endif
+    const long q = q0 + row;
+    const bool valid = q < a.B;
+    const long qc = valid ? q : a.B - 1;       // rows past the batch solve a copy, write nothing
+    const long tile = qc >> 6;
+    const int ql = (int)(qc & 63);
+    double *__restrict__ Ls = qpb_lds + (wv * 4 + row) * LDS_ROW;
+    const bool isx = c < NX, isy = c < NY, isz0 = c < NZ, isz1 = 16 + c < NZ;
+    const int ix = isx ? c : NX - 1, iy = isy ? c : (NY > 0 ? NY - 1 : 0);
+    const int iz0 = isz0 ? c : NZ - 1, iz1 = isz1 ? 16 + c : NZ - 1;
+    constexpr double RDY = 1.0 / -1e-7;        // leaf y pivots: D = 0 regularised to -1e-7
+
+    // ---- stage this QP's P, A, G as dense matrices in the row's LDS
+    constexpr int NPL = (QPB_NNZP + 15) / 16, NGL = (QPB_NNZG + 15) / 16, NAL = (QPB_NNZA + 15) / 16;
+    double vP[NPL], vG[NGL], vA[NAL > 0 ? NAL : 1];
+    int iP[NPL], iP2[NPL], iG[NGL], iA[NAL > 0 ? NAL : 1];
+    {
+        const double *tP = a.P + tile * (QPB_NNZP * 64) + ql;
+        const double *tG = a.G + tile * (QPB_NNZG * 64) + ql;
+#pragma unroll
+        for (int u = 0; u < NPL; u++) {
+            const int k = c + 16 * u;
+            const bool ok = k < QPB_NNZP;
+            vP[u] = ok ? tP[k * 64] : 0.0;
+            iP[u] = ok ? qpb_scP[k] : -1;
+            iP2[u] = ok ? qpb_scP2[k] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < NGL; u++) {
+            const int k = c + 16 * u;
+            const bool ok = k < QPB_NNZG;
+            vG[u] = ok ? tG[k * 64] : 0.0;
+            iG[u] = ok ? qpb_scG[k] : -1;
+        }
+#if NY > 0
+        const double *tA = a.A + tile * (QPB_NNZA * 64) + ql;
+#pragma unroll
+        for (int u = 0; u < NAL; u++) {
+            const int k = c + 16 * u;
+            const bool ok = k < QPB_NNZA;
+            vA[u] = ok ? tA[k * 64] : 0.0;
+            iA[u] = ok ? qpb_scA[k] : -1;
+        }
+#endif
+    }
+    const double cx = isx ? a.c[tile * (NX * 64) + c * 64 + ql] : 0.0;
+    const double hz0 = isz0 ? a.h[tile * (NZ * 64) + c * 64 + ql] : 0.0;
+    const double hz1 = isz1 ? a.h[tile * (NZ * 64) + (16 + c) * 64 + ql] : 0.0;
+#if NY > 0
+    const double by = isy ? a.b[tile * (NY * 64) + c * 64 + ql] : 0.0;
+#else
+    const double by = 0.0;
+#endif
+    for (int k = c; k < OFF_T; k += 16) Ls[k] = 0.0;
+    qpb_wsync();
+#pragma unroll
+    for (int u = 0; u < NPL; u++) {
+        if (iP[u] >= 0) Ls[iP[u]] = vP[u];
+        if (iP2[u] >= 0) Ls[iP2[u]] = vP[u];
+    }
+#pragma unroll
+    for (int u = 0; u < NGL; u++)
+        if (iG[u] >= 0) Ls[OFF_G + iG[u]] = vG[u];
+#pragma unroll
+    for (int u = 0; u < NAL; u++)
+        if (iA[u] >= 0) Ls[OFF_A + iA[u]] = vA[u];
+    qpb_wsync();
+    const double *Pd = Ls, *Ad = Ls + OFF_A, *Gd = Ls + OFF_G;
+    double *Tx = Ls + OFF_T, *PR = Ls + OFF_PR, *H0s = Ls + OFF_H0;
+    // Pd[j*NX+i] = P(i,j) (both triangles); Ad[j*NY+l] = A(l,j); Gd[j*NZ+r] = G(r,j)
+
+    // this lane's static slices, negated (every product is subtracted):
+    //   x_c: -P(c,:), -G(:,c), -A(:,c);  z_c / z_{16+c}: -G(c,:), -G(16+c,:);  y_c: -A(c,:)
+    // (-P rows and H0 rows are used once per iteration: parked in LDS, one
+    // contiguous run per lane, read where they are needed)
+    double nGc[NZ], nAc[NY1], nGl[NX], nGh[ZH ? NX : 1], nAr[NX];
+#pragma unroll
+    for (int j = 0; j < NX; j++) {
+        nGl[j] = isz0 ? -Gd[j * NZ + iz0] : 0.0;
+        if constexpr (ZH) nGh[j] = isz1 ? -Gd[j * NZ + iz1] : 0.0;
+        nAr[j] = isy ? -Ad[j * NY + iy] : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < NZ; r++) nGc[r] = isx ? -Gd[ix * NZ + r] : 0.0;
+#pragma unroll
+    for (int l = 0; l < NY1; l++) nAc[l] = (isx && NY > 0) ? -Ad[ix * NY + l] : 0.0;
+    // H0 = P (upper triangle, symmetrised) + 1e7 A'A (the leaf y rows folded into the x block)
+    {
+        double nP[NX], H0[NX];
+#pragma unroll
+        for (int j = 0; j < NX; j++) {
+            nP[j] = -Pd[j * NX + ix];
+            double v = ix <= j ? Pd[j * NX + ix] : Pd[ix * NX + j];
+#pragma unroll
+            for (int l = 0; l < NY; l++) v = __builtin_fma(Ad[ix * NY + l], -RDY * Ad[j * NY + l], v);
+            H0[j] = v;
+        }
+        if (isx) {
+#pragma unroll
+            for (int j = 0; j < NX; j++) { PR[c * NX + j] = nP[j]; H0s[c * NX + j] = H0[j]; }
+        }
+        qpb_wsync();
+    }
+
+    double H[NX], rDd = 0.0;
+    // factor with z diagonal kd: H = H0 + G' diag(w) G, w = -1/regularise(kd),
+    // then the LDL' of H (rows of -L in H, 1/D in rDd), -L transposed into Lt
+    auto factor = [&](double w0, double w1) {
+#pragma unroll
+        for (int e = 0; e < NX; e++) H[e] = H0s[ix * NX + e];
+        qpb_for<0, NZ>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            const double wr = r < 16 ? qpb_nb<(r & 15)>(w0) : qpb_nb<(r & 15)>(w1);
+            const double cr = nGc[r] * wr;        // -G(r,c) w_r
+            qpb_for<0, NX>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                if constexpr (qpb_Gnz[r][j]) qpb_fxs<j>(H[j], nGc[r], cr);   // += G(r,c) w_r G(r,j)
+            });
+        });
+        // right-looking LDL' in natural order; the pivot recurrence is the
+        // critical path: D_{k+1} comes from H'(k+1,k) and H'(k+1,k+1) with
+        // exactly the operations lane k+1's own update performs
+        double dpiv = qpb_nb<0>(H[0]);
+        qpb_for<0, NX>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const double rd = qpb_rcp_reg(dpiv);
+            if constexpr (k + 1 < NX) {
+                const double h = qpb_nb<k + 1>(H[k]), hkk = qpb_nb<k + 1>(H[k + 1]);
+                dpiv = __builtin_fma(h, h * -rd, hkk);
+            }
+            rDd = c == k ? rd : rDd;
+            const double nl = H[k] * -rd;        // -L(c,k)
+            qpb_for<k + 1, NX>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                qpb_fxs<j>(H[j], H[k], nl);        // H(c,j) -= L(c,k) H(j,k)
+            });
+            H[k] = c > k ? nl : 0.0;
+        });
+        // column c of -L, contiguous for lane c: Tx[c*NX + k] = -L(k, c)
+        if (isx) {
+#pragma unroll
+            for (int e = 0; e < NX; e++) Tx[e * NX + c] = H[e];
+        }
+        qpb_wsync();
+    };
+
+    // solve K [dx; dy; dz] = [bx; by; bz] with the current factor and w
+    auto solve = [&](double w0, double w1, double bx, double byv, double bz0, double bz1, double &dx, double &dy,
+                     double &dz0, double &dz1) {
+        const double v0 = -w0 * bz0, v1 = -w1 * bz1, yr = RDY * byv;   // leaf eliminations
+        qpb_fence(v0, v1, yr);
+        double ta[4] = {bx, 0.0, 0.0, 0.0};
+        qpb_for<0, NZ>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            qpb_fx<(r & 15)>(ta[r & 3], r < 16 ? v0 : v1, nGc[r]);
+        });
+        qpb_for<0, NY>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            qpb_fx<l>(ta[(NZ + l) & 3], yr, nAc[l]);
+        });
+        double t = (ta[0] + ta[1]) + (ta[2] + ta[3]);
+        qpb_for<0, NX>([&](auto kc) { qpb_fxd<decltype(kc)::value>(t, H[decltype(kc)::value]); });
+        t *= rDd;
+        double Lt[NX];
+#pragma unroll
+        for (int k = 0; k < NX; k++) Lt[k] = Tx[ix * NX + k];
+        qpb_for<0, NX>([&](auto kc) {
+            constexpr int k = NX - 1 - decltype(kc)::value;
+            qpb_fxd<k>(t, Lt[k]);
+        });
+        dx = t;
+        qpb_fence(t);
+        double g0 = 0.0, g1 = 0.0, gy = 0.0;
+        qpb_for<0, NX>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            qpb_fx<j>(g0, t, nGl[j]);
+            if constexpr (ZH && qpb_ghmask[j]) qpb_fx<j>(g1, t, nGh[j]);
+            if constexpr (NY > 0) qpb_fx<j>(gy, t, nAr[j]);
+        });
+        dz0 = -w0 * (bz0 + g0);                   // g = -G dx
+        dz1 = -w1 * (bz1 + g1);
+        dy = RDY * (byv + gy);
+    };
+
+    // ---- kkt_initialize (Auxilary.c:992-1089) as iteration -1, then the
+    // QP_SOLVE loop (qpSWIFT.c:502-602); the wave runs until all four rows stop
+    double x = 0.0, y = 0.0, s0 = 1.0, s1 = 1.0, z0 = 1.0, z1 = 1.0;
+    bool act = valid;
+    int flag = 3;
+    long itq = 0;
+    double st_rx2 = 0.0, st_ry2 = 0.0, st_rz2 = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0, fv = 0.0;
+    const double tol2 = a.tol > 0.0 ? a.tol * a.tol : -1.0;
+    double sigma = 100.0;
+    long it = -1;
+    for (;;) {
+        if (it >= 0 && it >= a.maxit) {
+            if (act) { flag = 2; itq = it; }
+            break;
+        }
+        // updatekktmatrix (Auxilary.c:211-215): z diagonal -s/z (-I at setup, s = z = 1)
+        const double rzi0 = qpb_rcp(z0), rzi1 = qpb_rcp(z1);
+        const double kd0 = isz0 ? -s0 * rzi0 : -1.0, kd1 = isz1 ? -s1 * rzi1 : -1.0;
+        const double w0 = -qpb_rcp_reg(kd0), w1 = -qpb_rcp_reg(kd1);
+        // residuals (Auxilary.c:745-786)
+        qpb_fence(x, y, z0, z1);
+        double tp = 0.0, ry = by, rz0 = hz0 - s0, rz1 = hz1 - s1, nPr[NX];
+#pragma unroll
+        for (int j = 0; j < NX; j++) nPr[j] = PR[ix * NX + j];
+        qpb_for<0, NX>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            qpb_fx<j>(rz0, x, nGl[j]);
+            if constexpr (ZH && qpb_ghmask[j]) qpb_fx<j>(rz1, x, nGh[j]);
+            if constexpr (NY > 0) qpb_fx<j>(ry, x, nAr[j]);
+            qpb_fx<j>(tp, x, nPr[j]);              // -P x
+        });
+        double ra[4] = {-cx, 0.0, 0.0, 0.0};
+        qpb_for<0, NZ>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            qpb_fx<(r & 15)>(ra[r & 3], r < 16 ? z0 : z1, nGc[r]);
+        });
+        qpb_for<0, NY>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            qpb_fx<l>(ra[(NZ + l) & 3], y, nAc[l]);
+        });
+        const double rx = ((ra[0] + ra[1]) + (ra[2] + ra[3])) + tp;
+        double red[4] = {isx ? rx * rx : 0.0, isy ? ry * ry : 0.0,
+                         (isz0 ? rz0 * rz0 : 0.0) + (isz1 ? rz1 * rz1 : 0.0),
+                         (isz0 ? s0 * z0 : 0.0) + (isz1 ? s1 * z1 : 0.0)};
+        qpb_rsum<4>(red);
+        const double sz = red[3];
+        // the factor does not depend on the residuals: formed before the exit
+        // test (wasted on a row's last iteration), overlapping the reductions
+        factor(w0, w1);
+        bool pc = true;
+        double mu = 0.0;
+        if (it >= 0) {
+            const double mu_it = sz * (1.0 / NZ);
+            if (act) {
+                fv = isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0;      // objective (Auxilary.c:1133-1141)
+                st_rx2 = red[0];
+                st_ry2 = NY > 0 ? red[1] : 0.0;
+                st_rz2 = red[2];
+                st_mu = mu_it;
+                if (red[0] < tol2 && red[2] < tol2 && (NY == 0 || red[1] < tol2) && mu_it < a.abstol) {
+                    flag = 0;
+                    itq = it;
+                    act = false;
+                }
+            }
+            if (!qpb_any(act)) break;
+            mu = mu_it;
+            pc = sigma > a.sigma_d;
+        }
+        if (!pc) sigma = a.sigma_d;
+        double cc0 = sigma * mu, cc1 = sigma * mu;
+        double dx, dy, dz0, dz1, dsl0, dsl1;
+        auto step_length = [&]() {
+            // alpha = min over d < 0 of v/(-d) == 1 / max(-d/v); 1 if none (Auxilary.c:359-393)
+            double bm[2] = {__builtin_fmax(isz0 ? -dsl0 * __builtin_amdgcn_rcp(s0) : 0.0,
+                                           isz1 ? -dsl1 * __builtin_amdgcn_rcp(s1) : 0.0),
+                            __builtin_fmax(isz0 ? -dz0 * rzi0 : 0.0, isz1 ? -dz1 * rzi1 : 0.0)};
+            bm[0] = __builtin_fmax(bm[0], 0.0);
+            bm[1] = __builtin_fmax(bm[1], 0.0);
+            qpb_rmax<2>(bm);
+            ap = bm[0] > 1e-10 ? __builtin_amdgcn_rcp(bm[0]) : 1.0;
+            ad = bm[1] > 1e-10 ? __builtin_amdgcn_rcp(bm[1]) : 1.0;
+        };
+        if (it < 0) {
+            // setup solve, rhs [-c; b; h] (Auxilary.c:1010-1040): x0, y0; then
+            // s0, z0 from r = h - G x0 = -dz (w = 1 exactly here)
+            solve(w0, w1, -cx, by, hz0, hz1, dx, dy, dz0, dz1);
+            x = isx ? dx : 0.0;
+            y = isy ? dy : 0.0;
+            const double zi0 = -dz0, zi1 = -dz1;
+            double lh[2] = {__builtin_fmax(isz0 ? -zi0 : -1e300, isz1 ? -zi1 : -1e300),
+                            __builtin_fmax(isz0 ? zi0 : -1e300, isz1 ? zi1 : -1e300)};
+            qpb_rmax<2>(lh);
+            const double sh = lh[0], hi = lh[1];    // sh = -min(zi)
+            s0 = sh < 0 ? zi0 : zi0 + (1 + sh);
+            s1 = sh < 0 ? zi1 : zi1 + (1 + sh);
+            z0 = hi < 0 ? -zi0 : -zi0 + (1 + hi);
+            z1 = hi < 0 ? -zi1 : -zi1 + (1 + hi);
+            if (!isz0) { s0 = 1.0; z0 = 1.0; }
+            if (!isz1) { s1 = 1.0; z1 = 1.0; }
+            it = 0;
+            continue;
+        }
+        if (qpb_any(act && pc)) {
+            // predictor (kktsolve_1, Auxilary.c:471-515), ds = -s.*z
+            solve(w0, w1, rx, ry, rz0 + s0, rz1 + s1, dx, dy, dz0, dz1);
+            dsl0 = -s0 * __builtin_fma(dz0, rzi0, 1.0);
+            dsl1 = -s1 * __builtin_fma(dz1, rzi1, 1.0);
+            step_length();
+            double rr[1] = {(isz0 ? (s0 + ap * dsl0) * (z0 + ad * dz0) : 0.0) +
+                            (isz1 ? (s1 + ap * dsl1) * (z1 + ad * dz1) : 0.0)};
+            qpb_rsum<1>(rr);
+            const double rho = rr[0] * qpb_rcp(sz);     // formrho
+            const double r1 = 1 > rho ? rho : 1;
+            const double cube = r1 * r1 * r1;
+            if (pc) {
+                sigma = a.sigma_d < cube ? cube : a.sigma_d;
+                cc0 = __builtin_fma(-dsl0, dz0, sigma * mu);
+                cc1 = __builtin_fma(-dsl1, dz1, sigma * mu);
+            }
+        }
+        // corrector / centering (kktsolve_2, Auxilary.c:524-564)
+        solve(w0, w1, rx, ry, __builtin_fma(-cc0, rzi0, rz0 + s0), __builtin_fma(-cc1, rzi1, rz1 + s1), dx, dy, dz0,
+              dz1);
+        dsl0 = __builtin_fma(__builtin_fma(-s0, dz0, cc0), rzi0, -s0);
+        dsl1 = __builtin_fma(__builtin_fma(-s1, dz1, cc1), rzi1, -s1);
+        step_length();
+        ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
+        ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
+        if (act) {
+            if (isx) x = __builtin_fma(dx, ap, x);
+            if (isy) y = __builtin_fma(dy, ad, y);
+            if (isz0) { s0 = __builtin_fma(dsl0, ap, s0); z0 = __builtin_fma(dz0, ad, z0); }
+            if (isz1) { s1 = __builtin_fma(dsl1, ap, s1); z1 = __builtin_fma(dz1, ad, z1); }
+        }
+        it++;
+    }
+    double fr[1] = {fv};
+    qpb_rsum<1>(fr);
+    // ---- outputs (tiled SoA)
+    if (valid) {
+        if (isx) a.x[tile * (NX * 64) + c * 64 + ql] = x;
+#if NY > 0
+        if (isy) a.y[tile * (NY * 64) + c * 64 + ql] = y;
+#endif
+        if (isz0) {
+            a.z[tile * (NZ * 64) + c * 64 + ql] = z0;
+            a.s[tile * (NZ * 64) + c * 64 + ql] = s0;
+        }
+        if (isz1) {
+            a.z[tile * (NZ * 64) + (16 + c) * 64 + ql] = z1;
+            a.s[tile * (NZ * 64) + (16 + c) * 64 + ql] = s1;
+        }
+        if (c == 0) {
+            a.flag[q] = flag;
+            a.iters[q] = (int)itq;
+            a.fval[q] = fr[0];
+            if (a.stats && QPB_R_TIMING != 2) {
+                double *o = a.stats + tile * 384 + ql;
+                o[0] = __builtin_sqrt(st_rx2); o[64] = __builtin_sqrt(st_ry2); o[128] = __builtin_sqrt(st_rz2);
+                o[192] = st_mu; o[256] = ap; o[320] = ad;
+            }
+#if QPB_R_TIMING == 2
+            if (a.stats) {
+                double *o = a.stats + tile * 384 + ql;
+                o[0] = t_rt0; o[64] = (double)__builtin_amdgcn_s_memrealtime();
+                o[128] = t_cy0; o[192] = (double)__builtin_readcyclecounter(); o[256] = (double)itq;
+                const unsigned hwid = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+                const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+                o[320] = (double)hwid + 4294967296.0 * (double)(xcc & 0xf);
+            }
+#endif
+        }
+    }
+}

@@ -184,11 +184,14 @@ int compile_plan(qpb_plan *plan) {
                           &plan->code);
 }
 
+std::string wave_source_of(const qpb_plan *plan) {
+    return plan->wave_qpw == 4 ? generate_row_kernel(plan->pl, nullptr)
+                               : generate_wave_kernel(plan->pl, plan->wave_wg, nullptr);
+}
+
 int compile_wave(qpb_plan *plan) {
     if (!plan->wave_ok) return fail(QPB_EINVAL, "plan is not eligible for the wave kernel");
-    return compile_kernel(plan->wave_kname,
-                          [plan] { return generate_wave_kernel(plan->pl, plan->wave_wg, nullptr); }, false,
-                          &plan->wave_code);
+    return compile_kernel(plan->wave_kname, [plan] { return wave_source_of(plan); }, false, &plan->wave_code);
 }
 
 int load_function(const std::string &kname, const std::shared_ptr<std::vector<char>> &code, hipFunction_t *fn) {
@@ -263,8 +266,17 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     plan->wave_max_batch = 4096;   // measured crossover vs the lane kernel
     if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
     if (plan->wave_ok) {
-        plan->wave_wg = qpb::wave_wg_for(plan->pl);
-        qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
+        // row form (four QPs per wavefront, all exchanges DPP) where the plan fits
+        // a 16-lane row; QPB_KERNEL_NOROW or QPB_ROW=0 keep one QP per wavefront
+        const char *er = getenv("QPB_ROW");
+        if (!(flags & QPB_KERNEL_NOROW) && !(er && atoi(er) == 0) && qpb::row_eligible(plan->pl)) {
+            plan->wave_qpw = 4;
+            plan->wave_wg = 64;
+            qpb::generate_row_kernel(plan->pl, &plan->wave_kname);
+        } else {
+            plan->wave_wg = qpb::wave_wg_for(plan->pl);
+            qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
+        }
     }
     *out = plan.release();
     return QPB_OK;
@@ -283,6 +295,7 @@ int qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info) {
     info->hash = pl.hash;
     info->wave_ok = plan->wave_ok ? 1 : 0;
     info->wave_max_batch = plan->kernel_pref == 1 ? 0 : plan->kernel_pref == 2 ? -1 : plan->wave_max_batch;
+    info->wave_qpw = plan->wave_qpw;
     return QPB_OK;
 }
 
@@ -306,7 +319,7 @@ long qpb_plan_source(const qpb_plan *plan, char *buf, long cap) {
 long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     if (!plan->wave_ok) return fail(QPB_EINVAL, "plan is not eligible for the wave kernel");
-    std::string s = qpb::generate_wave_kernel(plan->pl, plan->wave_wg, nullptr);
+    std::string s = qpb::wave_source_of(plan);
     if (buf && cap > 0) {
         long k = std::min<long>(cap - 1, (long)s.size());
         std::memcpy(buf, s.data(), k);
@@ -355,7 +368,7 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     a.maxit = st->maxit;
     void *params[] = {&a};
     const unsigned wg = (unsigned)(wave ? plan->wave_wg : plan->gen.wg);
-    const long per_block = wave ? wg / 64 : wg;    // QPs per workgroup
+    const long per_block = wave ? (wg / 64) * plan->wave_qpw : wg;    // QPs per workgroup
     const unsigned grid = (unsigned)((B + per_block - 1) / per_block);
     hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, wg, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("launch: ") + hipGetErrorString(e));

@@ -15,6 +15,7 @@ struct qpb_plan {
     std::shared_ptr<std::vector<char>> code;
     bool wave_ok = false;                       // wave kernel (one QP per wavefront)
     int wave_wg = 256;
+    int wave_qpw = 1;                           // QPs per wavefront: 1 wave form, 4 row form
     long wave_max_batch = 0;                    // auto: wave kernel for B <= this
     int kernel_pref = 0;                        // 0 auto, 1 lane only, 2 wave only
     std::string wave_kname;
@@ -35,5 +36,6 @@ struct CopySegs {
 int strided_copy(const CopySegs &t, void *stream);
 int compile_plan(qpb_plan *plan);
 int compile_wave(qpb_plan *plan);
+std::string wave_source_of(const qpb_plan *plan);   // wave or row form, as the plan chose
 int set_error(int code, const char *msg);
 }  // namespace qpb

@@ -70,6 +70,7 @@ struct qpb_args {
 #define ROWS_X ((NX + 15) / 16)
 #define ROWS_Z (ZC > 1 ? 4 : (NZ + 15) / 16)
 #define ROWS_Y ((NY1 + 15) / 16)
+#define ROWS_R (ROWS_Z > ROWS_X ? (ROWS_Z > ROWS_Y ? ROWS_Z : ROWS_Y) : (ROWS_X > ROWS_Y ? ROWS_X : ROWS_Y))
 
 static __device__ __forceinline__ double qpb_rcp(double v) {
     double r = __builtin_amdgcn_rcp(v);
@@ -94,6 +95,33 @@ template <int J> static __device__ __forceinline__ double qpb_xb(double v) {
     else return qpb_bc(v, J);
 }
 
+// acc + (v of dense lane J) * m as ONE v_fmac_f64 with a DPP row_newbcast
+// source (the compiler does not fold a 64-bit DPP move into a VOP2 FMA).  The
+// caller guarantees that v was not written by the two preceding VALU
+// instructions (the DPP read hazard): every use below reads a value produced
+// several dependent instructions earlier.
+template <int J> static __device__ __forceinline__ double qpb_fmac_xb(double acc, double v, double m) {
+    if constexpr (ND <= 16) {
+        asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+            : "+v"(acc) : "v"(v), "v"(m), "i"(J));
+        return acc;
+    } else {
+        return __builtin_fma(qpb_bc(v, J), m, acc);
+    }
+}
+
+// same, for a chain whose previous step wrote v (the triangular solves): the
+// two wait states the DPP read needs are inserted explicitly
+template <int J> static __device__ __forceinline__ double qpb_fmac_xb_dep(double acc, double v, double m) {
+    if constexpr (ND <= 16) {
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+            : "+v"(acc) : "v"(v), "v"(m), "i"(J));
+        return acc;
+    } else {
+        return __builtin_fma(qpb_bc(v, J), m, acc);
+    }
+}
+
 template <int CTRL> static __device__ __forceinline__ double qpb_dpp(double v) {
     return __builtin_amdgcn_update_dpp(0.0, v, CTRL, 0xf, 0xf, true);
 }
@@ -110,6 +138,24 @@ template <int R> static __device__ __forceinline__ double qpb_rsum(double v) {
     for (int k = 1; k < R; k++) r += qpb_bc(v, 16 * k);
     return r;
 }
+// K independent sums at once, stage-major so the K DPP chains overlap
+template <int R, int K> static __device__ __forceinline__ void qpb_rsum_n(double (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += qpb_dpp<0xB1>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += qpb_dpp<0x4E>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += qpb_dpp<0x141>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] += qpb_dpp<0x140>(v[k]);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        double r = qpb_bc(v[k], 0);
+#pragma unroll
+        for (int j = 1; j < R; j++) r += qpb_bc(v[k], 16 * j);
+        v[k] = r;
+    }
+}
 template <int R> static __device__ __forceinline__ double qpb_rmax(double v) {
     v = __builtin_fmax(v, qpb_dpp<0xB1>(v));
     v = __builtin_fmax(v, qpb_dpp<0x4E>(v));
@@ -119,6 +165,24 @@ template <int R> static __device__ __forceinline__ double qpb_rmax(double v) {
 #pragma unroll
     for (int k = 1; k < R; k++) r = __builtin_fmax(r, qpb_bc(v, 16 * k));
     return r;
+}
+
+template <int R, int K> static __device__ __forceinline__ void qpb_rmax_n(double (&v)[K]) {
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_fmax(v[k], qpb_dpp<0xB1>(v[k]));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_fmax(v[k], qpb_dpp<0x4E>(v[k]));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_fmax(v[k], qpb_dpp<0x141>(v[k]));
+#pragma unroll
+    for (int k = 0; k < K; k++) v[k] = __builtin_fmax(v[k], qpb_dpp<0x140>(v[k]));
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        double r = qpb_bc(v[k], 0);
+#pragma unroll
+        for (int j = 1; j < R; j++) r = __builtin_fmax(r, qpb_bc(v[k], 16 * j));
+        v[k] = r;
+    }
 }
 
 // LDS is shared by the lanes of one wave only: in-order per wave, so a compiler
@@ -141,7 +205,7 @@ static __device__ __forceinline__ double qpb_regularise(double d) {
 static __device__ __forceinline__ double qpb_rcp_reg(double d) {
     double r = __builtin_amdgcn_rcp(d);
     r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
-    asm volatile("" : "+v"(r));
+    asm("" : "+v"(r));     // opaque but not a scheduling barrier
     const double reg = d > 0.0 ? 1e7 : -1e7;
     return __builtin_fabs(d) <= 1e-14 ? reg : r;
 }
@@ -153,7 +217,9 @@ template <int J0, int J1, class F> static __device__ __forceinline__ void qpb_fo
     }
 }
 
-#if QPB_W_TIMING
+#if QPB_W_TIMING == 2      // per QP: start / end (100 MHz realtime, core cycles) + iterations
+#define QPB_TS(k) do { } while (0)
+#elif QPB_W_TIMING
 #define QPB_TS(k)                                                                      \
     do {                                                                               \
         if (ql == 0 && a.stats && (k) < 384) {                                         \
@@ -192,6 +258,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     const int dvar = dk == 0 ? di : (dk == 1 ? NX + di : NX + NY + di);   // x | y | z numbering
     constexpr double RDY = 1.0 / -1e-7;      // leaf y pivots: D = 0 regularised to -1e-7
 
+#if QPB_W_TIMING == 2
+    const double t_rt0 = (double)__builtin_amdgcn_s_memrealtime(), t_cy0 = (double)__builtin_readcyclecounter();
+#endif
     QPB_TS(0);
     // ---- stage this QP's inputs as dense matrices in LDS (tiled SoA -> dense):
     // every global load is issued before the first LDS store
@@ -316,25 +385,31 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     }
 
     double H[ND], Lt[ND], rDd = 0.0, w[ZC];
-    // factor with z diagonal kd (per z row): leaf z rows fold into the x block
-    // as G'diag(w)G, w = -1/regularise(kd); dense z rows take kd at their pivot
-    auto factor = [&](const double *kd) {
+    // The factor with z diagonal kd (per z row) in three pieces, so that its
+    // register-only part can be scheduled together with the residuals: leaf z
+    // rows fold into the x block as G'diag(w)G, w = -1/regularise(kd); dense z
+    // rows take kd at their pivot.
+    constexpr int VBW = NV;          // w | kd exchange, after the residual's x | z | y
+    auto factor_publish = [&](const double *kd) {
 #pragma unroll
         for (int t = 0; t < ZC; t++) {
             w[t] = -qpb_rcp_reg(kd[t]);
             if (isz[t]) {
-                Vb[lane + 64 * t] = w[t];
-                if constexpr (!QPB_XID) Vb[NZ + lane + 64 * t] = kd[t];   // dense z rows' diagonals
+                Vb[VBW + lane + 64 * t] = w[t];
+                if constexpr (!QPB_XID) Vb[VBW + NZ + lane + 64 * t] = kd[t];   // dense z rows' diagonals
             }
         }
-        qpb_wsync();
+    };
+    // after a wsync: H = H0 + G_L' W G_L, then the right-looking LDL' of the
+    // dense block in permutation order (registers and DPP only)
+    auto factor_ldl = [&]() {
 #pragma unroll
         for (int e = 0; e < ND; e++) H[e] = H0[e];
         if constexpr (QPB_W_GG) {      // small G: every (r, j) unrolled, products precomputed
             int e = 0;
 #pragma unroll
             for (int r = 0; r < NZ; r++) {
-                const double wr = Vb[r];
+                const double wr = Vb[VBW + r];
 #pragma unroll
                 for (int j = 0; j < NX; j++)
                     if (qpb_Gnz[r][j]) {
@@ -348,7 +423,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma nounroll
                 for (int u = qpb_goff[g]; u < qpb_goff[g + 1]; u++) {
                     const int r = __builtin_amdgcn_readfirstlane(qpb_grow[u]);
-                    const double t = dxm * Gd[dxi * NZ + r] * Vb[r];     // G(r, i) w_r
+                    const double t = dxm * Gd[dxi * NZ + r] * Vb[VBW + r];     // G(r, i) w_r
                     qpb_for<0, qpb_gncol[g]>([&](auto cc) {
                         constexpr int j = qpb_gcol[g][decltype(cc)::value];
                         H[qpb_xpos[j]] = __builtin_fma(t, Gd[j * NZ + r], H[qpb_xpos[j]]);
@@ -359,23 +434,37 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         double kdz[ND];
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            if constexpr (qpb_dkind[k] == 2) kdz[k] = Vb[NZ + qpb_didx[k]];
+            if constexpr (qpb_dkind[k] == 2) kdz[k] = Vb[VBW + NZ + qpb_didx[k]];
         });
-        qpb_wsync();
+        // The pivot recurrence is the critical path: D_{k+1} is formed from
+        // H'(k+1,k) and H'(k+1,k+1) (values before step k) with exactly the
+        // operations lane k+1's own update performs, so the trailing updates
+        // of step k are off the chain.
+        double dpiv = qpb_xb<0>(H[0]);
+        if constexpr (qpb_dkind[0] == 2) dpiv += kdz[0];
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            double dpiv = qpb_xb<k>(H[k]);
-            if constexpr (qpb_dkind[k] == 2) dpiv += kdz[k];
             const double rd = qpb_rcp_reg(dpiv);
+            if constexpr (k + 1 < ND) {
+                const double h = qpb_xb<k + 1>(H[k]), hkk = qpb_xb<k + 1>(H[k + 1]);
+                dpiv = __builtin_fma(h, h * -rd, hkk);
+                if constexpr (qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
+            }
             rDd = lane == k ? rd : rDd;
-            const double l = H[k] * rd;
+            // -L(d,k): kept negated so every update (and the solves) is a plain
+            // v_fmac_f64 whose broadcast operand folds into it as DPP row_newbcast
+            const double nl = H[k] * -rd;
             qpb_for<k + 1, ND>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                H[j] = __builtin_fma(-l, qpb_xb<j>(H[k]), H[j]);
+                H[j] = qpb_fmac_xb<j>(H[j], H[k], nl);
             });
-            H[k] = lane > k ? l : 0.0;        // L(d,k) below the diagonal, 0 elsewhere
+            H[k] = lane > k ? nl : 0.0;       // -L(d,k) below the diagonal, 0 elsewhere
         });
-        // transpose L through LDS: lane e gets column e (0 on and above the diagonal)
+    };
+    // transpose -L through LDS: lane e gets column e (0 on and above the
+    // diagonal); the first wsync also orders every earlier Vb read before the
+    // solve's stores
+    auto factor_transpose = [&]() {
         if (isd) {
 #pragma unroll
             for (int e = 0; e < ND; e++) Tx[lane * ND + e] = H[e];
@@ -388,7 +477,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 
     // solve K [dx; dy; dz] = [bx; byv; bz] with the current factor
     constexpr int VBX = 0, VBY = NX, VBZ = NX + NY, VBV = NX + NY + NZ, VBO = NX + NY + 2 * NZ;
+    int sstamp = 0;     // timing build: solve-internal stamps base (0 = off)
     auto solve = [&](double bx, double byv, const double *bz, double &dx, double &dy, double *dz) {
+        if (sstamp) QPB_TS(sstamp + 0);
         if constexpr (!QPB_XID) {
             if (lane < NX) Vb[VBX + lane] = bx;
             if (lane < NY) Vb[VBY + lane] = byv;
@@ -402,6 +493,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         if constexpr (QPB_XID)
             if (lane < NY) Vb[VBY + lane] = byv;
         qpb_wsync();
+        if (sstamp) QPB_TS(sstamp + 1);
         // this dense row's right-hand side after the leaves' forward elimination
         double ta[QPB_W_SPLIT];
 #pragma unroll
@@ -419,21 +511,24 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
         for (int k = 0; k < QPB_W_SPLIT; k++) t += ta[k];
         qpb_wsync();
+        if (sstamp) QPB_TS(sstamp + 2);
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            t = __builtin_fma(-H[k], qpb_xb<k>(t), t);
+            t = qpb_fmac_xb_dep<k>(t, t, H[k]);
         });
         t *= rDd;
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = ND - 1 - decltype(kc)::value;
-            t = __builtin_fma(-Lt[k], qpb_xb<k>(t), t);
+            t = qpb_fmac_xb_dep<k>(t, t, Lt[k]);
         });
+        if (sstamp) QPB_TS(sstamp + 3);
         if constexpr (QPB_XID) {
             if (lane < NX) Vb[VBO + lane] = t;
         } else if (isd) {
             Vb[VBO + dvar] = t;               // dense solution, by variable
         }
         qpb_wsync();
+        if (sstamp) QPB_TS(sstamp + 4);
         if constexpr (QPB_XID) dx = t;
         else dx = Vb[VBO + ix];
         double gza[ZC][QPB_W_SPLIT], gya[QPB_W_SPLIT];
@@ -464,20 +559,15 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         if constexpr (QPB_XID) dy = RDY * (byv - gy);
         else dy = yleaf ? RDY * (byv - gy) : Vb[VBO + NX + iy];
         qpb_wsync();
+        if (sstamp) QPB_TS(sstamp + 5);
     };
 
-    // lane sums / maxima over this lane's z slots (0 / neutral outside the range)
+    // lane sums over this lane's z slots (0 outside the range)
     auto zsum = [&](auto f) {
         double v = 0.0;
 #pragma unroll
         for (int t = 0; t < ZC; t++) v += isz[t] ? f(t) : 0.0;
         return qpb_rsum<ROWS_Z>(v);
-    };
-    auto zmax = [&](auto f, double neutral) {
-        double v = neutral;
-#pragma unroll
-        for (int t = 0; t < ZC; t++) v = __builtin_fmax(v, isz[t] ? f(t) : neutral);
-        return qpb_rmax<ROWS_Z>(v);
     };
 
     QPB_TS(1);
@@ -490,72 +580,92 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     for (int t = 0; t < ZC; t++) { s[t] = 1.0; z[t] = 1.0; }
     long it = -1;
     int flag = 3;
-    double fval = 0.0, st_rx = 0.0, st_ry = 0.0, st_rz = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;
+    // squared residual norms; the exit test compares them with tol^2 (sqrt is
+    // monotone), the norms themselves are taken once, for the statistics
+    double st_rx2 = 0.0, st_ry2 = 0.0, st_rz2 = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;
+    double fv = 0.0;    // this lane's objective term at the last residual evaluation
+    const double tol2 = a.tol > 0.0 ? a.tol * a.tol : -1.0;
     double sigma = 100.0;
     for (;;) {
-        double rx = 0.0, ry = 0.0, rz[ZC], rzi[ZC], kd[ZC], sz = 1.0, mu = 0.0;
-        bool pc = true;
-        if (it >= 0) {
-            if (it >= a.maxit) { flag = 2; break; }
-            QPB_TS(8 + 8 * it);
-            // residuals (Auxilary.c:745-786), objective (Auxilary.c:1133-1141)
-            if (lane < NX) Vb[lane] = x;
+        if (it >= 0 && it >= a.maxit) { flag = 2; break; }
+        QPB_TS(it >= 0 ? 8 + 8 * it : 2);
+        // updatekktmatrix (Auxilary.c:211-215): z diagonal -s/z.  The setup
+        // system has -I there, which is this with s = z = 1 (iteration -1).
+        double rx, ry, rz[ZC], rzi[ZC], kd[ZC], sz, mu = 0.0;
+#pragma unroll
+        for (int t = 0; t < ZC; t++) {
+            rzi[t] = qpb_rcp(z[t]);
+            kd[t] = isz[t] ? -s[t] * rzi[t] : -1.0;
+        }
+        // The factor does not depend on the residuals, so it is formed before
+        // the exit test (wasted on the last iteration): one LDS exchange serves
+        // both, and the LDL's latency-bound pivot chain is scheduled together
+        // with the residual products and reductions.
+        factor_publish(kd);
+        // residuals (Auxilary.c:745-786), objective (Auxilary.c:1133-1141)
+        if (lane < NX) Vb[lane] = x;
+#pragma unroll
+        for (int t = 0; t < ZC; t++)
+            if (isz[t]) Vb[NX + lane + 64 * t] = z[t];
+        if (lane < NY) Vb[NX + NZ + lane] = y;
+        qpb_wsync();
+        factor_ldl();
+        double tp = 0.0;
+        ry = by;
+        rx = -cx;
+#pragma unroll
+        for (int t = 0; t < ZC; t++) rz[t] = hz[t] - s[t];
+#pragma unroll
+        for (int j = 0; j < NX; j++) {
+            const double xj = Vb[j];
+            tp = __builtin_fma(-PR(j), xj, tp);
+#pragma unroll
+            for (int t = 0; t < ZC; t++) rz[t] = __builtin_fma(-GR(t, j), xj, rz[t]);
+            if constexpr (NY > 0) ry = __builtin_fma(-AR(j), xj, ry);
+        }
+        {
+            double ra[QPB_W_SPLIT];
+#pragma unroll
+            for (int k = 0; k < QPB_W_SPLIT; k++) ra[k] = k ? 0.0 : rx;
+#pragma unroll
+            for (int r = 0; r < NZ; r++)   // G(r, i): the dense-row slice when dense row i is x_i
+                ra[r % QPB_W_SPLIT] = __builtin_fma(-(QPB_XID ? GC(r) : Gd[ix * NZ + r]), Vb[NX + r], ra[r % QPB_W_SPLIT]);
+#pragma unroll
+            for (int l = 0; l < NY; l++)
+                ra[(NZ + l) % QPB_W_SPLIT] =
+                    __builtin_fma(-(QPB_XID ? AC(l) : Ad[ix * NY + l]), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
+            rx = ra[0];
+#pragma unroll
+            for (int k = 1; k < QPB_W_SPLIT; k++) rx += ra[k];
+        }
+        rx += tp;
+        {
+            double red[4] = {isx ? rx * rx : 0.0, isy ? ry * ry : 0.0, 0.0, 0.0};
 #pragma unroll
             for (int t = 0; t < ZC; t++)
-                if (isz[t]) Vb[NX + lane + 64 * t] = z[t];
-            if (lane < NY) Vb[NX + NZ + lane] = y;
-            qpb_wsync();
-            double tp = 0.0;
-            ry = by;
-            rx = -cx;
-#pragma unroll
-            for (int t = 0; t < ZC; t++) rz[t] = hz[t] - s[t];
-#pragma unroll
-            for (int j = 0; j < NX; j++) {
-                const double xj = Vb[j];
-                tp = __builtin_fma(-PR(j), xj, tp);
-#pragma unroll
-                for (int t = 0; t < ZC; t++) rz[t] = __builtin_fma(-GR(t, j), xj, rz[t]);
-                if constexpr (NY > 0) ry = __builtin_fma(-AR(j), xj, ry);
+                if (isz[t]) {
+                    red[2] = __builtin_fma(rz[t], rz[t], red[2]);
+                    red[3] = __builtin_fma(s[t], z[t], red[3]);
+                }
+            qpb_rsum_n<ROWS_R>(red);
+            sz = red[3];
+            if (it >= 0) {
+                fv = isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0;      // summed at exit
+                st_rx2 = red[0];
+                st_ry2 = NY > 0 ? red[1] : 0.0;
+                st_rz2 = red[2];
+                st_mu = sz * (1.0 / NZ);
             }
-            {
-                double ra[QPB_W_SPLIT];
-#pragma unroll
-                for (int k = 0; k < QPB_W_SPLIT; k++) ra[k] = k ? 0.0 : rx;
-#pragma unroll
-                for (int r = 0; r < NZ; r++)   // G(r, i): the dense-row slice when dense row i is x_i
-                    ra[r % QPB_W_SPLIT] = __builtin_fma(-(QPB_XID ? GC(r) : Gd[ix * NZ + r]), Vb[NX + r], ra[r % QPB_W_SPLIT]);
-#pragma unroll
-                for (int l = 0; l < NY; l++)
-                    ra[(NZ + l) % QPB_W_SPLIT] =
-                        __builtin_fma(-(QPB_XID ? AC(l) : Ad[ix * NY + l]), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
-                rx = ra[0];
-#pragma unroll
-                for (int k = 1; k < QPB_W_SPLIT; k++) rx += ra[k];
-            }
-            qpb_wsync();
-            rx += tp;
-            fval = qpb_rsum<ROWS_X>(isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0);
-            st_rx = __builtin_sqrt(qpb_rsum<ROWS_X>(isx ? rx * rx : 0.0));
-            st_ry = NY > 0 ? __builtin_sqrt(qpb_rsum<ROWS_Y>(isy ? ry * ry : 0.0)) : 0.0;
-            st_rz = __builtin_sqrt(zsum([&](int t) { return rz[t] * rz[t]; }));
-            sz = zsum([&](int t) { return s[t] * z[t]; });
-            st_mu = sz * (1.0 / NZ);
-            if (st_rx < a.tol && st_rz < a.tol && (NY == 0 || st_ry < a.tol) && st_mu < a.abstol) { flag = 0; break; }
-            QPB_TS(9 + 8 * it);
+        }
+        bool pc = true;
+        if (it >= 0) {
+            if (st_rx2 < tol2 && st_rz2 < tol2 && (NY == 0 || st_ry2 < tol2) && st_mu < a.abstol) { flag = 0; break; }
             mu = st_mu;
             pc = sigma > a.sigma_d;
-#pragma unroll
-            for (int t = 0; t < ZC; t++) {
-                rzi[t] = qpb_rcp(z[t]);
-                kd[t] = isz[t] ? -s[t] * rzi[t] : -1.0;   // updatekktmatrix (Auxilary.c:211-215)
-            }
-        } else {
-#pragma unroll
-            for (int t = 0; t < ZC; t++) { kd[t] = -1.0; rzi[t] = 1.0; rz[t] = 0.0; }   // KKT with -I
         }
-        factor(kd);
-        QPB_TS(it >= 0 ? 10 + 8 * it : 2);
+        QPB_TS(it >= 0 ? 9 + 8 * it : 5);
+        factor_transpose();
+        QPB_TS(it >= 0 ? 10 + 8 * it : 6);
         if (!pc) sigma = a.sigma_d;
         double cc[ZC];
 #pragma unroll
@@ -563,8 +673,15 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         double dx, dy, dz[ZC], dsl[ZC];
         auto step_length = [&]() {
             // alpha = min over d < 0 of v/(-d) == 1 / max(-d/v); 1 if none (Auxilary.c:359-393)
-            const double bp = zmax([&](int t) { return -dsl[t] * __builtin_amdgcn_rcp(s[t]); }, 0.0);
-            const double bd = zmax([&](int t) { return -dz[t] * rzi[t]; }, 0.0);
+            double bm[2] = {0.0, 0.0};
+#pragma unroll
+            for (int t = 0; t < ZC; t++)
+                if (isz[t]) {
+                    bm[0] = __builtin_fmax(bm[0], -dsl[t] * __builtin_amdgcn_rcp(s[t]));
+                    bm[1] = __builtin_fmax(bm[1], -dz[t] * rzi[t]);
+                }
+            qpb_rmax_n<ROWS_Z>(bm);
+            const double bp = bm[0], bd = bm[1];
             ap = bp > 1e-10 ? __builtin_amdgcn_rcp(bp) : 1.0;
             ad = bd > 1e-10 ? __builtin_amdgcn_rcp(bd) : 1.0;
         };
@@ -578,6 +695,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             for (int t = 0; t < ZC; t++)
                 bz[t] = pass == 2 ? hz[t] : (pass == 0 ? rz[t] + s[t] : __builtin_fma(-cc[t], rzi[t], rz[t] + s[t]));
             if (pass == 2) { bxv = -cx; byv = by; }
+            if (QPB_W_TIMING) sstamp = (it == 1 && pass == 0) ? 300 : 0;
             solve(bxv, byv, bz, dx, dy, dz);
             QPB_TS(it >= 0 ? (pass == 0 ? 11 : 13) + 8 * it : 3);
             if (pass == 2) {
@@ -595,8 +713,15 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                     zi[t] = hz[t] - gx;
                 }
                 qpb_wsync();
-                const double lo = -zmax([&](int t) { return -zi[t]; }, -1e300);
-                const double hi = zmax([&](int t) { return zi[t]; }, -1e300);
+                double lh[2] = {-1e300, -1e300};
+#pragma unroll
+                for (int t = 0; t < ZC; t++)
+                    if (isz[t]) {
+                        lh[0] = __builtin_fmax(lh[0], -zi[t]);
+                        lh[1] = __builtin_fmax(lh[1], zi[t]);
+                    }
+                qpb_rmax_n<ROWS_Z>(lh);
+                const double lo = -lh[0], hi = lh[1];
                 const double sh = -lo;
 #pragma unroll
                 for (int t = 0; t < ZC; t++) {
@@ -640,6 +765,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         it++;
     }
     QPB_TS(370);
+    const double fval = qpb_rsum<ROWS_X>(fv);
     // ---- outputs (tiled SoA)
     if (isx) a.x[tile * (NX * 64) + lane * 64 + ql] = x;
 #if NY > 0
@@ -657,8 +783,18 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         a.fval[q] = fval;
         if (a.stats && !QPB_W_TIMING) {
             double *o = a.stats + tile * 384 + ql;
-            o[0] = st_rx; o[64] = st_ry; o[128] = st_rz; o[192] = st_mu; o[256] = ap; o[320] = ad;
+            o[0] = __builtin_sqrt(st_rx2); o[64] = __builtin_sqrt(st_ry2); o[128] = __builtin_sqrt(st_rz2); o[192] = st_mu; o[256] = ap; o[320] = ad;
         }
     }
     QPB_TS(371);
+#if QPB_W_TIMING == 2
+    if (lane == 0 && a.stats) {
+        double *o = a.stats + tile * 384 + ql;
+        o[0] = t_rt0; o[64] = (double)__builtin_amdgcn_s_memrealtime();
+        o[128] = t_cy0; o[192] = (double)__builtin_readcyclecounter(); o[256] = (double)it;
+        const unsigned hwid = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_ID (wave, simd, cu, se)
+        const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));    // XCC_ID
+        o[320] = (double)hwid + 4294967296.0 * (double)(xcc & 0xf);
+    }
+#endif
 }

@@ -23,4 +23,8 @@ bool wave_eligible(const Plan &pl, std::string *why);
 int wave_wg_for(const Plan &pl);
 // Full hiprtc source; the kernel name is returned through name_out.
 std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out);
+// Row form (qpb_row.hip, one QP per 16-lane row, four per wavefront): plans
+// with every z / y row a leaf, the x block in natural order, n, p <= 16, m <= 32.
+bool row_eligible(const Plan &pl);
+std::string generate_row_kernel(const Plan &pl, std::string *name_out);
 }  // namespace qpb

@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=1024, help="QPs per GPU per step (configs[1]: 1024)")
     ap.add_argument("--large-batch", type=int, default=1 << 20,
                     help="QPs of the secondary large-batch leg (1-GPU runs; 0 = skip)")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave", "wave1", "auto1"])
     ap.add_argument("--no-mixed", dest="mixed", action="store_false",
                     help="skip the configs[2] leg (4 gait patterns x 1024 QPs)")
     ap.add_argument("--tol", type=float, default=1e-6)

@@ -51,7 +51,9 @@ typedef struct qpb_plan qpb_plan;
 #define QPB_P_UPPER  0x1   /* P pattern is the upper triangle (symmetric P)        */
 #define QPB_EXACT    0x10  /* bit-faithful arithmetic: IEEE division, no FMA       */
 #define QPB_KERNEL_LANE 0x100  /* always the lane kernel (one QP per lane)         */
-#define QPB_KERNEL_WAVE 0x200  /* always the wave kernel (one QP per wavefront)    */
+#define QPB_KERNEL_WAVE 0x200  /* always the wave kernel (wave or row form)         */
+#define QPB_KERNEL_NOROW 0x400 /* wave kernel in its one-QP-per-wavefront form even
+                                  where the row form (four QPs per wavefront) fits */
 
 /* error codes */
 #define QPB_OK        0
@@ -78,6 +80,7 @@ typedef struct qpb_plan_info {
     uint64_t hash;               /* pattern + permutation hash */
     int  wave_ok;                /* plan can use the wave-cooperative kernel */
     long wave_max_batch;         /* qpb_solve uses it for B <= this (-1: always) */
+    int  wave_qpw;               /* QPs per wavefront of that kernel: 1 wave form, 4 row form */
 } qpb_plan_info;
 
 void qpb_default_settings(qpb_settings *st);

@@ -47,10 +47,12 @@ def main():
             os.environ.pop("QPB_WG", None); os.environ.pop("QPB_LDS", None)
             plans_[v] = Plan.from_dense(n, m, p, d0["P"][0], d0["A"][0], d0["G"][0], exact=True)
         elif v.startswith("wave"):
-            # "wave" or "wave:KNOB=V,KNOB=V" (QPB_W_* knobs of qpb_wave.hip)
+            # "wave[1]" or "wave[1]:KNOB=V,KNOB=V" (QPB_W_* knobs of qpb_wave.hip, QPB_R_*
+            # of qpb_row.hip); "wave" takes the row form where it fits, "wave1" never
+            kind = v.split(":", 1)[0]
             opts = v.split(":", 1)[1].replace(",", " ") if ":" in v else ""
-            os.environ["QPB_WAVE_OPTS"] = " ".join("QPB_W_" + o for o in opts.split())
-            plans_[v] = Plan.from_dense(n, m, p, d0["P"][0], d0["A"][0], d0["G"][0], kernel="wave")
+            os.environ["QPB_WAVE_OPTS"] = " ".join(f"QPB_W_{o} QPB_R_{o}" for o in opts.split())
+            plans_[v] = Plan.from_dense(n, m, p, d0["P"][0], d0["A"][0], d0["G"][0], kernel=kind)
             plans_[v].compile()
             os.environ.pop("QPB_WAVE_OPTS", None)
         else:
@@ -81,18 +83,40 @@ def main():
             outs[v] = out
     for v in a.variants:
         pl = plans_[v]
+        if "TIMING=2" in v:      # per QP: start / end realtime (100 MHz) and cycles, iterations, XCC
+            st = outs[v]["stats"].cpu().numpy().reshape(-1, 6, 64)[: (a.batch + 63) // 64]
+            f = lambda k: st[:, k, :].reshape(-1)[: a.batch]
+            rt0, rt1, cy0, cy1, itn, hw = (f(k) for k in range(6))
+            dur_us = (rt1 - rt0) / 100.0
+            cyc = cy1 - cy0
+            xcc = (hw // 4294967296).astype(int)
+            span = (rt1.max() - rt0.min()) / 100.0
+            summ = dict(variant=v, span_us=span, start_spread_us=(rt0.max() - rt0.min()) / 100.0,
+                        dur_us_median=float(np.median(dur_us)), dur_us_max=float(dur_us.max()),
+                        clock_ghz=float(np.median(cyc / np.maximum(dur_us, 1e-3)) / 1e3),
+                        cycles_per_iter=float(np.median(cyc / np.maximum(itn + 1, 1))),
+                        iters_hist={int(k): int((itn == k).sum()) for k in np.unique(itn)},
+                        dur_by_iters={int(k): float(np.median(dur_us[itn == k])) for k in np.unique(itn)},
+                        end_by_xcc={int(k): float((rt1[xcc == k].max() - rt0.min()) / 100.0) for k in np.unique(xcc)},
+                        start_by_xcc={int(k): float((rt0[xcc == k].min() - rt0.min()) / 100.0) for k in np.unique(xcc)})
+            print(json.dumps(summ))
+            continue
         if "TIMING=1" in v:      # phase timestamps of QP 0 of tile 0 (s_memtime cycles)
             t = outs[v]["stats"][:384].cpu().numpy()
             base = t[0]
-            ph = {"stage": t[1] - t[0], "init_factor": t[2] - t[1], "init_solve": t[3] - t[2],
+            ph = {"stage": t[1] - t[0], "init_factor": t[6] - t[1], "init_solve": t[3] - t[6],
                   "init_sz": t[4] - t[3]}
             its = []
             for it in range(int(outs[v]["iters"][0].item())):
                 r = t[8 + 8 * it: 16 + 8 * it]
-                its.append(dict(resid=r[1] - r[0], factor=r[2] - r[1], pred_solve=r[3] - r[2], pred_step=r[4] - r[3],
+                its.append(dict(resid_ldl=r[1] - r[0], transpose=r[2] - r[1], pred_solve=r[3] - r[2], pred_step=r[4] - r[3],
                                 corr_solve=r[5] - r[4], corr_step=r[6] - r[5],
                                 update=(t[16 + 8 * it] if t[16 + 8 * it] > 0 else t[370]) - r[6]))
             ph["out"] = t[371] - t[370]
+            if t[305] > 0:
+                ss = t[300:306]
+                ph["solve_inner"] = dict(publish=ss[1] - ss[0], leaf_fwd=ss[2] - ss[1], dense=ss[3] - ss[2],
+                                         publish_dx=ss[4] - ss[3], leaf_back=ss[5] - ss[4])
             ph["total"] = t[371] - base
             print(json.dumps(dict(variant=v, phases=ph, iterations=its)))
             continue

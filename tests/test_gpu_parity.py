@@ -64,7 +64,8 @@ def test_exact_kernel_bit_identical_to_reference(name):
 @pytest.mark.parametrize("name", DENSE_CASES)
 @pytest.mark.parametrize("exact,own_order,kernel", [(False, False, "lane"), (False, True, "lane"),
                                                     (True, True, "lane"), (False, True, "wave"),
-                                                    (False, False, "wave")])
+                                                    (False, False, "wave"), (False, True, "wave1"),
+                                                    (False, False, "wave1")])
 def test_kernel_within_tolerance_of_reference(name, exact, own_order, kernel):
     """Fast kernel and/or own ordering vs the reference: |.|_inf <= 1e-6 * max(1, |ref|).
     The wave kernel always eliminates in its own order [z | y | x].
@@ -77,7 +78,7 @@ def test_kernel_within_tolerance_of_reference(name, exact, own_order, kernel):
     truncated = int(g["maxit"]) < 100
     if own_order and (name == "edge_zero_g_row" or truncated):
         pytest.skip("depends on the reference's own KKT order")
-    if kernel == "wave" and name == "edge_zero_g_row":
+    if kernel.startswith("wave") and name == "edge_zero_g_row":
         pytest.skip("the wave kernel needs every G row non-empty")
     _, r = _solve(g, perm=None if own_order else g["perm"][0], exact=exact, p_upper=True, kernel=kernel)
     n, m, p, P, A, G = _dense(g)
@@ -140,11 +141,13 @@ def _oracle_perm(plan):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "c1_noeq", "mixed_stance4", "mixed_trot_blfr",
                                   "mixed_trot_brfl", "mixed_crawl_blflfr", "c1_maxit3", "c30_tol1e-6", "c30_tol1e-2"])
-def test_wave_kernel_matches_oracle_in_its_order(name, oracle):
-    """Wave kernel vs the oracle run with the wave kernel's elimination order:
-    same factorisation, so agreement is at rounding level (1e-9 relative)."""
+@pytest.mark.parametrize("kernel", ["wave", "wave1"])
+def test_wave_kernel_matches_oracle_in_its_order(name, kernel, oracle):
+    """Wave kernel (row form where the pattern fits, and one QP per wavefront) vs
+    the oracle run with the kernel's elimination order: same factorisation, so
+    agreement is at rounding level (1e-9 relative)."""
     g = golden(name)
-    plan, r = _solve(g, perm=None, exact=False, p_upper=True, kernel="wave")
+    plan, r = _solve(g, perm=None, exact=False, p_upper=True, kernel=kernel)
     n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
     tol = float(g["tol"])
     for q in range(0, g["x"].shape[0], 3):
@@ -166,8 +169,8 @@ def test_wave_kernel_matches_oracle_in_its_order(name, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["lane", "wave"])
-@pytest.mark.parametrize("B", [1, 63, 65, 1000])
+@pytest.mark.parametrize("kernel", ["lane", "wave", "wave1"])
+@pytest.mark.parametrize("B", [1, 2, 3, 5, 63, 65, 1000])
 def test_ragged_batches(B, kernel, oracle):
     from apf_quadruped_amd import workloads as W
     from apf_quadruped_amd.batch import Plan
@@ -183,7 +186,7 @@ def test_ragged_batches(B, kernel, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["lane", "wave"])
+@pytest.mark.parametrize("kernel", ["lane", "wave", "wave1"])
 def test_large_batch_properties(kernel, oracle):
     """B = 65536 (config 5's global batch on one GPU): all optimal, KKT residuals
     small, deterministic, each QP independent of its neighbours."""
@@ -234,7 +237,7 @@ def test_argmin_device_reduction():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["lane", "wave"])
+@pytest.mark.parametrize("kernel", ["lane", "wave", "wave1"])
 def test_solve_best_fused_argmin(kernel):
     """qpb_solve_best == qpb_solve + qpb_argmin, repeatedly, for ragged batch sizes
     (1 and 1024 take the single-block argmin, 3000 too; 100003 the two-stage one)."""

@@ -82,3 +82,26 @@ def test_kernel_compiles_for_gfx950(exact, tmp_path, monkeypatch):
     src = plan.source()
     assert "__global__" in src and ("[exact]" in src) == exact
     plan.compile()                     # hiprtc --offload-arch=gfx950 (or cache hit)
+
+
+@pytest.mark.parametrize("name,kernel,qpw", [("c1", "wave", 4), ("c1", "wave1", 1), ("c1", "auto", 4),
+                                             ("c1", "auto1", 1), ("stance4", "wave", 4),
+                                             ("crawl_blflfr", "wave", 4), ("trot_blfr", "wave", 1)])
+def test_wave_kernel_form(name, kernel, qpw):
+    """The wave kernel takes its row form (four QPs per wavefront) exactly for
+    patterns whose z / y rows are all leaves with the x block in natural order
+    and n, p <= 16, m <= 32; "wave1" / "auto1" keep one QP per wavefront."""
+    from apf_quadruped_amd import plans
+    d = plans.standard_qp(name)
+    plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel=kernel)
+    assert plan.info.wave_ok == 1 and plan.info.wave_qpw == qpw
+    src = plan.wave_source()
+    assert ("[row-cooperative" in src) == (qpw == 4)
+    plan.compile()                     # hiprtc for gfx950 (or cache hit), no GPU needed
+
+
+def test_controller_shape_keeps_one_qp_per_wave():
+    from apf_quadruped_amd import plans, workloads as W
+    d = W.controller_qp(plans.SEED + 30, [0])
+    plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel="wave")
+    assert plan.info.wave_ok == 1 and plan.info.wave_qpw == 1
