@@ -26,7 +26,8 @@ class QpbPlanInfo(C.Structure):
                 ("nnzK", C.c_long), ("lnz", C.c_long),
                 ("fac_updates", C.c_long), ("fac_divs", C.c_long),
                 ("ordering", C.c_int), ("exact", C.c_int), ("hash", C.c_uint64),
-                ("wave_ok", C.c_int), ("wave_max_batch", C.c_long), ("wave_qpw", C.c_int)]
+                ("wave_ok", C.c_int), ("wave_max_batch", C.c_long), ("wave_qpw", C.c_int),
+                ("tree_ok", C.c_int), ("large_kernel", C.c_int)]
 
 
 _lib = None
@@ -61,6 +62,8 @@ def lib() -> C.CDLL:
     L.qpb_plan_source.argtypes = [vp, C.c_char_p, C.c_long]
     L.qpb_plan_wave_source.restype = C.c_long
     L.qpb_plan_wave_source.argtypes = [vp, C.c_char_p, C.c_long]
+    L.qpb_plan_tree_source.restype = C.c_long
+    L.qpb_plan_tree_source.argtypes = [vp, C.c_char_p, C.c_long]
     L.qpb_plan_compile.argtypes = [vp]
     L.qpb_solve.restype = C.c_int
     L.qpb_solve.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp]

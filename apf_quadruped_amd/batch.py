@@ -21,11 +21,12 @@ from . import _lib
 from ._lib import QpbPlanInfo, QpbSettings, check
 
 QPB_P_FULL, QPB_P_UPPER, QPB_EXACT = 0x0, 0x1, 0x10
-QPB_KERNEL_LANE, QPB_KERNEL_WAVE, QPB_KERNEL_NOROW = 0x100, 0x200, 0x400
+QPB_KERNEL_LANE, QPB_KERNEL_WAVE, QPB_KERNEL_NOROW, QPB_KERNEL_TREE = 0x100, 0x200, 0x400, 0x800
 # "wave" = the wave kernel in the form the plan picks (row form: four QPs per
 # wavefront, where it fits); "wave1" = one QP per wavefront regardless
 KERNEL_FLAGS = {"auto": 0, "lane": QPB_KERNEL_LANE, "wave": QPB_KERNEL_WAVE,
-                "wave1": QPB_KERNEL_WAVE | QPB_KERNEL_NOROW, "auto1": QPB_KERNEL_NOROW}
+                "wave1": QPB_KERNEL_WAVE | QPB_KERNEL_NOROW, "auto1": QPB_KERNEL_NOROW,
+                "tree": QPB_KERNEL_TREE}
 QP_OPTIMAL, QP_KKTFAIL, QP_MAXIT, QP_FATAL = 0, 1, 2, 3
 
 
@@ -121,7 +122,8 @@ class Plan:
         """Plan for the non-zero pattern of one dense QP (P [n,n], A [p,n], G [m,n]).
         kernel: "auto" (wave kernel for small batches when eligible), "lane", "wave"
         (its row form -- four QPs per wavefront -- where the pattern fits a 16-lane
-        row), "wave1" / "auto1" (as "wave" / "auto" but one QP per wavefront)."""
+        row), "wave1" / "auto1" (as "wave" / "auto" but one QP per wavefront),
+        "tree" (one QP per workgroup, level-scheduled sparse LDL'; any pattern)."""
         Pjc, Pir = dense_pattern(P, upper=p_upper)
         Ajc, Air = dense_pattern(A) if p else (None, None)
         Gjc, Gir = dense_pattern(G)
@@ -136,12 +138,12 @@ class Plan:
         return buf.value.decode()
 
     def kernel_for(self, B: int) -> str:
-        """Which kernel qpb_solve runs for a batch of B ("wave" or "lane"; the wave
-        kernel's form is info.wave_qpw: 4 QPs per wavefront = row form)."""
+        """Which kernel qpb_solve runs for a batch of B ("wave", "lane" or "tree";
+        the wave kernel's form is info.wave_qpw: 4 QPs per wavefront = row form)."""
         i = self.info
         if i.wave_ok and (i.wave_max_batch < 0 or B <= i.wave_max_batch):
             return "wave"
-        return "lane"
+        return {1: "lane", 2: "wave", 3: "tree"}[i.large_kernel]
 
     def oracle_perm(self, B: int) -> np.ndarray:
         """The KKT permutation the kernels factor with (both kernels follow the
@@ -154,6 +156,14 @@ class Plan:
         check(0 if size >= 0 else int(size), "qpb_plan_wave_source")
         buf = C.create_string_buffer(size + 1)
         L.qpb_plan_wave_source(self._h, buf, size + 1)
+        return buf.value.decode()
+
+    def tree_source(self) -> str:
+        L = _lib.lib()
+        size = L.qpb_plan_tree_source(self._h, None, 0)
+        check(0 if size >= 0 else int(size), "qpb_plan_tree_source")
+        buf = C.create_string_buffer(size + 1)
+        L.qpb_plan_tree_source(self._h, buf, size + 1)
         return buf.value.decode()
 
     def compile(self) -> None:
@@ -282,7 +292,8 @@ class Plan:
 
     def kernel_name(self, B: int) -> str:
         """Name of the kernel qpb_solve launches for a batch of B."""
-        src = self.wave_source() if self.kernel_for(B) == "wave" else self.source()
+        k = self.kernel_for(B)
+        src = self.wave_source() if k == "wave" else self.tree_source() if k == "tree" else self.source()
         for line in src.splitlines():
             if line.startswith("#define QPB_KERNEL_NAME "):
                 return line.split()[-1]

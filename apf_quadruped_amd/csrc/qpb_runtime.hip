@@ -22,6 +22,7 @@
 #include "qpb_codegen.hpp"
 #include "qpb_plan.hpp"
 #include "qpb_runtime.hpp"
+#include "qpb_tree.hpp"
 #include "qpb_wave.hpp"
 
 namespace {
@@ -194,6 +195,12 @@ int compile_wave(qpb_plan *plan) {
     return compile_kernel(plan->wave_kname, [plan] { return wave_source_of(plan); }, false, &plan->wave_code);
 }
 
+int compile_tree(qpb_plan *plan) {
+    if (!plan->tree_ok) return fail(QPB_EINVAL, "plan is not eligible for the tree kernel");
+    return compile_kernel(plan->tree_kname, [plan] { return generate_tree_kernel(plan->pl, plan->tree_wg, nullptr); },
+                          false, &plan->tree_code);
+}
+
 int load_function(const std::string &kname, const std::shared_ptr<std::vector<char>> &code, hipFunction_t *fn) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return fail(QPB_EHIP, "hipGetDevice failed (no GPU?)");
@@ -260,9 +267,21 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     // from the reference's), for plans whose KKT has the z/y-leaf structure
     std::string why;
     plan->wave_ok = !plan->gen.exact && qpb::wave_eligible(plan->pl, &why);
-    plan->kernel_pref = (flags & QPB_KERNEL_WAVE) ? 2 : (flags & QPB_KERNEL_LANE) ? 1 : 0;
+    plan->kernel_pref = (flags & QPB_KERNEL_TREE) ? 3 : (flags & QPB_KERNEL_WAVE) ? 2 : (flags & QPB_KERNEL_LANE) ? 1 : 0;
     if (plan->kernel_pref == 2 && !plan->wave_ok)
         return fail(QPB_EINVAL, "QPB_KERNEL_WAVE: " + (plan->gen.exact ? std::string("exact plans use the lane kernel") : why));
+    // tree kernel (one QP per workgroup, level-scheduled sparse LDL'): any
+    // fast-mode plan whose per-QP state fits the LDS; auto dispatch uses it for
+    // KKT systems too large for one QP per lane (N > 64)
+    std::string why_tree;
+    plan->tree_ok = !plan->gen.exact && qpb::tree_eligible(plan->pl, &why_tree);
+    plan->large_tree = plan->tree_ok && plan->pl.N > 64;
+    if (plan->kernel_pref == 3 && !plan->tree_ok)
+        return fail(QPB_EINVAL, "QPB_KERNEL_TREE: " + (plan->gen.exact ? std::string("exact plans use the lane kernel") : why_tree));
+    if (plan->tree_ok) {
+        plan->tree_wg = qpb::tree_wg_for(plan->pl);
+        qpb::generate_tree_kernel(plan->pl, plan->tree_wg, &plan->tree_kname);
+    }
     plan->wave_max_batch = 4096;   // measured crossover vs the lane kernel
     if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
     if (plan->wave_ok) {
@@ -294,8 +313,11 @@ int qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info) {
     info->ordering = pl.ordering_kind; info->exact = plan->gen.exact ? 1 : 0;
     info->hash = pl.hash;
     info->wave_ok = plan->wave_ok ? 1 : 0;
-    info->wave_max_batch = plan->kernel_pref == 1 ? 0 : plan->kernel_pref == 2 ? -1 : plan->wave_max_batch;
+    info->wave_max_batch = (plan->kernel_pref == 1 || plan->kernel_pref == 3) ? 0 : plan->kernel_pref == 2 ? -1 : plan->wave_max_batch;
     info->wave_qpw = plan->wave_qpw;
+    info->tree_ok = plan->tree_ok ? 1 : 0;
+    info->large_kernel = plan->kernel_pref == 3 ? 3 : plan->kernel_pref == 2 ? 2 : plan->kernel_pref == 1 ? 1
+                       : plan->large_tree ? 3 : 1;
     return QPB_OK;
 }
 
@@ -308,6 +330,18 @@ int qpb_plan_get_perm(const qpb_plan *plan, long *perm) {
 long qpb_plan_source(const qpb_plan *plan, char *buf, long cap) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     std::string s = qpb::generate_kernel(plan->pl, plan->gen);
+    if (buf && cap > 0) {
+        long k = std::min<long>(cap - 1, (long)s.size());
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (long)s.size();
+}
+
+long qpb_plan_tree_source(const qpb_plan *plan, char *buf, long cap) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    if (!plan->tree_ok) return fail(QPB_EINVAL, "plan is not eligible for the tree kernel");
+    std::string s = qpb::generate_tree_kernel(plan->pl, plan->tree_wg, nullptr);
     if (buf && cap > 0) {
         long k = std::min<long>(cap - 1, (long)s.size());
         std::memcpy(buf, s.data(), k);
@@ -330,8 +364,11 @@ long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap) {
 
 int qpb_plan_compile(qpb_plan *plan) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
-    int rc = plan->kernel_pref == 2 ? QPB_OK : qpb::compile_plan(plan);
-    if (!rc && plan->wave_ok && plan->kernel_pref != 1) rc = qpb::compile_wave(plan);
+    const int k = plan->kernel_pref;
+    int rc = QPB_OK;
+    if (k == 1 || (k == 0 && !plan->large_tree)) rc = qpb::compile_plan(plan);
+    if (!rc && plan->wave_ok && (k == 0 || k == 2)) rc = qpb::compile_wave(plan);
+    if (!rc && plan->tree_ok && (k == 3 || (k == 0 && plan->large_tree))) rc = qpb::compile_tree(plan);
     return rc;
 }
 
@@ -348,10 +385,14 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     if (pl.p > 0 && (!A || !b || !y)) return fail(QPB_EINVAL, "p > 0 needs A, b and y");
     // kernel choice: the wave kernel (one QP per wavefront) has the lower latency
     // and wins while the batch does not fill the GPU with lane-kernel waves
+    // beyond it: the lane kernel (one QP per lane) for small KKT systems, the tree
+    // kernel (one QP per workgroup) for large ones
     const bool wave = plan->wave_ok && (plan->kernel_pref == 2 || (plan->kernel_pref == 0 && B <= plan->wave_max_batch));
+    const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
     hipFunction_t fn;
-    int rc = wave ? qpb::compile_wave(plan) : qpb::compile_plan(plan);
+    int rc = wave ? qpb::compile_wave(plan) : tree ? qpb::compile_tree(plan) : qpb::compile_plan(plan);
     if (!rc) rc = wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
+                : tree ? qpb::load_function(plan->tree_kname, plan->tree_code, &fn)
                        : qpb::load_function(plan->kname, plan->code, &fn);
     if (rc) return rc;
     qpb_settings def;
@@ -367,8 +408,8 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     a.sigma_d = st->sigma_d;
     a.maxit = st->maxit;
     void *params[] = {&a};
-    const unsigned wg = (unsigned)(wave ? plan->wave_wg : plan->gen.wg);
-    const long per_block = wave ? (wg / 64) * plan->wave_qpw : wg;    // QPs per workgroup
+    const unsigned wg = (unsigned)(wave ? plan->wave_wg : tree ? plan->tree_wg : plan->gen.wg);
+    const long per_block = wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup
     const unsigned grid = (unsigned)((B + per_block - 1) / per_block);
     hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, wg, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("launch: ") + hipGetErrorString(e));

@@ -20,6 +20,11 @@ struct qpb_plan {
     int kernel_pref = 0;                        // 0 auto, 1 lane only, 2 wave only
     std::string wave_kname;
     std::shared_ptr<std::vector<char>> wave_code;
+    bool tree_ok = false;                       // tree kernel (one QP per workgroup, any pattern)
+    bool large_tree = false;                    // auto: tree (not lane) kernel beyond the wave kernel's range
+    int tree_wg = 256;
+    std::string tree_kname;
+    std::shared_ptr<std::vector<char>> tree_code;
 };
 
 namespace qpb {
@@ -36,6 +41,7 @@ struct CopySegs {
 int strided_copy(const CopySegs &t, void *stream);
 int compile_plan(qpb_plan *plan);
 int compile_wave(qpb_plan *plan);
+int compile_tree(qpb_plan *plan);
 std::string wave_source_of(const qpb_plan *plan);   // wave or row form, as the plan chose
 int set_error(int code, const char *msg);
 }  // namespace qpb

@@ -1,0 +1,290 @@
+// qpb_tree.cpp -- plan -> source of the tree kernel (qpb_tree.hip).
+//
+// The tree kernel solves one QP per workgroup for ANY plan (no leaf/dense-block
+// structure assumed, e.g. the MPC-horizon QP of BASELINE configs[3], N = 380):
+// every sparse operation of the IPM is a "gather program" -- a list of tasks,
+// each task one output value accumulated over a list of terms, grouped into the
+// levels of a dependency order.  Tasks of one level are independent; a level is
+// split into steps of at most QPB_WG lanes with 2^g lanes per task (the terms of
+// a task are dealt round-robin to its lanes and summed with a lane butterfly),
+// and a workgroup barrier closes each level.  This file turns the plan's KKT,
+// permutation and elimination tree into five such programs:
+//
+//   fac  left-looking LDL' of P K P' over the elimination-tree levels
+//        (level = height above the leaves): task (i, j) of column j computes
+//        K(i,j) - sum_k LD(i,k) LD(j,k) / D(k) over the k with L(j,k), L(i,k) != 0;
+//        the factor is stored unscaled, LD = L D, next to 1/D (reference:
+//        LDL_numeric, ldl.c:253-326, with its pivot regularisation ldl.c:273-274,
+//        319-320; same factor, different summation order)
+//   fwd  w = D^-1 L^-1 b, one task per row over the same levels (LDL_lsolve +
+//        LDL_dsolve, ldl.c:495-532)
+//   bwd  x = w - D^-1 LD' x, levels in reverse (LDL_ltsolve, ldl.c:539-557)
+//   mv   the residual products [P A' G'; A; G] [x; y; z] (computeresiduals,
+//        Auxilary.c:745-786), one task per KKT row
+//   obj  P x for the objective (obj_value, Auxilary.c:1133-1141)
+// plus the KKT assembly tables (Auxilary.c:71-181 and updatekktmatrix
+// Auxilary.c:205-233, including its "last slot of the z column" rule).
+#include "qpb_tree.hpp"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <numeric>
+#include <sstream>
+
+namespace qpb {
+
+namespace {
+const char *kTreeTemplate =
+#include "qpb_tree_src.inc"
+    ;
+
+constexpr int FB = 21;                       // descriptor field width (bits)
+constexpr long FMAX = (1L << FB) - 1;
+
+uint64_t pk(uint64_t a, uint64_t b, uint64_t c = 0) { return a | (b << FB) | (c << (2 * FB)); }
+
+struct Task {
+    int32_t out;
+    std::vector<uint64_t> con;
+};
+
+struct Prog {
+    std::vector<int32_t> steps;   // 4 per step: desc offset, task offset, ntask << 4 | log2 G, R | barrier << 16
+    std::vector<int32_t> hdr;     // one output code per task
+    std::vector<uint64_t> desc;   // [R][ntask * G] per step
+    long nsteps() const { return (long)steps.size() / 4; }
+};
+
+// One level's tasks -> steps.  Tasks are sorted by term count; the lanes-per-task
+// exponent g minimises a rough latency model: per step, one round per term a lane
+// sums, log2 G butterfly stages and a fixed step cost.
+void pack_level(std::vector<Task> &tasks, int wg, uint64_t dummy, Prog &P) {
+    if (tasks.empty()) return;
+    std::stable_sort(tasks.begin(), tasks.end(),
+                     [](const Task &a, const Task &b) { return a.con.size() > b.con.size(); });
+    int best_g = 0;
+    double best_cost = 1e300;
+    for (int g = 0; (1 << g) <= std::min(64, wg); g++) {
+        const long G = 1L << g, per = wg >> g;
+        double cost = 0;
+        for (size_t s = 0; s < tasks.size(); s += per) {
+            const long R = ((long)tasks[s].con.size() + G - 1) / G;
+            cost += 4.0 * R + 3.0 * g + 8.0;
+        }
+        if (cost < best_cost - 1e-9) { best_cost = cost; best_g = g; }
+    }
+    const int g = best_g;
+    const long G = 1L << g, per = wg >> g;
+    for (size_t s = 0; s < tasks.size(); s += per) {
+        const size_t e = std::min(tasks.size(), s + (size_t)per);
+        const long nt = (long)(e - s), act = nt * G;
+        const long R = ((long)tasks[s].con.size() + G - 1) / G;
+        const long doff = (long)P.desc.size(), toff = (long)P.hdr.size();
+        P.desc.resize(P.desc.size() + (size_t)(R * act), dummy);
+        for (size_t t = s; t < e; t++) {
+            P.hdr.push_back(tasks[t].out);
+            const long lt = (long)(t - s);
+            for (size_t ci = 0; ci < tasks[t].con.size(); ci++) {
+                const long r = (long)ci / G, sub = (long)ci % G;
+                P.desc[doff + r * act + lt * G + sub] = tasks[t].con[ci];
+            }
+        }
+        const bool last = e == tasks.size();
+        P.steps.insert(P.steps.end(), {(int32_t)doff, (int32_t)toff, (int32_t)((nt << 4) | g),
+                                       (int32_t)(R | (last ? 1 << 16 : 0))});
+    }
+}
+
+template <class T, class F>
+void table(std::ostringstream &o, const char *type, const char *name, long cnt, F f) {
+    o << "__constant__ " << type << " " << name << "[" << (cnt > 0 ? cnt : 1) << "] = {";
+    if (cnt <= 0) o << "0";
+    for (long k = 0; k < cnt; k++) {
+        o << (k ? "," : "") << (T)f(k);
+        if (k % 16 == 15) o << "\n";
+    }
+    o << "};\n";
+}
+
+void emit_prog(std::ostringstream &o, const char *name, const Prog &P) {
+    o << "#define QPB_" << name << "_NSTEPS " << P.nsteps() << "\n";
+    std::string s = std::string("qpb_") + name;
+    table<long>(o, "int", (s + "_steps").c_str(), (long)P.steps.size(), [&](long k) { return P.steps[k]; });
+    table<long>(o, "int", (s + "_hdr").c_str(), (long)P.hdr.size(), [&](long k) { return P.hdr[k]; });
+    o << "__constant__ unsigned long long " << s << "_desc[" << std::max<size_t>(P.desc.size(), 1) << "] = {";
+    if (P.desc.empty()) o << "0";
+    for (size_t k = 0; k < P.desc.size(); k++) {
+        o << (k ? "," : "") << P.desc[k] << "ull";
+        if (k % 12 == 11) o << "\n";
+    }
+    o << "};\n";
+}
+
+long lds_doubles(const Plan &pl) {
+    const long n = pl.n, m = pl.m, p = pl.p, N = pl.N;
+    const long npag = pl.Pin.nnz() + (p ? pl.A.nnz() : 0) + pl.G.nnz();
+    // qpb_tree.hip LDS layout: PAG+1, LD+1, rD, V, S, R, W, C, H, B, DS, LAM, DZ, DSL, XP, RED
+    return (npag + 1) + (pl.lnz + 1) + 4 * N + m + n + m + std::max(p, 1L) + 4 * m + n + 64;
+}
+
+// position of row i in column k of L (Li ascends within a column), -1 if absent
+long lpos(const Plan &pl, long i, long k) {
+    auto b = pl.Li.begin() + pl.Lp[k], e = pl.Li.begin() + pl.Lp[k + 1];
+    auto it = std::lower_bound(b, e, i);
+    return (it != e && *it == i) ? (long)(it - pl.Li.begin()) : -1;
+}
+}  // namespace
+
+int tree_wg_for(const Plan &pl) {
+    if (const char *e = getenv("QPB_TREE_WG")) {
+        const int w = atoi(e);
+        if (w == 64 || w == 128 || w == 256 || w == 512) return w;
+    }
+    return pl.N <= 64 ? 64 : pl.N <= 160 ? 128 : 256;
+}
+
+bool tree_eligible(const Plan &pl, std::string *why) {
+    auto no = [&](const char *m) { if (why) *why = m; return false; };
+    const long npag = pl.Pin.nnz() + (pl.p ? pl.A.nnz() : 0) + pl.G.nnz();
+    if (pl.lnz + 1 > FMAX || pl.N > FMAX || npag + 1 > FMAX) return no("factor or value count beyond 2^21");
+    if (lds_doubles(pl) * 8 > 160 * 1024) return no("per-QP state exceeds the 160 KiB LDS of a CU");
+    if (why) why->clear();
+    return true;
+}
+
+std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, TreeStats *stats) {
+    const long n = pl.n, m = pl.m, p = pl.p, N = pl.N, lnz = pl.lnz;
+    const long nP = pl.Pin.nnz(), nA = p ? pl.A.nnz() : 0, nG = pl.G.nnz(), npag = nP + nA + nG;
+    std::ostringstream o;
+    o << "// generated by qpb_tree for plan " << std::hex << pl.hash << std::dec << ": n=" << n << " m=" << m
+      << " p=" << p << " N=" << N << " Lnz=" << lnz << " [tree, fast]\n";
+    o << "#define QPB_NX " << n << "\n#define QPB_NZ " << m << "\n#define QPB_NY " << p << "\n#define QPB_N " << N
+      << "\n#define QPB_LNZ " << lnz << "\n#define QPB_NNZP " << nP << "\n#define QPB_NNZA " << nA
+      << "\n#define QPB_NNZG " << nG << "\n#define QPB_WG " << wg << "\n";
+    if (const char *e = getenv("QPB_TREE_OPTS")) {     // experiment knobs (#ifndef blocks of qpb_tree.hip)
+        std::istringstream in(e);
+        std::string kv;
+        while (in >> kv) {
+            const size_t eq = kv.find('=');
+            if (eq != std::string::npos) o << "#define " << kv.substr(0, eq) << " " << kv.substr(eq + 1) << "\n";
+        }
+    }
+
+    // levels: height above the leaves of the elimination tree (parent > child)
+    std::vector<long> level(N, 0);
+    for (long j = 0; j < N; j++)
+        if (pl.parent[j] >= 0) level[pl.parent[j]] = std::max(level[pl.parent[j]], level[j] + 1);
+    const long H = N ? *std::max_element(level.begin(), level.end()) + 1 : 0;
+    // row structures of L: rs[i] = (k, position of L(i,k)), k ascending
+    std::vector<std::vector<std::pair<long, long>>> rs(N);
+    for (long k = 0; k < N; k++)
+        for (long e = pl.Lp[k]; e < pl.Lp[k + 1]; e++) rs[pl.Li[e]].push_back({k, e});
+
+    // fac
+    Prog fac, fwd, bwd, mv, obj;
+    long fac_contrib = 0;
+    {
+        std::vector<std::vector<Task>> lv(H);
+        for (long j = 0; j < N; j++) {
+            Task d{(int32_t)(-1 - j), {}};
+            for (auto &kp : rs[j]) d.con.push_back(pk(kp.second, kp.second, kp.first));
+            fac_contrib += (long)d.con.size();
+            lv[level[j]].push_back(std::move(d));
+            for (long e = pl.Lp[j]; e < pl.Lp[j + 1]; e++) {
+                const long i = pl.Li[e];
+                Task t{(int32_t)e, {}};
+                size_t a = 0, b = 0;
+                const auto &ri = rs[i], &rj = rs[j];
+                while (a < ri.size() && b < rj.size() && ri[a].first < j && rj[b].first < j) {
+                    if (ri[a].first < rj[b].first) a++;
+                    else if (ri[a].first > rj[b].first) b++;
+                    else { t.con.push_back(pk(ri[a].second, rj[b].second, ri[a].first)); a++; b++; }
+                }
+                fac_contrib += (long)t.con.size();
+                if (!t.con.empty()) lv[level[j]].push_back(std::move(t));   // else LD(i,j) = K(i,j) as assembled
+            }
+        }
+        for (auto &l : lv) pack_level(l, wg, pk(lnz, lnz, 0), fac);
+    }
+    // fwd / bwd
+    {
+        std::vector<std::vector<Task>> lf(H), lb(H);
+        for (long i = 0; i < N; i++) {
+            Task t{(int32_t)i, {}};
+            for (auto &kp : rs[i]) t.con.push_back(pk(kp.second, kp.first));
+            lf[level[i]].push_back(std::move(t));
+            Task u{(int32_t)i, {}};
+            for (long e = pl.Lp[i]; e < pl.Lp[i + 1]; e++) u.con.push_back(pk(e, pl.Li[e]));
+            if (!u.con.empty()) lb[level[i]].push_back(std::move(u));
+        }
+        for (auto &l : lf) pack_level(l, wg, pk(lnz, 0), fwd);
+        for (long h = H - 1; h >= 0; h--) pack_level(lb[h], wg, pk(lnz, 0), bwd);
+    }
+    // mv / obj (natural KKT rows; K is symmetric in pattern and, before the z
+    // diagonal update, in value: column r lists row r)
+    auto pag = [&](const Slot &s) -> long {
+        return s.kind == Src::P ? s.idx : s.kind == Src::A ? nP + s.idx : s.kind == Src::G ? nP + nA + s.idx : -1;
+    };
+    {
+        std::vector<Task> lm, lo;
+        for (long r = 0; r < N; r++) {
+            Task t{(int32_t)r, {}}, u{(int32_t)r, {}};
+            for (long s = pl.K.jc[r]; s < pl.K.jc[r + 1]; s++) {
+                const Slot &sl = pl.K_init[s];
+                const long v = pag(sl);
+                if (v < 0) continue;
+                t.con.push_back(pk(v, pl.K.ir[s]));
+                if (sl.kind == Src::P) u.con.push_back(pk(v, pl.K.ir[s]));
+            }
+            lm.push_back(std::move(t));
+            if (r < n) lo.push_back(std::move(u));
+        }
+        pack_level(lm, wg, pk(npag, 0), mv);
+        pack_level(lo, wg, pk(npag, 0), obj);
+    }
+    // KKT assembly into the factor layout: column c = perm[a] of the KKT gives
+    // entry (a, b = pinv[row]) of P K P' for b <= a only (ldl.c:287-288)
+    std::vector<int32_t> asrc_i(lnz + N, -1), asrc_l(lnz + N, -1);
+    auto code = [&](const Slot &s) -> int32_t {
+        if (s.kind == Src::NegOne) return -2;
+        if (s.kind == Src::ZDiag) return -3 - s.idx;
+        return (int32_t)pag(s);
+    };
+    for (long c = 0; c < N; c++) {
+        const long a = pl.pinv[c];
+        for (long s = pl.K.jc[c]; s < pl.K.jc[c + 1]; s++) {
+            const long b = pl.pinv[pl.K.ir[s]];
+            if (b > a) continue;
+            const long tgt = b == a ? lnz + a : lpos(pl, a, b);
+            if (tgt < 0) continue;   // cannot happen: the symbolic factor holds every KKT entry
+            asrc_i[tgt] = code(pl.K_init[s]);
+            asrc_l[tgt] = code(pl.K_loop[s]);
+        }
+    }
+    table<long>(o, "int", "qpb_pinv", N, [&](long k) { return pl.pinv[k]; });
+    table<long>(o, "int", "qpb_asrc_i", lnz + N, [&](long k) { return asrc_i[k]; });
+    table<long>(o, "int", "qpb_asrc_l", lnz + N, [&](long k) { return asrc_l[k]; });
+    emit_prog(o, "fac", fac);
+    emit_prog(o, "fwd", fwd);
+    emit_prog(o, "bwd", bwd);
+    emit_prog(o, "mv", mv);
+    emit_prog(o, "obj", obj);
+    if (stats) {
+        stats->levels = H;
+        stats->fac_steps = fac.nsteps(); stats->fwd_steps = fwd.nsteps();
+        stats->bwd_steps = bwd.nsteps(); stats->mv_steps = mv.nsteps();
+        stats->fac_contrib = fac_contrib;
+        stats->desc_words = (long)(fac.desc.size() + fwd.desc.size() + bwd.desc.size() + mv.desc.size() + obj.desc.size());
+        stats->lds_bytes = lds_doubles(pl) * 8;
+    }
+    const std::string body = o.str() + kTreeTemplate;
+    const uint64_t h = fnv1a(body);
+    char name[96];
+    snprintf(name, sizeof name, "qpb_tree_%016llx_w%d_%08llx", (unsigned long long)pl.hash, wg,
+             (unsigned long long)(h & 0xffffffffull));
+    if (name_out) *name_out = name;
+    return std::string("#define QPB_KERNEL_NAME ") + name + "\n" + body;
+}
+
+}  // namespace qpb

@@ -1,0 +1,402 @@
+// qpb_tree.hip -- tree kernel: ONE QP per workgroup, any sparsity pattern.
+//
+// Template source: the host (qpb_tree.cpp generate_tree_kernel) prepends the
+// sizes, the KKT assembly tables and five gather programs (fac, fwd, bwd, mv,
+// obj), each a list of steps; see qpb_tree.cpp for their meaning.  Everything a
+// QP needs lives in the workgroup's LDS for the whole solve: the P/A/G values,
+// the factor (stored as LD = L*D, plus 1/D), and every IPM vector.  Global
+// memory is touched to stage the inputs, to read the (plan-wide, cache-resident)
+// program tables, and to write the outputs.
+//
+// A program step: lane l < ntask*G works on task l/G and sums that task's terms
+// l%G, l%G+G, ...; a butterfly over the G lanes completes the sum; the task's
+// first lane applies the epilogue.  A workgroup barrier closes each level.
+//
+// Reference: qpSWIFT's Mehrotra predictor-corrector (qpSWIFT.c:473-644,
+// kkt_initialize Auxilary.c:992-1089), LDL' with dynamic regularisation
+// (ldl.c:253-326), triangular solves (ldl.c:495-557), residuals
+// (Auxilary.c:745-786), step length (Auxilary.c:359-393), formrho
+// (Auxilary.c:879-892).  Fast mode: FMA contraction, reciprocal pivots.
+#pragma clang fp contract(fast)
+
+struct qpb_args {
+    const double *P, *A, *G, *c, *h, *b;
+    double *x, *y, *z, *s;
+    int *flag, *iters;
+    double *fval;
+    double *stats;
+    long B;
+    double tol, abstol, sigma_d;
+    long maxit;
+};
+
+#define NX QPB_NX
+#define NY QPB_NY
+#define NZ QPB_NZ
+#define NN QPB_N
+#define LNZ QPB_LNZ
+#define NY1 (NY > 0 ? NY : 1)
+#define NPAG (QPB_NNZP + QPB_NNZA + QPB_NNZG)
+#define NW (QPB_WG / 64)
+
+// LDS layout of a QP (doubles)
+#define O_PAG 0                        // P | A | G values, [NPAG] = 0
+#define O_LD (O_PAG + NPAG + 1)        // factor L*D in L's CSC order, [LNZ] = 0
+#define O_RD (O_LD + LNZ + 1)          // 1/D (holds the assembled diagonal before the factor)
+#define O_V (O_RD + NN)                // x | y | z
+#define O_S (O_V + NN)                 // s
+#define O_R (O_S + NZ)                 // residual products / rx | ry | rz
+#define O_W (O_R + NN)                 // permuted solve vector
+#define O_C (O_W + NN)
+#define O_H (O_C + NX)
+#define O_B (O_H + NZ)
+#define O_DS (O_B + NY1)
+#define O_LAM (O_DS + NZ)
+#define O_DZ (O_LAM + NZ)
+#define O_DSL (O_DZ + NZ)
+#define O_XP (O_DSL + NZ)              // x at the start of the iteration (objective at maxit)
+#define O_RED (O_XP + NX)              // reduction scratch [NW][8]
+#define LDS_QP (O_RED + 64)
+
+static __device__ __forceinline__ double qpb_rcp(double v) {
+    double r = __builtin_amdgcn_rcp(v);
+    double e = __builtin_fma(-v, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-v, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+// 1 / regularise(d) (ldl.c:273-274, 319-320): |d| <= 1e-14 -> d = +-1e-7 (sign: d > 0)
+static __device__ __forceinline__ double qpb_rcp_reg(double d) {
+    const double r = qpb_rcp(d);
+    const double reg = d > 0.0 ? 1e7 : -1e7;
+    return __builtin_fabs(d) <= 1e-14 ? reg : r;
+}
+
+static __device__ __forceinline__ unsigned long long qpb_f0(unsigned long long d) { return d & 0x1FFFFFull; }
+static __device__ __forceinline__ unsigned long long qpb_f1(unsigned long long d) { return (d >> 21) & 0x1FFFFFull; }
+static __device__ __forceinline__ unsigned long long qpb_f2(unsigned long long d) { return d >> 42; }
+
+// Run one gather program.  term(acc, desc) -> acc; epi(out_code, acc).
+template <class Term, class Epi>
+static __device__ __forceinline__ void qpb_run(const int *__restrict__ steps, int nsteps,
+                                               const int *__restrict__ hdr,
+                                               const unsigned long long *__restrict__ desc, Term term, Epi epi) {
+    const int l = threadIdx.x;
+    for (int st = 0; st < nsteps; st++) {
+        const int doff = steps[4 * st], toff = steps[4 * st + 1], ntg = steps[4 * st + 2], rb = steps[4 * st + 3];
+        const int g = ntg & 15, act = (ntg >> 4) << g, R = rb & 0xffff;
+        double acc = 0.0;
+        if (l < act) {
+            const unsigned long long *d = desc + doff + l;
+            int r = 0;
+            for (; r + 4 <= R; r += 4) {
+                const unsigned long long d0 = d[(r + 0) * act], d1 = d[(r + 1) * act], d2 = d[(r + 2) * act],
+                                         d3 = d[(r + 3) * act];
+                acc = term(acc, d0);
+                acc = term(acc, d1);
+                acc = term(acc, d2);
+                acc = term(acc, d3);
+            }
+            for (; r < R; r++) acc = term(acc, d[r * act]);
+        }
+        for (int o = 1; o < (1 << g); o <<= 1) acc += __shfl_xor(acc, o, 64);
+        if (l < act && (l & ((1 << g) - 1)) == 0) epi(hdr[toff + (l >> g)], acc);
+        if (rb >> 16) __syncthreads();
+    }
+}
+
+// K-value sums over the workgroup (result in every thread)
+template <int K>
+static __device__ __forceinline__ void qpb_bsum(double (&v)[K], double *red) {
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < K; k++) red[w * 8 + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        v[k] = red[k];
+        for (int ww = 1; ww < NW; ww++) v[k] += red[ww * 8 + k];
+    }
+    __syncthreads();
+}
+template <int K>
+static __device__ __forceinline__ void qpb_bmin(double (&v)[K], double *red) {
+#pragma unroll
+    for (int k = 0; k < K; k++)
+        for (int o = 32; o > 0; o >>= 1) v[k] = __builtin_fmin(v[k], __shfl_xor(v[k], o, 64));
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int k = 0; k < K; k++) red[w * 8 + k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        v[k] = red[k];
+        for (int ww = 1; ww < NW; ww++) v[k] = __builtin_fmin(v[k], red[ww * 8 + k]);
+    }
+    __syncthreads();
+}
+
+extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a) {
+    __shared__ __attribute__((aligned(16))) double L[LDS_QP];
+    const int t = threadIdx.x;
+    const long q = blockIdx.x;
+    if (q >= a.B) return;                        // workgroup-uniform
+    const long tile = q >> 6;
+    const int ql = (int)(q & 63);
+    double *__restrict__ PAG = L + O_PAG;
+    double *__restrict__ LD = L + O_LD;
+    double *__restrict__ rD = L + O_RD;
+    double *__restrict__ V = L + O_V;
+    double *__restrict__ S = L + O_S;
+    double *__restrict__ R = L + O_R;
+    double *__restrict__ W = L + O_W;
+    double *__restrict__ Cv = L + O_C;
+    double *__restrict__ Hv = L + O_H;
+    double *__restrict__ Bv = L + O_B;
+    double *__restrict__ DS = L + O_DS;
+    double *__restrict__ LAM = L + O_LAM;
+    double *__restrict__ DZ = L + O_DZ;
+    double *__restrict__ DSL = L + O_DSL;
+    double *__restrict__ XP = L + O_XP;
+    double *__restrict__ RED = L + O_RED;
+
+    // ---- stage the inputs (tiled SoA: value j of QP q at tile*nv*64 + j*64 + q%64)
+    for (int j = t; j < QPB_NNZP; j += QPB_WG) PAG[j] = a.P[tile * (QPB_NNZP * 64) + j * 64 + ql];
+#if QPB_NNZA > 0
+    for (int j = t; j < QPB_NNZA; j += QPB_WG) PAG[QPB_NNZP + j] = a.A[tile * (QPB_NNZA * 64) + j * 64 + ql];
+#endif
+    for (int j = t; j < QPB_NNZG; j += QPB_WG) PAG[QPB_NNZP + QPB_NNZA + j] = a.G[tile * (QPB_NNZG * 64) + j * 64 + ql];
+    for (int j = t; j < NX; j += QPB_WG) Cv[j] = a.c[tile * (NX * 64) + j * 64 + ql];
+    for (int j = t; j < NZ; j += QPB_WG) Hv[j] = a.h[tile * (NZ * 64) + j * 64 + ql];
+#if NY > 0
+    for (int j = t; j < NY; j += QPB_WG) Bv[j] = a.b[tile * (NY * 64) + j * 64 + ql];
+#endif
+    if (t == 0) { PAG[NPAG] = 0.0; LD[LNZ] = 0.0; }
+    __syncthreads();
+
+    // KKT values into the factor layout (init: z diagonal -1; loop: -s/z)
+    auto assemble = [&](const int *__restrict__ src) {
+        for (int e = t; e < LNZ + NN; e += QPB_WG) {
+            const int sc = src[e];
+            double v;
+            if (sc >= 0) v = PAG[sc];
+            else if (sc == -1) v = 0.0;
+            else if (sc == -2) v = -1.0;
+            else { const int r = -3 - sc; v = -S[r] * qpb_rcp(V[NX + NY + r]); }
+            L[O_LD + e + (e >= LNZ ? 1 : 0)] = v;      // e >= LNZ: diagonal -> rD[e - LNZ]
+        }
+        __syncthreads();
+    };
+    auto factor = [&]() {
+        qpb_run(qpb_fac_steps, QPB_fac_NSTEPS, qpb_fac_hdr, qpb_fac_desc,
+                [&](double acc, unsigned long long d) {
+                    return __builtin_fma(-LD[qpb_f0(d)] * rD[qpb_f2(d)], LD[qpb_f1(d)], acc);
+                },
+                [&](int out, double acc) {
+                    if (out >= 0) LD[out] += acc;
+                    else { const int j = -1 - out; rD[j] = qpb_rcp_reg(rD[j] + acc); }
+                });
+    };
+    // W (permuted rhs) -> W (permuted solution)
+    auto solve = [&]() {
+        qpb_run(qpb_fwd_steps, QPB_fwd_NSTEPS, qpb_fwd_hdr, qpb_fwd_desc,
+                [&](double acc, unsigned long long d) { return __builtin_fma(-LD[qpb_f0(d)], W[qpb_f1(d)], acc); },
+                [&](int i, double acc) { W[i] = rD[i] * (W[i] + acc); });
+        qpb_run(qpb_bwd_steps, QPB_bwd_NSTEPS, qpb_bwd_hdr, qpb_bwd_desc,
+                [&](double acc, unsigned long long d) { return __builtin_fma(-LD[qpb_f0(d)], W[qpb_f1(d)], acc); },
+                [&](int k, double acc) { W[k] = __builtin_fma(rD[k], acc, W[k]); });
+    };
+    // R = [P A' G'; A 0 0; G 0 0] V (raw products)
+    auto products = [&](const double *__restrict__ vec) {
+        qpb_run(qpb_mv_steps, QPB_mv_NSTEPS, qpb_mv_hdr, qpb_mv_desc,
+                [&](double acc, unsigned long long d) { return __builtin_fma(PAG[qpb_f0(d)], vec[qpb_f1(d)], acc); },
+                [&](int r, double acc) { R[r] = acc; });
+    };
+
+    // ---- kkt_initialize (Auxilary.c:992-1089): K with the -I block, rhs [-c; b; h]
+    assemble(qpb_asrc_i);
+    for (int r = t; r < NN; r += QPB_WG)
+        W[qpb_pinv[r]] = r < NX ? -Cv[r] : (r < NX + NY ? Bv[r - NX] : Hv[r - NX - NY]);
+    factor();
+    solve();
+    for (int r = t; r < NN; r += QPB_WG) V[r] = r < NX + NY ? W[qpb_pinv[r]] : 0.0;
+    __syncthreads();
+    products(V);
+    {
+        double lo = 1e300, hi = -1e300;
+        for (int r = t; r < NZ; r += QPB_WG) {
+            const double zi = Hv[r] - R[NX + NY + r];
+            lo = __builtin_fmin(lo, zi);
+            hi = __builtin_fmax(hi, zi);
+        }
+        double mm[2] = {lo, -hi};
+        qpb_bmin(mm, RED);
+        lo = mm[0];
+        hi = -mm[1];
+        const double shift = -lo;
+        for (int r = t; r < NZ; r += QPB_WG) {
+            const double zi = Hv[r] - R[NX + NY + r];
+            S[r] = shift < 0 ? zi : zi + (1.0 + shift);
+            V[NX + NY + r] = hi < 0 ? -zi : -zi + (1.0 + hi);
+        }
+        __syncthreads();
+    }
+
+    // ---- QP_SOLVE (qpSWIFT.c:502-602)
+    double sigma = 100.0, alpha_p = 0.0, alpha_d = 0.0;
+    double n_rx = 0.0, n_ry = 0.0, n_rz = 0.0, n_mu = 0.0;
+    long it = 0;
+    int flag = 2;
+    const double invm = 1.0 / (double)NZ;
+    for (; it < a.maxit; it++) {
+        products(V);
+        {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int r = t; r < NN; r += QPB_WG) {
+                double v;
+                if (r < NX) { v = -R[r] - Cv[r]; XP[r] = V[r]; acc[0] = __builtin_fma(v, v, acc[0]); }
+                else if (r < NX + NY) { v = Bv[r - NX] - R[r]; acc[1] = __builtin_fma(v, v, acc[1]); }
+                else {
+                    const int i = r - NX - NY;
+                    v = Hv[i] - R[r] - S[i];
+                    acc[2] = __builtin_fma(v, v, acc[2]);
+                    acc[3] = __builtin_fma(S[i], V[r], acc[3]);
+                }
+                R[r] = v;
+            }
+            qpb_bsum(acc, RED);
+            n_rx = __builtin_sqrt(acc[0]);
+            n_ry = __builtin_sqrt(acc[1]);
+            n_rz = __builtin_sqrt(acc[2]);
+            n_mu = acc[3] * invm;
+        }
+        if (n_rx < a.tol && n_rz < a.tol && (NY == 0 || n_ry < a.tol) && n_mu < a.abstol) { flag = 0; break; }
+        double mu;
+        {
+            double acc[1] = {0.0};
+            for (int i = t; i < NZ; i += QPB_WG) {
+                const double lm = __builtin_sqrt(S[i] * V[NX + NY + i]);
+                LAM[i] = lm;
+                acc[0] = __builtin_fma(lm, lm, acc[0]);
+            }
+            qpb_bsum(acc, RED);
+            mu = acc[0] * invm;
+        }
+        // rhs b = [rx; ry; rz - ds/z] (updatekktmatrix_b, Auxilary.c:274-295)
+        auto rhs = [&]() {
+            for (int r = t; r < NN; r += QPB_WG) {
+                double v = R[r];
+                if (r >= NX + NY) { const int i = r - NX - NY; v -= DS[i] * qpb_rcp(V[r]); }
+                W[qpb_pinv[r]] = v;
+            }
+        };
+        if (sigma > a.sigma_d) {
+            // predictor: ds = -lambda^2 (form_ds, Auxilary.c:319-326); kktsolve_1
+            for (int i = t; i < NZ; i += QPB_WG) DS[i] = -LAM[i] * LAM[i];
+            __syncthreads();
+            assemble(qpb_asrc_l);
+            rhs();
+            factor();
+            solve();
+            double ab[2] = {1e300, 1e300};
+            for (int i = t; i < NZ; i += QPB_WG) {
+                const double zi = V[NX + NY + i], dz = W[qpb_pinv[NX + NY + i]];
+                const double dsl = (DS[i] - S[i] * dz) * qpb_rcp(zi);
+                DZ[i] = dz;
+                DSL[i] = dsl;
+                if (dsl < 0) ab[0] = __builtin_fmin(ab[0], -(S[i] / dsl));
+                if (dz < 0) ab[1] = __builtin_fmin(ab[1], -(zi / dz));
+            }
+            qpb_bmin(ab, RED);
+            const double ap = ab[0] < 1e10 ? ab[0] : 1.0, ad = ab[1] < 1e10 ? ab[1] : 1.0;
+            double rr[2] = {0.0, 0.0};
+            for (int i = t; i < NZ; i += QPB_WG) {
+                const double zi = V[NX + NY + i];
+                rr[0] = __builtin_fma(__builtin_fma(ap, DSL[i], S[i]), __builtin_fma(ad, DZ[i], zi), rr[0]);
+                rr[1] = __builtin_fma(S[i], zi, rr[1]);
+            }
+            qpb_bsum(rr, RED);
+            const double rho = rr[0] / rr[1];
+            const double r1 = rho < 1.0 ? rho : 1.0, cube = r1 * r1 * r1;
+            sigma = a.sigma_d < cube ? cube : a.sigma_d;
+            const double smu = sigma * mu;
+            for (int i = t; i < NZ; i += QPB_WG) DS[i] = -(LAM[i] * LAM[i]) - DSL[i] * DZ[i] + smu;
+            __syncthreads();
+            rhs();
+            __syncthreads();
+            solve();
+        } else {
+            // pure centering (qpSWIFT.c:572-579): refactor
+            sigma = a.sigma_d;
+            const double smu = sigma * mu;
+            for (int i = t; i < NZ; i += QPB_WG) DS[i] = -(LAM[i] * LAM[i]) + smu;
+            __syncthreads();
+            assemble(qpb_asrc_l);
+            rhs();
+            factor();
+            solve();
+        }
+        // kktsolve_2 extraction, step length, updates (qpSWIFT.c:583-600)
+        {
+            double ab[2] = {1e300, 1e300};
+            for (int i = t; i < NZ; i += QPB_WG) {
+                const double zi = V[NX + NY + i], dz = W[qpb_pinv[NX + NY + i]];
+                const double dsl = (DS[i] - S[i] * dz) * qpb_rcp(zi);
+                DZ[i] = dz;
+                DSL[i] = dsl;
+                if (dsl < 0) ab[0] = __builtin_fmin(ab[0], -(S[i] / dsl));
+                if (dz < 0) ab[1] = __builtin_fmin(ab[1], -(zi / dz));
+            }
+            qpb_bmin(ab, RED);
+            alpha_p = ab[0] < 1e10 ? ab[0] : 1.0;
+            alpha_d = ab[1] < 1e10 ? ab[1] : 1.0;
+            alpha_p = 0.99 * alpha_p > 1.0 ? 1.0 : 0.99 * alpha_p;
+            alpha_d = 0.99 * alpha_d > 1.0 ? 1.0 : 0.99 * alpha_d;
+            for (int r = t; r < NN; r += QPB_WG) {
+                if (r < NX) V[r] = __builtin_fma(W[qpb_pinv[r]], alpha_p, V[r]);
+                else if (r < NX + NY) V[r] = __builtin_fma(W[qpb_pinv[r]], alpha_d, V[r]);
+                else {
+                    const int i = r - NX - NY;
+                    S[i] = __builtin_fma(DSL[i], alpha_p, S[i]);
+                    V[r] = __builtin_fma(DZ[i], alpha_d, V[r]);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (it == a.maxit) flag = 2;
+
+    // ---- objective of the x the last residuals were computed at (qpSWIFT.c:515)
+    const double *xo = flag == 0 ? V : XP;
+    qpb_run(qpb_obj_steps, QPB_obj_NSTEPS, qpb_obj_hdr, qpb_obj_desc,
+            [&](double acc, unsigned long long d) { return __builtin_fma(PAG[qpb_f0(d)], xo[qpb_f1(d)], acc); },
+            [&](int r, double acc) { R[r] = acc; });
+    double fv[1] = {0.0};
+    for (int r = t; r < NX; r += QPB_WG) fv[0] += xo[r] * (0.5 * R[r] + Cv[r]);
+    qpb_bsum(fv, RED);
+
+    // ---- outputs
+    for (int j = t; j < NX; j += QPB_WG) a.x[tile * (NX * 64) + j * 64 + ql] = V[j];
+#if NY > 0
+    for (int j = t; j < NY; j += QPB_WG) a.y[tile * (NY * 64) + j * 64 + ql] = V[NX + j];
+#endif
+    for (int j = t; j < NZ; j += QPB_WG) {
+        a.z[tile * (NZ * 64) + j * 64 + ql] = V[NX + NY + j];
+        a.s[tile * (NZ * 64) + j * 64 + ql] = S[j];
+    }
+    if (t == 0) {
+        a.flag[q] = flag;
+        a.iters[q] = (int)it;
+        a.fval[q] = fv[0];
+        if (a.stats) {
+            double *st = a.stats + tile * (6 * 64) + ql;
+            st[0] = n_rx; st[64] = n_ry; st[128] = n_rz; st[192] = n_mu; st[256] = alpha_p; st[320] = alpha_d;
+        }
+    }
+}

@@ -54,6 +54,8 @@ typedef struct qpb_plan qpb_plan;
 #define QPB_KERNEL_WAVE 0x200  /* always the wave kernel (wave or row form)         */
 #define QPB_KERNEL_NOROW 0x400 /* wave kernel in its one-QP-per-wavefront form even
                                   where the row form (four QPs per wavefront) fits */
+#define QPB_KERNEL_TREE 0x800  /* always the tree kernel (one QP per workgroup,
+                                  level-scheduled sparse LDL'; any pattern)        */
 
 /* error codes */
 #define QPB_OK        0
@@ -81,6 +83,8 @@ typedef struct qpb_plan_info {
     int  wave_ok;                /* plan can use the wave-cooperative kernel */
     long wave_max_batch;         /* qpb_solve uses it for B <= this (-1: always) */
     int  wave_qpw;               /* QPs per wavefront of that kernel: 1 wave form, 4 row form */
+    int  tree_ok;                /* plan can use the tree kernel (one QP per workgroup) */
+    int  large_kernel;           /* kernel used beyond the wave kernel's range: 1 lane, 2 wave, 3 tree */
 } qpb_plan_info;
 
 void qpb_default_settings(qpb_settings *st);
@@ -97,6 +101,7 @@ int  qpb_plan_get_perm(const qpb_plan *plan, long *perm /* [N] */);
  * cap-1 bytes plus a NUL when buf is non-NULL). */
 long qpb_plan_source(const qpb_plan *plan, char *buf, long cap);
 long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap);
+long qpb_plan_tree_source(const qpb_plan *plan, char *buf, long cap);
 /* Compile the plan's kernels for gfx950 (hiprtc) or fetch them from the
  * code-object cache; needs no GPU.  qpb_solve calls this implicitly. */
 int  qpb_plan_compile(qpb_plan *plan);

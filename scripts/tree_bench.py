@@ -1,0 +1,62 @@
+"""Kernel timings per plan / kernel / batch (HIP events around qpb_solve).
+
+    python scripts/tree_bench.py [name:kernel:B ...]
+
+Default cases: the MPC-horizon QP on the tree kernel (configs[3]) and the
+controller / C1 shapes on the tree vs wave kernels.  One JSON line per case."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def qp(name, ids):
+    from apf_quadruped_amd import plans, workloads as W
+    if name == "c30":
+        return W.controller_qp(plans.SEED + 30, ids)
+    return plans.standard_qp(name, ids)
+
+
+def main():
+    import torch
+    from apf_quadruped_amd.batch import Plan
+    cases = sys.argv[1:] or ["mpc_h10:tree:1024", "mpc_h10:tree:8192", "c30:tree:1024", "c30:wave:1024",
+                             "c30:tree:8192", "c30:wave:8192", "c1:tree:1024", "c1:wave:1024", "c1:tree:65536",
+                             "c1:wave:65536", "c1:lane:65536", "c1:wave:262144", "c1:lane:262144",
+                             "c1:wave:1048576", "c1:lane:1048576"]
+    for case in cases:
+        name, kernel, B = case.split(":")
+        B = int(B)
+        d0 = qp(name, np.arange(1))
+        plan = Plan.from_dense(d0["n"], d0["m"], d0["p"], d0["P"][0], d0["A"][0], d0["G"][0], kernel=kernel)
+        nb = min(B, 4096)
+        d = qp(name, np.arange(nb))
+        reps = (B + nb - 1) // nb
+        tile = lambda a: np.concatenate([a] * reps)[:B]
+        vals = plan.pack(*(tile(d[k]) for k in ("P", "A", "G", "c", "h", "b")))
+        vals = {k: torch.from_numpy(v).cuda() for k, v in vals.items()}
+        out = plan.alloc_outputs(B)
+        go = plan.launcher(vals, out, B)
+        go()
+        torch.cuda.synchronize()
+        iters = 3 if B >= 262144 else 10
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            go()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        r = plan.unpack(out, B)
+        print(json.dumps(dict(case=case, kernel=plan.kernel_name(B), ms=ms, qps=B / ms * 1e3,
+                              optimal=float((r["flag"] == 0).mean()), mean_iters=float(r["iters"].mean()),
+                              max_iters=int(r["iters"].max()))), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -169,7 +169,7 @@ def test_wave_kernel_matches_oracle_in_its_order(name, kernel, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["lane", "wave", "wave1"])
+@pytest.mark.parametrize("kernel", ["lane", "wave", "wave1", "tree"])
 @pytest.mark.parametrize("B", [1, 2, 3, 5, 63, 65, 1000])
 def test_ragged_batches(B, kernel, oracle):
     from apf_quadruped_amd import workloads as W
@@ -237,7 +237,7 @@ def test_argmin_device_reduction():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["lane", "wave", "wave1"])
+@pytest.mark.parametrize("kernel", ["lane", "wave", "wave1", "tree"])
 def test_solve_best_fused_argmin(kernel):
     """qpb_solve_best == qpb_solve + qpb_argmin, repeatedly, for ragged batch sizes
     (1 and 1024 take the single-block argmin, 3000 too; 100003 the two-stage one)."""

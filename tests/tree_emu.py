@@ -1,0 +1,110 @@
+"""CPU emulation of the tree kernel's gather programs (test tool, no GPU).
+
+Parses the tables the generator prepends to qpb_tree.hip (Plan.tree_source())
+and executes the programs step by step with the kernel's semantics (lane l of a
+step sums terms l%G, l%G+G, ... of task l/G; the task's epilogue applies the
+sum).  Used to check the generated KKT assembly, LDL', solves and residual
+products against dense numpy linear algebra on the CPU."""
+from __future__ import annotations
+
+import re
+
+import numpy as np
+
+FB = 21
+FM = (1 << FB) - 1
+
+
+def parse_tables(src: str) -> dict:
+    out = {}
+    for m in re.finditer(r"#define (QPB_\w+) (-?\d+)\n", src):
+        out[m.group(1)] = int(m.group(2))
+    for m in re.finditer(r"__constant__ (?:int|unsigned long long) (\w+)\[\d+\] = \{([^}]*)\};", src):
+        vals = [int(v.strip().rstrip("ul")) for v in m.group(2).replace("\n", "").split(",") if v.strip()]
+        out[m.group(1)] = np.array(vals, dtype=np.int64 if "desc" not in m.group(1) else np.uint64)
+    return out
+
+
+def run_prog(T, name, term, epi, wg):
+    steps = T[f"qpb_{name}_steps"].reshape(-1, 4)[:T[f"QPB_{name}_NSTEPS"]]
+    hdr, desc = T[f"qpb_{name}_hdr"], T[f"qpb_{name}_desc"]
+    for doff, toff, ntg, rb in steps:
+        g = int(ntg) & 15
+        G, nt, R = 1 << g, int(ntg) >> 4, int(rb) & 0xFFFF
+        act = nt * G
+        assert act <= wg
+        acc = np.zeros(act)
+        for r in range(R):
+            for lane in range(act):
+                d = int(desc[doff + r * act + lane])
+                acc[lane] = term(acc[lane], d & FM, (d >> FB) & FM, d >> (2 * FB))
+        for t in range(nt):
+            epi(int(hdr[toff + t]), float(acc[t * G:(t + 1) * G].sum()))
+
+
+def rcp_reg(d):
+    if abs(d) <= 1e-14:
+        return 1e7 if d > 0 else -1e7
+    return 1.0 / d
+
+
+class TreeEmu:
+    def __init__(self, plan):
+        self.plan = plan
+        self.src = plan.tree_source()
+        self.T = parse_tables(self.src)
+        T = self.T
+        self.n, self.m, self.p, self.N = T["QPB_NX"], T["QPB_NZ"], T["QPB_NY"], T["QPB_N"]
+        self.lnz, self.wg = T["QPB_LNZ"], T["QPB_WG"]
+        self.pinv = T["qpb_pinv"][:self.N]
+
+    def assemble(self, pag, loop, s=None, z=None):
+        src = self.T["qpb_asrc_l" if loop else "qpb_asrc_i"][: self.lnz + self.N]
+        LD = np.zeros(self.lnz + 1)
+        rD = np.zeros(self.N)
+        for e, sc in enumerate(src):
+            v = pag[sc] if sc >= 0 else 0.0 if sc == -1 else -1.0 if sc == -2 else -s[-3 - sc] / z[-3 - sc]
+            if e < self.lnz:
+                LD[e] = v
+            else:
+                rD[e - self.lnz] = v
+        return LD, rD
+
+    def factor(self, LD, rD):
+        def term(acc, a, b, k):
+            return acc - LD[a] * rD[k] * LD[b]
+
+        def epi(out, acc):
+            if out >= 0:
+                LD[out] += acc
+            else:
+                j = -1 - out
+                rD[j] = rcp_reg(rD[j] + acc)
+        run_prog(self.T, "fac", term, epi, self.wg)
+
+    def solve(self, LD, rD, rhs_natural):
+        W = np.zeros(self.N)
+        W[self.pinv] = rhs_natural
+
+        def tf(acc, a, k, _):
+            return acc - LD[a] * W[k]
+
+        def ef(i, acc):
+            W[i] = rD[i] * (W[i] + acc)
+
+        def eb(k, acc):
+            W[k] = W[k] + rD[k] * acc
+        run_prog(self.T, "fwd", tf, ef, self.wg)
+        run_prog(self.T, "bwd", tf, eb, self.wg)
+        return W[self.pinv]
+
+    def products(self, pag, v, prog="mv"):
+        R = np.zeros(self.N)
+
+        def term(acc, a, j, _):
+            return acc + pag[a] * v[j]
+
+        def epi(r, acc):
+            R[r] = acc
+        run_prog(self.T, prog, term, epi, self.wg)
+        return R
