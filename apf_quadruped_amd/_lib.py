@@ -64,6 +64,8 @@ def lib() -> C.CDLL:
     L.qpb_plan_wave_source.argtypes = [vp, C.c_char_p, C.c_long]
     L.qpb_plan_tree_source.restype = C.c_long
     L.qpb_plan_tree_source.argtypes = [vp, C.c_char_p, C.c_long]
+    L.qpb_plan_tree_tables.restype = C.c_long
+    L.qpb_plan_tree_tables.argtypes = [vp, C.c_void_p, C.c_long]
     L.qpb_plan_compile.argtypes = [vp]
     L.qpb_solve.restype = C.c_int
     L.qpb_solve.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp]

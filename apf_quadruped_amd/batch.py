@@ -166,6 +166,15 @@ class Plan:
         L.qpb_plan_tree_source(self._h, buf, size + 1)
         return buf.value.decode()
 
+    def tree_tables(self) -> bytes:
+        """The tree kernel's plan tables (the device buffer it reads)."""
+        L = _lib.lib()
+        size = L.qpb_plan_tree_tables(self._h, None, 0)
+        check(0 if size >= 0 else int(size), "qpb_plan_tree_tables")
+        buf = C.create_string_buffer(max(size, 1))
+        L.qpb_plan_tree_tables(self._h, buf, size)
+        return buf.raw[:size]
+
     def compile(self) -> None:
         check(_lib.lib().qpb_plan_compile(self._h), "qpb_plan_compile")
 

@@ -33,6 +33,7 @@ struct KernelArgs {
     double tol;                             // reltol / sqrt(3) (qpSWIFT.c:521)
     double abstol, sigma_d;
     long maxit;
+    const void *tab = nullptr;              // tree kernel only: plan tables on the device
 };
 
 std::string kernel_name(const Plan &pl, const GenOptions &opt);

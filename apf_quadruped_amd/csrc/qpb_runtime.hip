@@ -136,6 +136,16 @@ __global__ void __launch_bounds__(256) qpb_strided_copy(qpb::CopySegs t) {
 
 }  // namespace
 
+qpb_plan::~qpb_plan() {
+    for (auto &kv : tree_dev) {
+        int cur = 0;
+        if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
+            (void)hipFree(kv.second);
+            (void)hipSetDevice(cur);
+        }
+    }
+}
+
 namespace qpb {
 
 // Compile (hiprtc, gfx950) or fetch from the memory / disk cache.
@@ -193,6 +203,26 @@ std::string wave_source_of(const qpb_plan *plan) {
 int compile_wave(qpb_plan *plan) {
     if (!plan->wave_ok) return fail(QPB_EINVAL, "plan is not eligible for the wave kernel");
     return compile_kernel(plan->wave_kname, [plan] { return wave_source_of(plan); }, false, &plan->wave_code);
+}
+
+// the tree kernel's plan tables on the current device (uploaded on first use;
+// a regular hipMalloc buffer, so they are cached in L2 like any input)
+int tree_tables_on_device(qpb_plan *plan, const void **out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(QPB_EHIP, "hipGetDevice failed (no GPU?)");
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = plan->tree_dev.find(dev);
+    if (it != plan->tree_dev.end()) { *out = it->second; return QPB_OK; }
+    void *p = nullptr;
+    const size_t n = std::max<size_t>(plan->tree_tables.size(), 8);
+    if (hipMalloc(&p, n) != hipSuccess) return fail(QPB_ENOMEM, "tree tables: hipMalloc failed");
+    if (hipMemcpy(p, plan->tree_tables.data(), plan->tree_tables.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(p);
+        return fail(QPB_EHIP, "tree tables: upload failed");
+    }
+    plan->tree_dev[dev] = p;
+    *out = p;
+    return QPB_OK;
 }
 
 int compile_tree(qpb_plan *plan) {
@@ -280,10 +310,9 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
         return fail(QPB_EINVAL, "QPB_KERNEL_TREE: " + (plan->gen.exact ? std::string("exact plans use the lane kernel") : why_tree));
     if (plan->tree_ok) {
         plan->tree_wg = qpb::tree_wg_for(plan->pl);
-        qpb::generate_tree_kernel(plan->pl, plan->tree_wg, &plan->tree_kname);
+        qpb::generate_tree_kernel(plan->pl, plan->tree_wg, &plan->tree_kname, nullptr, &plan->tree_tables);
     }
     plan->wave_max_batch = 4096;   // measured crossover vs the lane kernel
-    if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
     if (plan->wave_ok) {
         // row form (four QPs per wavefront, all exchanges DPP) where the plan fits
         // a 16-lane row; QPB_KERNEL_NOROW or QPB_ROW=0 keep one QP per wavefront
@@ -291,17 +320,27 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
         if (!(flags & QPB_KERNEL_NOROW) && !(er && atoi(er) == 0) && qpb::row_eligible(plan->pl)) {
             plan->wave_qpw = 4;
             plan->wave_wg = 64;
+            plan->wave_max_batch = -1;   // the row form beats the lane kernel at every batch size
             qpb::generate_row_kernel(plan->pl, &plan->wave_kname);
         } else {
             plan->wave_wg = qpb::wave_wg_for(plan->pl);
             qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
         }
     }
+    if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
     *out = plan.release();
     return QPB_OK;
 }
 
 void qpb_plan_destroy(qpb_plan *plan) { delete plan; }
+
+long qpb_plan_tree_tables(const qpb_plan *plan, void *buf, long cap) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    if (!plan->tree_ok) return fail(QPB_EINVAL, "plan is not eligible for the tree kernel");
+    const long n = (long)plan->tree_tables.size();
+    if (buf && cap > 0) std::memcpy(buf, plan->tree_tables.data(), (size_t)std::min(cap, n));
+    return n;
+}
 
 int qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info) {
     if (!plan || !info) return fail(QPB_EINVAL, "NULL argument");
@@ -387,7 +426,8 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     // and wins while the batch does not fill the GPU with lane-kernel waves
     // beyond it: the lane kernel (one QP per lane) for small KKT systems, the tree
     // kernel (one QP per workgroup) for large ones
-    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 || (plan->kernel_pref == 0 && B <= plan->wave_max_batch));
+    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
+                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
     const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
     hipFunction_t fn;
     int rc = wave ? qpb::compile_wave(plan) : tree ? qpb::compile_tree(plan) : qpb::compile_plan(plan);
@@ -407,6 +447,7 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     a.abstol = st->abstol;
     a.sigma_d = st->sigma_d;
     a.maxit = st->maxit;
+    if (tree && (rc = qpb::tree_tables_on_device(plan, &a.tab))) return rc;
     void *params[] = {&a};
     const unsigned wg = (unsigned)(wave ? plan->wave_wg : tree ? plan->tree_wg : plan->gen.wg);
     const long per_block = wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup

@@ -1,6 +1,7 @@
 // qpb_runtime.hpp -- internals shared by the batched C ABI and the qpSWIFT drop-in.
 #pragma once
 
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -25,6 +26,9 @@ struct qpb_plan {
     int tree_wg = 256;
     std::string tree_kname;
     std::shared_ptr<std::vector<char>> tree_code;
+    std::vector<char> tree_tables;              // plan tables of the tree kernel (host copy)
+    std::map<int, void *> tree_dev;             // device -> uploaded tables
+    ~qpb_plan();
 };
 
 namespace qpb {

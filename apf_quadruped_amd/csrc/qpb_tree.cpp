@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <numeric>
 #include <sstream>
@@ -96,36 +97,32 @@ void pack_level(std::vector<Task> &tasks, int wg, uint64_t dummy, Prog &P) {
     }
 }
 
-template <class T, class F>
-void table(std::ostringstream &o, const char *type, const char *name, long cnt, F f) {
-    o << "__constant__ " << type << " " << name << "[" << (cnt > 0 ? cnt : 1) << "] = {";
-    if (cnt <= 0) o << "0";
-    for (long k = 0; k < cnt; k++) {
-        o << (k ? "," : "") << (T)f(k);
-        if (k % 16 == 15) o << "\n";
+// Plan-wide tables of the tree kernel, one device buffer: every program's
+// descriptors (u64) first, then the int tables (permutation, assembly sources,
+// program steps and output codes).  The source receives their offsets.
+struct Blob {
+    std::vector<uint64_t> d;
+    std::vector<int32_t> i;
+    std::ostringstream macros;
+    void ints(const char *name, const std::vector<int32_t> &v) {
+        macros << "#define QPB_I_" << name << " " << i.size() << "\n";
+        i.insert(i.end(), v.begin(), v.end());
     }
-    o << "};\n";
-}
-
-void emit_prog(std::ostringstream &o, const char *name, const Prog &P) {
-    o << "#define QPB_" << name << "_NSTEPS " << P.nsteps() << "\n";
-    std::string s = std::string("qpb_") + name;
-    table<long>(o, "int", (s + "_steps").c_str(), (long)P.steps.size(), [&](long k) { return P.steps[k]; });
-    table<long>(o, "int", (s + "_hdr").c_str(), (long)P.hdr.size(), [&](long k) { return P.hdr[k]; });
-    o << "__constant__ unsigned long long " << s << "_desc[" << std::max<size_t>(P.desc.size(), 1) << "] = {";
-    if (P.desc.empty()) o << "0";
-    for (size_t k = 0; k < P.desc.size(); k++) {
-        o << (k ? "," : "") << P.desc[k] << "ull";
-        if (k % 12 == 11) o << "\n";
+    void prog(const char *name, const Prog &P) {
+        macros << "#define QPB_" << name << "_NSTEPS " << P.nsteps() << "\n";
+        macros << "#define QPB_D_" << name << " " << d.size() << "\n";
+        d.insert(d.end(), P.desc.begin(), P.desc.end());
+        ints((std::string(name) + "_steps").c_str(), P.steps);
+        ints((std::string(name) + "_hdr").c_str(), P.hdr);
     }
-    o << "};\n";
-}
+};
 
 long lds_doubles(const Plan &pl) {
     const long n = pl.n, m = pl.m, p = pl.p, N = pl.N;
     const long npag = pl.Pin.nnz() + (p ? pl.A.nnz() : 0) + pl.G.nnz();
     // qpb_tree.hip LDS layout: PAG+1, LD+1, rD, V, S, R, W, C, H, B, DS, LAM, DZ, DSL, XP, RED
-    return (npag + 1) + (pl.lnz + 1) + 4 * N + m + n + m + std::max(p, 1L) + 4 * m + n + 64;
+    // (+ the program step tables, <= 2 ints per level and program: bounded by 10 N + 16 ints)
+    return (npag + 1) + (pl.lnz + 1) + 4 * N + m + n + m + std::max(p, 1L) + 4 * m + n + 64 + (10 * N + 16) / 2;
 }
 
 // position of row i in column k of L (Li ascends within a column), -1 if absent
@@ -153,7 +150,8 @@ bool tree_eligible(const Plan &pl, std::string *why) {
     return true;
 }
 
-std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, TreeStats *stats) {
+std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, TreeStats *stats,
+                                 std::vector<char> *tables) {
     const long n = pl.n, m = pl.m, p = pl.p, N = pl.N, lnz = pl.lnz;
     const long nP = pl.Pin.nnz(), nA = p ? pl.A.nnz() : 0, nG = pl.G.nnz(), npag = nP + nA + nG;
     std::ostringstream o;
@@ -262,14 +260,29 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
             asrc_l[tgt] = code(pl.K_loop[s]);
         }
     }
-    table<long>(o, "int", "qpb_pinv", N, [&](long k) { return pl.pinv[k]; });
-    table<long>(o, "int", "qpb_asrc_i", lnz + N, [&](long k) { return asrc_i[k]; });
-    table<long>(o, "int", "qpb_asrc_l", lnz + N, [&](long k) { return asrc_l[k]; });
-    emit_prog(o, "fac", fac);
-    emit_prog(o, "fwd", fwd);
-    emit_prog(o, "bwd", bwd);
-    emit_prog(o, "mv", mv);
-    emit_prog(o, "obj", obj);
+    Blob bl;
+    bl.prog("fac", fac);
+    bl.prog("fwd", fwd);
+    bl.prog("bwd", bwd);
+    bl.prog("mv", mv);
+    bl.prog("obj", obj);
+    bl.ints("pinv", std::vector<int32_t>(pl.pinv.begin(), pl.pinv.end()));
+    bl.ints("asrc_i", asrc_i);
+    bl.ints("asrc_l", asrc_l);
+    o << bl.macros.str() << "#define QPB_NDESC " << bl.d.size() << "\n";
+    // the tables' content is part of the kernel's identity (code-object cache key)
+    {
+        std::string raw((const char *)bl.d.data(), bl.d.size() * 8);
+        raw.append((const char *)bl.i.data(), bl.i.size() * 4);
+        char hx[40];
+        snprintf(hx, sizeof hx, "%016llx", (unsigned long long)fnv1a(raw));
+        o << "// tables " << hx << "\n";
+    }
+    if (tables) {
+        tables->resize(bl.d.size() * 8 + bl.i.size() * 4);
+        std::memcpy(tables->data(), bl.d.data(), bl.d.size() * 8);
+        std::memcpy(tables->data() + bl.d.size() * 8, bl.i.data(), bl.i.size() * 4);
+    }
     if (stats) {
         stats->levels = H;
         stats->fac_steps = fac.nsteps(); stats->fwd_steps = fwd.nsteps();

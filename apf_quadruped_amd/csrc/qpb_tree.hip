@@ -9,8 +9,8 @@
 // program tables, and to write the outputs.
 //
 // A program step: lane l < ntask*G works on task l/G and sums that task's terms
-// l%G, l%G+G, ...; a butterfly over the G lanes completes the sum; the task's
-// first lane applies the epilogue.  A workgroup barrier closes each level.
+// l%G, l%G+G, ...; a DPP butterfly over the G lanes completes the sum; the
+// task's last lane applies the epilogue.  A workgroup barrier closes each level.
 //
 // Reference: qpSWIFT's Mehrotra predictor-corrector (qpSWIFT.c:473-644,
 // kkt_initialize Auxilary.c:992-1089), LDL' with dynamic regularisation
@@ -28,6 +28,7 @@ struct qpb_args {
     long B;
     double tol, abstol, sigma_d;
     long maxit;
+    const void *tab;        // plan tables (qpb_tree.cpp Blob): u64 descriptors, then int32 tables
 };
 
 #define NX QPB_NX
@@ -57,6 +58,13 @@ struct qpb_args {
 #define O_XP (O_DSL + NZ)              // x at the start of the iteration (objective at maxit)
 #define O_RED (O_XP + NX)              // reduction scratch [NW][8]
 #define LDS_QP (O_RED + 64)
+// step tables of the five programs (ints, in LDS)
+#define QPB_MS_FAC 0
+#define QPB_MS_FWD (QPB_MS_FAC + 4 * QPB_fac_NSTEPS)
+#define QPB_MS_BWD (QPB_MS_FWD + 4 * QPB_fwd_NSTEPS)
+#define QPB_MS_MV (QPB_MS_BWD + 4 * QPB_bwd_NSTEPS)
+#define QPB_MS_OBJ (QPB_MS_MV + 4 * QPB_mv_NSTEPS)
+#define QPB_MS_TOTAL (QPB_MS_OBJ + 4 * QPB_obj_NSTEPS + 4)
 
 static __device__ __forceinline__ double qpb_rcp(double v) {
     double r = __builtin_amdgcn_rcp(v);
@@ -76,33 +84,138 @@ static __device__ __forceinline__ double qpb_rcp_reg(double d) {
 static __device__ __forceinline__ unsigned long long qpb_f0(unsigned long long d) { return d & 0x1FFFFFull; }
 static __device__ __forceinline__ unsigned long long qpb_f1(unsigned long long d) { return (d >> 21) & 0x1FFFFFull; }
 static __device__ __forceinline__ unsigned long long qpb_f2(unsigned long long d) { return d >> 42; }
+// dummy descriptors (terms that read the zero entries LD[LNZ] / PAG[NPAG])
+#define QPB_DUMMY_FAC ((unsigned long long)LNZ | ((unsigned long long)LNZ << 21))
+#define QPB_DUMMY_SOLVE ((unsigned long long)LNZ)
+#define QPB_DUMMY_MV ((unsigned long long)NPAG)
 
-// Run one gather program.  term(acc, desc) -> acc; epi(out_code, acc).
-template <class Term, class Epi>
-static __device__ __forceinline__ void qpb_run(const int *__restrict__ steps, int nsteps,
-                                               const int *__restrict__ hdr,
-                                               const unsigned long long *__restrict__ desc, Term term, Epi epi) {
+// DPP move with a row mask (rows outside it read 0)
+template <int CTRL, int RM = 0xf> static __device__ __forceinline__ double qpb_dpp(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, CTRL, RM, 0xf, false);
+}
+// sum over aligned groups of 2^g lanes (g uniform, 0..6), all DPP: butterflies
+// inside a row (quad_perm, row_half_mirror, row_mirror) leave the group sum in
+// every lane of a <= 16-lane group; row_bcast15 / row_bcast31 then fold rows
+// upwards, so the LAST lane of every group holds its sum
+static __device__ __forceinline__ double qpb_gsum(double v, int g) {
+    if (g >= 1) v += qpb_dpp<0xB1>(v);          // quad_perm [1,0,3,2]
+    if (g >= 2) v += qpb_dpp<0x4E>(v);          // quad_perm [2,3,0,1]
+    if (g >= 3) v += qpb_dpp<0x141>(v);         // row_half_mirror
+    if (g >= 4) v += qpb_dpp<0x140>(v);         // row_mirror
+    if (g >= 5) v += qpb_dpp<0x142, 0xA>(v);    // row_bcast15 into rows 1, 3
+    if (g >= 6) v += qpb_dpp<0x143, 0xC>(v);    // row_bcast31 into rows 2, 3
+    return v;
+}
+// as qpb_gsum, called by the active lanes only: every group is fully active,
+// and no butterfly stage reads across a group boundary
+static __device__ __forceinline__ double qpb_gsum_act(double v, int g) { return qpb_gsum(v, g); }
+static __device__ __forceinline__ double qpb_wmin(double v) {
+    v = __builtin_fmin(v, qpb_dpp<0xB1>(v));
+    v = __builtin_fmin(v, qpb_dpp<0x4E>(v));
+    v = __builtin_fmin(v, qpb_dpp<0x141>(v));
+    v = __builtin_fmin(v, qpb_dpp<0x140>(v));
+    const double u = __builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xf, false);
+    v = __builtin_fmin(v, u);
+    const double w = __builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xf, false);
+    return __builtin_fmin(v, w);                // lane 63 holds the wave minimum
+}
+
+#ifndef QPB_T_TIMING
+#define QPB_T_TIMING 0  // 1: per-phase cycle counts (s_memtime) into stats instead of the residual norms
+#endif
+#if QPB_T_TIMING
+#define QPB_TIC() const long qpb_t0 = (long)__builtin_readcyclecounter()
+#define QPB_TOC(v) (v) += (double)((long)__builtin_readcyclecounter() - qpb_t0)
+#else
+#define QPB_TIC()
+#define QPB_TOC(v)
+#endif
+
+#ifndef QPB_T_EXP
+#define QPB_T_EXP 0     // timing experiments only (wrong results): 1 no table loads, 2 no barriers
+#endif
+#ifndef QPB_T_PF
+#define QPB_T_PF 8      // descriptor rounds prefetched per step
+#endif
+
+// Workgroup barrier that waits for LDS traffic only: descriptor prefetches
+// (global loads of plan constants) stay in flight across it.  The "memory"
+// clobber keeps the compiler from moving LDS accesses across.
+static __device__ __forceinline__ void qpb_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Run one gather program.  ms: the program's step table, staged in LDS (4 ints
+// per step).  term(acc, desc) -> acc; pre(code) -> the epilogue's own operands
+// (loaded before the terms are summed); post(code, acc, pre) writes the result.
+// Descriptors, output codes and step metadata are prefetched two steps ahead
+// into two register sets (A for even, B for odd steps; the loop is unrolled by
+// two so neither is copied).  Every prefetch load is unconditional (inactive
+// lanes and steps past the end read entry 0) so the compiler can wait with
+// vmcnt(N) instead of vmcnt(0); descriptor slots past a step's round count hold
+// the program's dummy (a term that reads zeros), so the terms of a step are
+// summed without branches in one of four widths and their LDS reads issue
+// back to back.
+struct qpb_pre { double a, b; };
+template <class Term, class Pre, class Post>
+static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const int *__restrict__ hdr,
+                                               const unsigned long long *__restrict__ desc,
+                                               unsigned long long dummy, Term term, Pre pre, Post post) {
+    if (nsteps <= 0) return;
     const int l = threadIdx.x;
-    for (int st = 0; st < nsteps; st++) {
-        const int doff = steps[4 * st], toff = steps[4 * st + 1], ntg = steps[4 * st + 2], rb = steps[4 * st + 3];
-        const int g = ntg & 15, act = (ntg >> 4) << g, R = rb & 0xffff;
+    struct Set { unsigned long long d[QPB_T_PF]; int h, doff, ntg, rb; };
+    Set A, B;
+    auto prefetch = [&](int st, Set &S) {
+        st = st < nsteps ? st : nsteps - 1;
+        S.doff = ms[4 * st]; const int toff = ms[4 * st + 1]; S.ntg = ms[4 * st + 2]; S.rb = ms[4 * st + 3];
+        const int g = S.ntg & 15, act = (S.ntg >> 4) << g, R = S.rb & 0xffff;
+        const bool on = l < act;
+#pragma unroll
+        for (int r = 0; r < QPB_T_PF; r++) {
+#if QPB_T_EXP == 1
+            const unsigned long long v = dummy + (unsigned long long)(toff & 0);
+#else
+            const unsigned long long v = desc[(on && r < R) ? S.doff + r * act + l : 0];
+#endif
+            S.d[r] = r < R ? v : dummy;
+        }
+#if QPB_T_EXP == 1
+        S.h = (l >> g) & 1;
+#else
+        S.h = hdr[on ? toff + (l >> g) : 0];
+#endif
+    };
+    auto step = [&](const Set &S) {
+        const int g = S.ntg & 15, act = (S.ntg >> 4) << g, R = S.rb & 0xffff;
         double acc = 0.0;
         if (l < act) {
-            const unsigned long long *d = desc + doff + l;
-            int r = 0;
-            for (; r + 4 <= R; r += 4) {
-                const unsigned long long d0 = d[(r + 0) * act], d1 = d[(r + 1) * act], d2 = d[(r + 2) * act],
-                                         d3 = d[(r + 3) * act];
-                acc = term(acc, d0);
-                acc = term(acc, d1);
-                acc = term(acc, d2);
-                acc = term(acc, d3);
+            const qpb_pre e = pre(S.h);
+            if (R <= 1) {
+                acc = term(acc, S.d[0]);
+            } else if (R <= 2) {
+                acc = term(term(acc, S.d[0]), S.d[1]);
+            } else if (R <= 4) {
+                double u = term(term(0.0, S.d[0]), S.d[1]), v = term(term(0.0, S.d[2]), S.d[3]);
+                acc = u + v;
+            } else {
+                double u = 0.0, v = 0.0;
+#pragma unroll
+                for (int r = 0; r < QPB_T_PF; r += 2) { u = term(u, S.d[r]); v = term(v, S.d[r + 1]); }
+                for (int r = QPB_T_PF; r < R; r++) u = term(u, desc[S.doff + r * act + l]);   // rare
+                acc = u + v;
             }
-            for (; r < R; r++) acc = term(acc, d[r * act]);
+            acc = qpb_gsum_act(acc, g);
+            if ((l & ((1 << g) - 1)) == (1 << g) - 1) post(S.h, acc, e);
         }
-        for (int o = 1; o < (1 << g); o <<= 1) acc += __shfl_xor(acc, o, 64);
-        if (l < act && (l & ((1 << g) - 1)) == 0) epi(hdr[toff + (l >> g)], acc);
-        if (rb >> 16) __syncthreads();
+#if QPB_T_EXP != 2
+        if (S.rb >> 16) qpb_bar();
+#endif
+    };
+    prefetch(0, A);
+    prefetch(1, B);
+    for (int st = 0; st < nsteps; st += 2) {
+        step(A);
+        prefetch(st + 2, A);
+        if (st + 1 < nsteps) step(B);
+        prefetch(st + 3, B);
     }
 }
 
@@ -110,10 +223,9 @@ static __device__ __forceinline__ void qpb_run(const int *__restrict__ steps, in
 template <int K>
 static __device__ __forceinline__ void qpb_bsum(double (&v)[K], double *red) {
 #pragma unroll
-    for (int k = 0; k < K; k++)
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+    for (int k = 0; k < K; k++) v[k] = qpb_gsum(v[k], 6);
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0)
+    if ((threadIdx.x & 63) == 63)
 #pragma unroll
         for (int k = 0; k < K; k++) red[w * 8 + k] = v[k];
     __syncthreads();
@@ -127,10 +239,9 @@ static __device__ __forceinline__ void qpb_bsum(double (&v)[K], double *red) {
 template <int K>
 static __device__ __forceinline__ void qpb_bmin(double (&v)[K], double *red) {
 #pragma unroll
-    for (int k = 0; k < K; k++)
-        for (int o = 32; o > 0; o >>= 1) v[k] = __builtin_fmin(v[k], __shfl_xor(v[k], o, 64));
+    for (int k = 0; k < K; k++) v[k] = qpb_wmin(v[k]);
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0)
+    if ((threadIdx.x & 63) == 63)
 #pragma unroll
         for (int k = 0; k < K; k++) red[w * 8 + k] = v[k];
     __syncthreads();
@@ -144,11 +255,19 @@ static __device__ __forceinline__ void qpb_bmin(double (&v)[K], double *red) {
 
 extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double L[LDS_QP];
+    __shared__ __attribute__((aligned(16))) int MS[QPB_MS_TOTAL];      // program step tables
     const int t = threadIdx.x;
     const long q = blockIdx.x;
     if (q >= a.B) return;                        // workgroup-uniform
     const long tile = q >> 6;
     const int ql = (int)(q & 63);
+    double tm_fac = 0.0, tm_sol = 0.0, tm_mv = 0.0, tm_all = 0.0;
+    (void)tm_fac; (void)tm_sol; (void)tm_mv; (void)tm_all;
+    const unsigned long long *__restrict__ TD = (const unsigned long long *)a.tab;
+    const int *__restrict__ TI = (const int *)(TD + QPB_NDESC);
+#define qpb_pinv (TI + QPB_I_pinv)
+#define qpb_asrc_i (TI + QPB_I_asrc_i)
+#define qpb_asrc_l (TI + QPB_I_asrc_l)
     double *__restrict__ PAG = L + O_PAG;
     double *__restrict__ LD = L + O_LD;
     double *__restrict__ rD = L + O_RD;
@@ -178,6 +297,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     for (int j = t; j < NY; j += QPB_WG) Bv[j] = a.b[tile * (NY * 64) + j * 64 + ql];
 #endif
     if (t == 0) { PAG[NPAG] = 0.0; LD[LNZ] = 0.0; }
+    for (int j = t; j < 4 * QPB_fac_NSTEPS; j += QPB_WG) MS[QPB_MS_FAC + j] = TI[QPB_I_fac_steps + j];
+    for (int j = t; j < 4 * QPB_fwd_NSTEPS; j += QPB_WG) MS[QPB_MS_FWD + j] = TI[QPB_I_fwd_steps + j];
+    for (int j = t; j < 4 * QPB_bwd_NSTEPS; j += QPB_WG) MS[QPB_MS_BWD + j] = TI[QPB_I_bwd_steps + j];
+    for (int j = t; j < 4 * QPB_mv_NSTEPS; j += QPB_WG) MS[QPB_MS_MV + j] = TI[QPB_I_mv_steps + j];
+    for (int j = t; j < 4 * QPB_obj_NSTEPS; j += QPB_WG) MS[QPB_MS_OBJ + j] = TI[QPB_I_obj_steps + j];
     __syncthreads();
 
     // KKT values into the factor layout (init: z diagonal -1; loop: -s/z)
@@ -194,32 +318,45 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
         __syncthreads();
     };
     auto factor = [&]() {
-        qpb_run(qpb_fac_steps, QPB_fac_NSTEPS, qpb_fac_hdr, qpb_fac_desc,
+        QPB_TIC();
+        qpb_run(MS + QPB_MS_FAC, QPB_fac_NSTEPS, TI + QPB_I_fac_hdr, TD + QPB_D_fac, QPB_DUMMY_FAC,
                 [&](double acc, unsigned long long d) {
                     return __builtin_fma(-LD[qpb_f0(d)] * rD[qpb_f2(d)], LD[qpb_f1(d)], acc);
                 },
-                [&](int out, double acc) {
-                    if (out >= 0) LD[out] += acc;
-                    else { const int j = -1 - out; rD[j] = qpb_rcp_reg(rD[j] + acc); }
+                [&](int out) { return qpb_pre{out >= 0 ? LD[out] : rD[-1 - out], 0.0}; },
+                [&](int out, double acc, qpb_pre e) {
+                    if (out >= 0) LD[out] = e.a + acc;
+                    else rD[-1 - out] = qpb_rcp_reg(e.a + acc);
                 });
+        QPB_TOC(tm_fac);
     };
     // W (permuted rhs) -> W (permuted solution)
     auto solve = [&]() {
-        qpb_run(qpb_fwd_steps, QPB_fwd_NSTEPS, qpb_fwd_hdr, qpb_fwd_desc,
+        QPB_TIC();
+        qpb_run(MS + QPB_MS_FWD, QPB_fwd_NSTEPS, TI + QPB_I_fwd_hdr, TD + QPB_D_fwd, QPB_DUMMY_SOLVE,
                 [&](double acc, unsigned long long d) { return __builtin_fma(-LD[qpb_f0(d)], W[qpb_f1(d)], acc); },
-                [&](int i, double acc) { W[i] = rD[i] * (W[i] + acc); });
-        qpb_run(qpb_bwd_steps, QPB_bwd_NSTEPS, qpb_bwd_hdr, qpb_bwd_desc,
+                [&](int i) { return qpb_pre{W[i], rD[i]}; },
+                [&](int i, double acc, qpb_pre e) { W[i] = e.b * (e.a + acc); });
+        qpb_run(MS + QPB_MS_BWD, QPB_bwd_NSTEPS, TI + QPB_I_bwd_hdr, TD + QPB_D_bwd, QPB_DUMMY_SOLVE,
                 [&](double acc, unsigned long long d) { return __builtin_fma(-LD[qpb_f0(d)], W[qpb_f1(d)], acc); },
-                [&](int k, double acc) { W[k] = __builtin_fma(rD[k], acc, W[k]); });
+                [&](int k) { return qpb_pre{W[k], rD[k]}; },
+                [&](int k, double acc, qpb_pre e) { W[k] = __builtin_fma(e.b, acc, e.a); });
+        QPB_TOC(tm_sol);
     };
     // R = [P A' G'; A 0 0; G 0 0] V (raw products)
     auto products = [&](const double *__restrict__ vec) {
-        qpb_run(qpb_mv_steps, QPB_mv_NSTEPS, qpb_mv_hdr, qpb_mv_desc,
+        QPB_TIC();
+        qpb_run(MS + QPB_MS_MV, QPB_mv_NSTEPS, TI + QPB_I_mv_hdr, TD + QPB_D_mv, QPB_DUMMY_MV,
                 [&](double acc, unsigned long long d) { return __builtin_fma(PAG[qpb_f0(d)], vec[qpb_f1(d)], acc); },
-                [&](int r, double acc) { R[r] = acc; });
+                [&](int) { return qpb_pre{0.0, 0.0}; },
+                [&](int r, double acc, qpb_pre) { R[r] = acc; });
+        QPB_TOC(tm_mv);
     };
 
     // ---- kkt_initialize (Auxilary.c:992-1089): K with the -I block, rhs [-c; b; h]
+#if QPB_T_TIMING
+    const long qpb_tall = (long)__builtin_readcyclecounter();
+#endif
     assemble(qpb_asrc_i);
     for (int r = t; r < NN; r += QPB_WG)
         W[qpb_pinv[r]] = r < NX ? -Cv[r] : (r < NX + NY ? Bv[r - NX] : Hv[r - NX - NY]);
@@ -374,9 +511,10 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
 
     // ---- objective of the x the last residuals were computed at (qpSWIFT.c:515)
     const double *xo = flag == 0 ? V : XP;
-    qpb_run(qpb_obj_steps, QPB_obj_NSTEPS, qpb_obj_hdr, qpb_obj_desc,
+    qpb_run(MS + QPB_MS_OBJ, QPB_obj_NSTEPS, TI + QPB_I_obj_hdr, TD + QPB_D_obj, QPB_DUMMY_MV,
             [&](double acc, unsigned long long d) { return __builtin_fma(PAG[qpb_f0(d)], xo[qpb_f1(d)], acc); },
-            [&](int r, double acc) { R[r] = acc; });
+            [&](int) { return qpb_pre{0.0, 0.0}; },
+            [&](int r, double acc, qpb_pre) { R[r] = acc; });
     double fv[1] = {0.0};
     for (int r = t; r < NX; r += QPB_WG) fv[0] += xo[r] * (0.5 * R[r] + Cv[r]);
     qpb_bsum(fv, RED);
@@ -396,7 +534,13 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
         a.fval[q] = fv[0];
         if (a.stats) {
             double *st = a.stats + tile * (6 * 64) + ql;
+#if QPB_T_TIMING
+            tm_all = (double)((long)__builtin_readcyclecounter() - qpb_tall);
+            st[0] = tm_fac; st[64] = tm_sol; st[128] = tm_mv; st[192] = tm_all; st[256] = (double)QPB_fac_NSTEPS;
+            st[320] = (double)(QPB_fwd_NSTEPS + QPB_bwd_NSTEPS);
+#else
             st[0] = n_rx; st[64] = n_ry; st[128] = n_rz; st[192] = n_mu; st[256] = alpha_p; st[320] = alpha_d;
+#endif
         }
     }
 }

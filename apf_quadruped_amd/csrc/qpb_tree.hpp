@@ -2,6 +2,7 @@
 #pragma once
 
 #include <string>
+#include <vector>
 
 #include "qpb_plan.hpp"
 
@@ -19,5 +20,8 @@ struct TreeStats {
 bool tree_eligible(const Plan &pl, std::string *why);
 // Threads per workgroup (= per QP): 64, 128 or 256 by KKT size (QPB_TREE_WG overrides).
 int tree_wg_for(const Plan &pl);
-std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, TreeStats *stats = nullptr);
+// Kernel source; `tables` receives the plan-wide table blob the kernel reads
+// through its `tab` argument (u64 descriptors, then int32 tables).
+std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, TreeStats *stats = nullptr,
+                                 std::vector<char> *tables = nullptr);
 }  // namespace qpb

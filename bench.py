@@ -10,10 +10,13 @@ winners are exchanged with one RCCL all_gather (config 5's argmin gather).
 Shards are independent (weak scaling): rank r owns QP ids [r*B, (r+1)*B);
 config 5 (65 536 QPs over 8 GPUs) is `--gpus 8 --batch 8192`.
 
-At this batch size qpb_solve runs the wave-cooperative kernel (one QP per
-wavefront).  Beside the headline, rank 0 of a 1-GPU run also measures a 2^20-QP
-batch (lane kernel, one QP per lane; working set ~2 GB, far above the 256 MB
-Infinity Cache) as `large_batch`, the HBM-scale throughput figure.
+At this batch size qpb_solve runs the row kernel (four QPs per wavefront).
+Beside the headline, rank 0 of a 1-GPU run also measures a 2^20-QP batch
+(working set ~2 GB, far above the 256 MB Infinity Cache) as `large_batch`, the
+HBM-scale throughput figure; configs[2] (4 gait patterns, 4 streams) as
+`mixed_patterns`; and under `shapes` configs[3] (MPC horizon, N = 380, tree
+kernel) and the controller's own 30/68/18 stance QP, each next to the
+reference qpSWIFT on the host cores.
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -45,6 +48,8 @@ def parse():
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave", "wave1", "auto1"])
     ap.add_argument("--no-mixed", dest="mixed", action="store_false",
                     help="skip the configs[2] leg (4 gait patterns x 1024 QPs)")
+    ap.add_argument("--no-shapes", dest="shapes", action="store_false",
+                    help="skip the configs[3] (MPC) and controller-shape legs")
     ap.add_argument("--tol", type=float, default=1e-6)
     ap.add_argument("--exact", action="store_true", help="bench the bit-faithful kernel")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -78,15 +83,17 @@ def flops_per_qp(info, iters):
     return (fac + solve + 2 * info.nnzG) + iters * per_it + resid
 
 
-def cpu_baseline(seed, sample, passes, tol):
-    """Reference qpSWIFT (oracle/_ref) on the host cores; port (oracle) if absent."""
+def cpu_baseline(seed, sample, passes, tol, gen=None, label="C1"):
+    """Reference qpSWIFT (oracle/_ref) on the host cores; port (oracle) if absent.
+    gen(ids) -> dense QP dict (default: C1 contact-force QPs)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from apf_quadruped_amd import workloads as W
     threads = max(1, min(16, os.cpu_count() or 1))
-    d = W.contact_force_qp(seed, np.arange(sample))
+    d = gen(np.arange(sample)) if gen is not None else W.contact_force_qp(seed, np.arange(sample))
+    n, m, p = int(d["n"]), int(d["m"]), int(d["p"])
     P, A, G = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
     c, h, b = (np.ascontiguousarray(d[k]) for k in ("c", "h", "b"))
-    x = np.zeros((sample, 12)); flags = np.zeros(sample, np.int64); iters = np.zeros(sample, np.int64)
+    x = np.zeros((sample, n)); flags = np.zeros(sample, np.int64); iters = np.zeros(sample, np.int64)
     dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
     lp = lambda a: a.ctypes.data_as(C.POINTER(C.c_long))
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_batch.so")
@@ -94,13 +101,13 @@ def cpu_baseline(seed, sample, passes, tol):
         L = C.CDLL(ref_so)
         L.ref_solve_dense_batch.argtypes = [C.c_long] * 4 + [C.POINTER(C.c_double)] * 6 + \
             [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_long), C.POINTER(C.c_long), C.c_int]
-        run = lambda: L.ref_solve_dense_batch(sample, 12, 20, 6, dp(P), dp(A), dp(G), dp(c), dp(h), dp(b),
+        run = lambda: L.ref_solve_dense_batch(sample, n, m, p, dp(P), dp(A), dp(G), dp(c), dp(h), dp(b),
                                               tol, dp(x), lp(flags), lp(iters), threads)
         kind = "reference"
     else:
         from oracle_py import Oracle
         o = Oracle()
-        run = lambda: o.lib.oracle_solve_dense_batch(sample, 12, 20, 6, dp(P), dp(A), dp(G), dp(c), dp(h),
+        run = lambda: o.lib.oracle_solve_dense_batch(sample, n, m, p, dp(P), dp(A), dp(G), dp(c), dp(h),
                                                      dp(b), None, tol, tol, 100, dp(x), lp(flags), lp(iters),
                                                      threads)
         kind = "port"
@@ -110,19 +117,43 @@ def cpu_baseline(seed, sample, passes, tol):
         run()
     dt = time.perf_counter() - t0
     return dict(value=sample * passes / dt, unit="QP solves/s", cores=threads, kind=kind,
-                sample=f"{sample} C1 QPs x {passes} passes, setup+solve per QP (QP_SETUP_dense + QP_SOLVE "
+                sample=f"{sample} {label} QPs x {passes} passes, setup+solve per QP (QP_SETUP_dense + QP_SOLVE "
                        f"+ QP_CLEANUP_dense, AMD ordering), tol {tol:g}, {threads} threads, {dt:.2f} s wall",
                 mean_iters=float(iters.mean()), optimal_frac=float((flags == 0).mean()))
 
 
-def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True):
+def shape_leg(name, gen, B, tol, dev, steps=20, warmup=2, cpu=None):
+    """One non-headline workload on one GPU: B QPs of `gen`'s shape per launch
+    (solve + argmin per step), kernel duration from HIP events, algorithmic-byte
+    roofline, and (cpu = (sample, passes)) the reference on the host cores."""
+    from apf_quadruped_amd.batch import Plan
+    d0 = gen(np.arange(1))
+    plan = Plan.from_dense(d0["n"], d0["m"], d0["p"], d0["P"][0], d0["A"][0], d0["G"][0])
+    plan.compile()
+    el, km, out, _ = run_leg(plan, B, steps, warmup, tol, dev, 0, 1, 0, gather=False, gen=gen)
+    bpq = plan.bytes_per_qp()
+    ach = bpq * B / (km * 1e-3) / 1e9
+    kn = plan.kernel_name(B)
+    res = {"workload": name, "batch": B, "value": B * steps / el, "unit": "QP solves/s",
+           "ms_per_step": el * 1e3 / steps, "kernel": kn, "kernel_ms": km, "kernel_qps": B / (km * 1e-3),
+           "kkt_N": plan.info.N, "nnz_L": plan.info.lnz,
+           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBS, "traffic": traffic_for(kn, B), "bytes_per_qp": bpq},
+           "mean_iters": float(out["iters"].float().mean().item()),
+           "optimal_frac": float((out["flag"] == 0).float().mean().item())}
+    if cpu is not None:
+        res["cpu_baseline"] = cpu_baseline(0, cpu[0], cpu[1], tol, gen=gen, label=name)
+    return res
+
+
+def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, gen=None):
     """Timed loop of `steps` steps (solve + argmin [+ all_gather]) on resident
     inputs.  Returns (wall seconds max over ranks, mean kernel ms max over
     ranks, outputs, gathered winners)."""
     import torch
     import torch.distributed as dist
     from apf_quadruped_amd.shard import shard_range
-    host = make_shard(plan, seed, shard_range(rank, world, B)[0], B)
+    host = make_shard(plan, seed, shard_range(rank, world, B)[0], B, chunk=65536 if gen is None else 1024, gen=gen)
     vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
     del host
     out = plan.alloc_outputs(B, device=dev)
@@ -268,7 +299,7 @@ def main():
     fpq = flops_per_qp(plan.info, mean_it)
     fp64_tf = fpq * B / (kern_ms * 1e-3) / 1e12
 
-    # secondary leg: one large batch per launch (lane kernel), HBM-scale numbers
+    # secondary leg: one large batch per launch (row kernel), HBM-scale numbers
     large = None
     if rank == 0 and world == 1 and args.large_batch > 0:
         BL = args.large_batch
@@ -293,6 +324,19 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(seed, args.cpu_sample, args.cpu_passes, args.tol)
+
+    # configs[3] (MPC horizon, N = 380, tree kernel) and the controller's own
+    # stance QP (30/68/18), each with its CPU reference
+    shapes = None
+    if rank == 0 and world == 1 and args.shapes:
+        from apf_quadruped_amd import workloads as W
+        shapes = [
+            shape_leg("configs[3]: MPC horizon N=10 (120/200/60), batch 1024", lambda ids: W.mpc_qp(plans.SEED + 4, ids),
+                      1024, args.tol, dev, cpu=None if args.no_cpu else (256, 16)),
+            shape_leg("controller stance QP 30/68/18 (main.cpp:1649), batch 1024",
+                      lambda ids: W.controller_qp(plans.SEED + 30, ids), 1024, args.tol, dev,
+                      cpu=None if args.no_cpu else (512, 16)),
+        ]
 
     if rank == 0:
         line = {
@@ -323,6 +367,7 @@ def main():
             "optimal_frac": float((flags == 0).mean()),
             "large_batch": large,
             "mixed_patterns": mixed,
+            "shapes": shapes,
             "cpu_baseline": cpu,
         }
         if world > 1:

@@ -102,6 +102,9 @@ int  qpb_plan_get_perm(const qpb_plan *plan, long *perm /* [N] */);
 long qpb_plan_source(const qpb_plan *plan, char *buf, long cap);
 long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap);
 long qpb_plan_tree_source(const qpb_plan *plan, char *buf, long cap);
+/* The tree kernel's plan tables (uploaded once per device; exposed for tests):
+ * returns their size in bytes, copies at most cap bytes when buf is non-NULL. */
+long qpb_plan_tree_tables(const qpb_plan *plan, void *buf, long cap);
 /* Compile the plan's kernels for gfx950 (hiprtc) or fetch them from the
  * code-object cache; needs no GPU.  qpb_solve calls this implicitly. */
 int  qpb_plan_compile(qpb_plan *plan);

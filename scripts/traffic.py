@@ -8,7 +8,7 @@ byte count is known exactly (2 * FETCH_SIZE == algorithmic input bytes within
 
     python scripts/traffic.py FETCH_CSV WRITE_CSV BATCH [BATCH ...]
 
-The wave kernel (qpb_wave_*, one QP per wavefront) reads its inputs with 8-B
+The wave, row and tree kernels (qpb_wave_*, qpb_row_*, qpb_tree_*) read their inputs with 8-B
 per-lane loads, an access width the guide leaves uncalibrated; its entry is
 recorded with the same formula and marked "calibrated": false.
 """
@@ -21,7 +21,8 @@ from collections import defaultdict
 
 def grid_for(kname, wg, batch):
     """Grid size (threads) of a launch of `batch` QPs."""
-    per_block = wg // 64 if kname.startswith("qpb_wave_") else wg
+    per_block = (wg // 64 if kname.startswith("qpb_wave_") else 4 * (wg // 64) if kname.startswith("qpb_row_")
+                 else 1 if kname.startswith("qpb_tree_") else wg)
     return (batch + per_block - 1) // per_block * wg
 
 
@@ -30,7 +31,7 @@ def per_kernel(path, counter, batch):
     vals = defaultdict(list)
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
-        if r["Counter_Name"] != counter or not (k.startswith("qpb_ipm") or k.startswith("qpb_wave")):
+        if r["Counter_Name"] != counter or not k.startswith(("qpb_ipm", "qpb_wave", "qpb_row", "qpb_tree")):
             continue
         if int(r["Grid_Size"]) != grid_for(k, int(r["Workgroup_Size"]), batch):
             continue
@@ -49,7 +50,7 @@ def main():
             if k in w:
                 data[k] = dict(batch=batch, fetch_kb=f[k], write_kb=w[k],
                                hbm_bytes_per_launch=(2 * f[k] + w[k]) * 1024.0,
-                               calibrated=not k.startswith("qpb_wave_"))
+                               calibrated=k.startswith("qpb_ipm"))
                 print(k, data[k])
     json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
 

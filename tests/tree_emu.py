@@ -15,13 +15,27 @@ FB = 21
 FM = (1 << FB) - 1
 
 
-def parse_tables(src: str) -> dict:
+def parse_tables(src: str, blob: bytes) -> dict:
+    """Sizes and table offsets from the generated source's macros; tables from
+    the plan's table blob (u64 descriptors, then int32 tables)."""
     out = {}
     for m in re.finditer(r"#define (QPB_\w+) (-?\d+)\n", src):
         out[m.group(1)] = int(m.group(2))
-    for m in re.finditer(r"__constant__ (?:int|unsigned long long) (\w+)\[\d+\] = \{([^}]*)\};", src):
-        vals = [int(v.strip().rstrip("ul")) for v in m.group(2).replace("\n", "").split(",") if v.strip()]
-        out[m.group(1)] = np.array(vals, dtype=np.int64 if "desc" not in m.group(1) else np.uint64)
+    nd = out["QPB_NDESC"]
+    D = np.frombuffer(blob[:8 * nd], dtype=np.uint64)
+    I = np.frombuffer(blob[8 * nd:], dtype=np.int32).astype(np.int64)
+    names = ["fac", "fwd", "bwd", "mv", "obj"]
+    for k, name in enumerate(names):
+        ns = out[f"QPB_{name}_NSTEPS"]
+        d0 = out[f"QPB_D_{name}"]
+        d1 = out[f"QPB_D_{names[k + 1]}"] if k + 1 < len(names) else nd
+        out[f"qpb_{name}_desc"] = D[d0:d1]
+        s0 = out[f"QPB_I_{name}_steps"]
+        out[f"qpb_{name}_steps"] = I[s0:s0 + 4 * ns]
+        h0 = out[f"QPB_I_{name}_hdr"]
+        out[f"qpb_{name}_hdr"] = I[h0:]
+    for name in ("pinv", "asrc_i", "asrc_l"):
+        out[f"qpb_{name}"] = I[out[f"QPB_I_{name}"]:]
     return out
 
 
@@ -52,7 +66,7 @@ class TreeEmu:
     def __init__(self, plan):
         self.plan = plan
         self.src = plan.tree_source()
-        self.T = parse_tables(self.src)
+        self.T = parse_tables(self.src, plan.tree_tables())
         T = self.T
         self.n, self.m, self.p, self.N = T["QPB_NX"], T["QPB_NZ"], T["QPB_NY"], T["QPB_N"]
         self.lnz, self.wg = T["QPB_LNZ"], T["QPB_WG"]
