@@ -148,11 +148,20 @@ static __device__ __forceinline__ void qpb_wsync() {
 
 static __device__ __forceinline__ bool qpb_any(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
 
+// XCD-aware block order: blocks b and b + 8 share an XCD (and its L2), so
+// logical block (b % 8) * (nb / 8) + b / 8 gives each XCD a contiguous run of
+// QPs -- the 64 QPs of a tile, whose values share cache lines, stay on one L2.
+// The host pads the grid to a multiple of 8 (surplus blocks find no QPs).
+static __device__ __forceinline__ long qpb_xcd_block() {
+    const unsigned b = blockIdx.x, nb = gridDim.x;
+    return (nb & 7) ? (long)b : (long)(b & 7) * (nb >> 3) + (b >> 3);
+}
+
 extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * 4 * LDS_ROW];
     const int lane = threadIdx.x & 63, row = lane >> 4, c = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long q0 = ((long)blockIdx.x * WPB + wv) * 4;
+    const long q0 = (qpb_xcd_block() * WPB + wv) * 4;
     if (q0 >= a.B) return;                     // wave-uniform
 #if QPB_R_TIMING == 2
     const double t_rt0 = (double)__builtin_amdgcn_s_memrealtime(), t_cy0 = (double)__builtin_readcyclecounter();

@@ -451,7 +451,8 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     void *params[] = {&a};
     const unsigned wg = (unsigned)(wave ? plan->wave_wg : tree ? plan->tree_wg : plan->gen.wg);
     const long per_block = wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup
-    const unsigned grid = (unsigned)((B + per_block - 1) / per_block);
+    unsigned grid = (unsigned)((B + per_block - 1) / per_block);
+    if (wave || tree) grid = (grid + 7) & ~7u;      // XCD-aware block order (qpb_xcd_block)
     hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, wg, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("launch: ") + hipGetErrorString(e));
     // an in-kernel "last wave reduces" argmin was measured slower than this

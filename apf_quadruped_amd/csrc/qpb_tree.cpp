@@ -40,10 +40,15 @@ const char *kTreeTemplate =
 #include "qpb_tree_src.inc"
     ;
 
-constexpr int FB = 21;                       // descriptor field width (bits)
-constexpr long FMAX = (1L << FB) - 1;
+// descriptor fields: LDS byte offsets (element index * 8) from the region base,
+// 16 bits each -- fac terms [a | b | k] in a u64, all other programs [a | j] in a u32
+constexpr int FB = 16;
+constexpr long FMAX = ((1L << FB) - 1) / 8;   // largest element index a field can address
 
-uint64_t pk(uint64_t a, uint64_t b, uint64_t c = 0) { return a | (b << FB) | (c << (2 * FB)); }
+uint64_t pk(uint64_t a, uint64_t b, uint64_t c = 0) { return (a * 8) | ((b * 8) << FB) | ((c * 8) << (2 * FB)); }
+
+// rounds of a step, padded to the widths the kernel sums without branches
+long round_bucket(long R) { return R <= 1 ? 1 : R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : R; }
 
 struct Task {
     int32_t out;
@@ -70,8 +75,8 @@ void pack_level(std::vector<Task> &tasks, int wg, uint64_t dummy, Prog &P) {
         const long G = 1L << g, per = wg >> g;
         double cost = 0;
         for (size_t s = 0; s < tasks.size(); s += per) {
-            const long R = ((long)tasks[s].con.size() + G - 1) / G;
-            cost += 4.0 * R + 3.0 * g + 8.0;
+            const long R = round_bucket(((long)tasks[s].con.size() + G - 1) / G);
+            cost += 3.0 * R + 3.0 * g + 30.0;
         }
         if (cost < best_cost - 1e-9) { best_cost = cost; best_g = g; }
     }
@@ -80,7 +85,7 @@ void pack_level(std::vector<Task> &tasks, int wg, uint64_t dummy, Prog &P) {
     for (size_t s = 0; s < tasks.size(); s += per) {
         const size_t e = std::min(tasks.size(), s + (size_t)per);
         const long nt = (long)(e - s), act = nt * G;
-        const long R = ((long)tasks[s].con.size() + G - 1) / G;
+        const long R = round_bucket(((long)tasks[s].con.size() + G - 1) / G);
         const long doff = (long)P.desc.size(), toff = (long)P.hdr.size();
         P.desc.resize(P.desc.size() + (size_t)(R * act), dummy);
         for (size_t t = s; t < e; t++) {
@@ -101,19 +106,33 @@ void pack_level(std::vector<Task> &tasks, int wg, uint64_t dummy, Prog &P) {
 // descriptors (u64) first, then the int tables (permutation, assembly sources,
 // program steps and output codes).  The source receives their offsets.
 struct Blob {
-    std::vector<uint64_t> d;
+    std::vector<uint64_t> d;     // fac descriptors
+    std::vector<uint32_t> d32;   // fwd / bwd / mv / obj descriptors
     std::vector<int32_t> i;
     std::ostringstream macros;
+    int wg = 64;
     void ints(const char *name, const std::vector<int32_t> &v) {
         macros << "#define QPB_I_" << name << " " << i.size() << "\n";
         i.insert(i.end(), v.begin(), v.end());
     }
-    void prog(const char *name, const Prog &P) {
+    // lanes past a step's active count and rounds past its count read (and
+    // ignore) entries beyond the program's end: wg entries of padding keep
+    // those reads inside the buffer
+    void prog(const char *name, const Prog &P, bool wide) {
         macros << "#define QPB_" << name << "_NSTEPS " << P.nsteps() << "\n";
-        macros << "#define QPB_D_" << name << " " << d.size() << "\n";
-        d.insert(d.end(), P.desc.begin(), P.desc.end());
+        if (wide) {
+            macros << "#define QPB_D_" << name << " " << d.size() << "\n";
+            d.insert(d.end(), P.desc.begin(), P.desc.end());
+            d.insert(d.end(), (size_t)wg, 0ull);
+        } else {
+            macros << "#define QPB_D_" << name << " " << d32.size() << "\n";
+            for (uint64_t v : P.desc) d32.push_back((uint32_t)v);
+            d32.insert(d32.end(), (size_t)wg, 0u);
+        }
         ints((std::string(name) + "_steps").c_str(), P.steps);
-        ints((std::string(name) + "_hdr").c_str(), P.hdr);
+        std::vector<int32_t> h = P.hdr;
+        h.insert(h.end(), (size_t)wg, 0);
+        ints((std::string(name) + "_hdr").c_str(), h);
     }
 };
 
@@ -144,7 +163,8 @@ int tree_wg_for(const Plan &pl) {
 bool tree_eligible(const Plan &pl, std::string *why) {
     auto no = [&](const char *m) { if (why) *why = m; return false; };
     const long npag = pl.Pin.nnz() + (pl.p ? pl.A.nnz() : 0) + pl.G.nnz();
-    if (pl.lnz + 1 > FMAX || pl.N > FMAX || npag + 1 > FMAX) return no("factor or value count beyond 2^21");
+    if (pl.lnz + 1 > FMAX || pl.N > FMAX || npag + 1 > FMAX)
+        return no("factor, KKT or value count beyond the 16-bit LDS offsets of the descriptors (8191)");
     if (lds_doubles(pl) * 8 > 160 * 1024) return no("per-QP state exceeds the 160 KiB LDS of a CU");
     if (why) why->clear();
     return true;
@@ -261,27 +281,32 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
         }
     }
     Blob bl;
-    bl.prog("fac", fac);
-    bl.prog("fwd", fwd);
-    bl.prog("bwd", bwd);
-    bl.prog("mv", mv);
-    bl.prog("obj", obj);
+    bl.wg = wg;
+    bl.prog("fac", fac, true);
+    bl.prog("fwd", fwd, false);
+    bl.prog("bwd", bwd, false);
+    bl.prog("mv", mv, false);
+    bl.prog("obj", obj, false);
     bl.ints("pinv", std::vector<int32_t>(pl.pinv.begin(), pl.pinv.end()));
     bl.ints("asrc_i", asrc_i);
     bl.ints("asrc_l", asrc_l);
-    o << bl.macros.str() << "#define QPB_NDESC " << bl.d.size() << "\n";
+    if (bl.d32.size() % 2) bl.d32.push_back(0u);   // keep the int tables 8-byte aligned
+    o << bl.macros.str() << "#define QPB_NDESC " << bl.d.size() << "\n#define QPB_NDESC32 " << bl.d32.size() << "\n";
     // the tables' content is part of the kernel's identity (code-object cache key)
     {
         std::string raw((const char *)bl.d.data(), bl.d.size() * 8);
+        raw.append((const char *)bl.d32.data(), bl.d32.size() * 4);
         raw.append((const char *)bl.i.data(), bl.i.size() * 4);
         char hx[40];
         snprintf(hx, sizeof hx, "%016llx", (unsigned long long)fnv1a(raw));
         o << "// tables " << hx << "\n";
     }
     if (tables) {
-        tables->resize(bl.d.size() * 8 + bl.i.size() * 4);
-        std::memcpy(tables->data(), bl.d.data(), bl.d.size() * 8);
-        std::memcpy(tables->data() + bl.d.size() * 8, bl.i.data(), bl.i.size() * 4);
+        const size_t n8 = bl.d.size() * 8, n4 = bl.d32.size() * 4, ni = bl.i.size() * 4;
+        tables->assign(n8 + n4 + ni + 64, 0);
+        std::memcpy(tables->data(), bl.d.data(), n8);
+        std::memcpy(tables->data() + n8, bl.d32.data(), n4);
+        std::memcpy(tables->data() + n8 + n4, bl.i.data(), ni);
     }
     if (stats) {
         stats->levels = H;

@@ -81,13 +81,10 @@ static __device__ __forceinline__ double qpb_rcp_reg(double d) {
     return __builtin_fabs(d) <= 1e-14 ? reg : r;
 }
 
-static __device__ __forceinline__ unsigned long long qpb_f0(unsigned long long d) { return d & 0x1FFFFFull; }
-static __device__ __forceinline__ unsigned long long qpb_f1(unsigned long long d) { return (d >> 21) & 0x1FFFFFull; }
-static __device__ __forceinline__ unsigned long long qpb_f2(unsigned long long d) { return d >> 42; }
-// dummy descriptors (terms that read the zero entries LD[LNZ] / PAG[NPAG])
-#define QPB_DUMMY_FAC ((unsigned long long)LNZ | ((unsigned long long)LNZ << 21))
-#define QPB_DUMMY_SOLVE ((unsigned long long)LNZ)
-#define QPB_DUMMY_MV ((unsigned long long)NPAG)
+// descriptor fields: LDS byte offsets from a region base (qpb_tree.cpp pk)
+static __device__ __forceinline__ unsigned qpb_lo16(unsigned w) { return w & 0xffffu; }
+static __device__ __forceinline__ unsigned qpb_hi16(unsigned w) { return w >> 16; }
+#define QPB_AT(region, byteoff) (*(const double *)((const char *)(L + (region)) + (byteoff)))
 
 // DPP move with a row mask (rows outside it read 0)
 template <int CTRL, int RM = 0xf> static __device__ __forceinline__ double qpb_dpp(double v) {
@@ -132,7 +129,8 @@ static __device__ __forceinline__ double qpb_wmin(double v) {
 #endif
 
 #ifndef QPB_T_EXP
-#define QPB_T_EXP 0     // timing experiments only (wrong results): 1 no table loads, 2 no barriers
+#define QPB_T_EXP 0     // timing experiments only (wrong results): 2 no barriers, 3 no terms,
+                        // 4 no group sums, 5 no epilogue
 #endif
 #ifndef QPB_T_PF
 #define QPB_T_PF 8      // descriptor rounds prefetched per step
@@ -144,57 +142,61 @@ static __device__ __forceinline__ double qpb_wmin(double v) {
 static __device__ __forceinline__ void qpb_bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Run one gather program.  ms: the program's step table, staged in LDS (4 ints
-// per step).  term(acc, desc) -> acc; pre(code) -> the epilogue's own operands
-// (loaded before the terms are summed); post(code, acc, pre) writes the result.
+// per step: descriptor offset, output-code offset, ntask << 4 | log2 G, rounds
+// | barrier << 16).  term(acc, desc) -> acc; pre(code) -> the epilogue's own
+// operands (loaded before the terms are summed); post(code, acc, pre) writes the
+// result.  D: descriptor word (u64 for the factor, u32 otherwise).
+//
 // Descriptors, output codes and step metadata are prefetched two steps ahead
 // into two register sets (A for even, B for odd steps; the loop is unrolled by
-// two so neither is copied).  Every prefetch load is unconditional (inactive
-// lanes and steps past the end read entry 0) so the compiler can wait with
-// vmcnt(N) instead of vmcnt(0); descriptor slots past a step's round count hold
-// the program's dummy (a term that reads zeros), so the terms of a step are
-// summed without branches in one of four widths and their LDS reads issue
-// back to back.
+// two so neither is copied).  Every prefetch issues the same loads (rounds past
+// a step's count re-read round 0, lanes past its active count read padding), so
+// the compiler waits with vmcnt(N) for the set a step consumes instead of
+// vmcnt(0); the step metadata is uniform (readfirstlane) so each load is an
+// SGPR base + the lane's offset.  Round counts are padded to 1, 2, 4 or 8 with
+// dummy terms (they read the zero entries), so a step sums its terms without
+// branches and their LDS reads issue back to back.
 struct qpb_pre { double a, b; };
-template <class Term, class Pre, class Post>
+template <class D> struct qpb_set { D d[QPB_T_PF]; int h, doff, ntg, rb; };
+template <class D, class Term, class Pre, class Post>
 static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const int *__restrict__ hdr,
-                                               const unsigned long long *__restrict__ desc,
-                                               unsigned long long dummy, Term term, Pre pre, Post post) {
+                                               const D *__restrict__ desc, Term term, Pre pre, Post post) {
     if (nsteps <= 0) return;
     const int l = threadIdx.x;
-    struct Set { unsigned long long d[QPB_T_PF]; int h, doff, ntg, rb; };
-    Set A, B;
-    auto prefetch = [&](int st, Set &S) {
+    qpb_set<D> A, B;
+    auto prefetch = [&](int st, qpb_set<D> &S) {
         st = st < nsteps ? st : nsteps - 1;
-        S.doff = ms[4 * st]; const int toff = ms[4 * st + 1]; S.ntg = ms[4 * st + 2]; S.rb = ms[4 * st + 3];
+        const int4 m = *(const int4 *)(ms + 4 * st);
+        S.doff = __builtin_amdgcn_readfirstlane(m.x);
+        const int toff = __builtin_amdgcn_readfirstlane(m.y);
+        S.ntg = __builtin_amdgcn_readfirstlane(m.z);
+        S.rb = __builtin_amdgcn_readfirstlane(m.w);
         const int g = S.ntg & 15, act = (S.ntg >> 4) << g, R = S.rb & 0xffff;
-        const bool on = l < act;
+        const D *base = desc + S.doff;
 #pragma unroll
-        for (int r = 0; r < QPB_T_PF; r++) {
-#if QPB_T_EXP == 1
-            const unsigned long long v = dummy + (unsigned long long)(toff & 0);
-#else
-            const unsigned long long v = desc[(on && r < R) ? S.doff + r * act + l : 0];
-#endif
-            S.d[r] = r < R ? v : dummy;
-        }
-#if QPB_T_EXP == 1
-        S.h = (l >> g) & 1;
-#else
-        S.h = hdr[on ? toff + (l >> g) : 0];
-#endif
+        for (int r = 0; r < QPB_T_PF; r++) S.d[r] = base[(r < R ? r : 0) * act + l];
+        S.h = hdr[toff + (l >> g)];
     };
-    auto step = [&](const Set &S) {
+    auto step = [&](const qpb_set<D> &S) {
         const int g = S.ntg & 15, act = (S.ntg >> 4) << g, R = S.rb & 0xffff;
-        double acc = 0.0;
         if (l < act) {
+#if QPB_T_EXP == 5
+            const qpb_pre e{0.0, 1.0};
+#else
             const qpb_pre e = pre(S.h);
-            if (R <= 1) {
-                acc = term(acc, S.d[0]);
-            } else if (R <= 2) {
-                acc = term(term(acc, S.d[0]), S.d[1]);
-            } else if (R <= 4) {
-                double u = term(term(0.0, S.d[0]), S.d[1]), v = term(term(0.0, S.d[2]), S.d[3]);
-                acc = u + v;
+#endif
+            double acc;
+#if QPB_T_EXP == 3
+            if (true) {
+                acc = 0.0;
+            } else
+#endif
+            if (R == 1) {
+                acc = term(0.0, S.d[0]);
+            } else if (R == 2) {
+                acc = term(term(0.0, S.d[0]), S.d[1]);
+            } else if (R == 4) {
+                acc = term(term(0.0, S.d[0]), S.d[1]) + term(term(0.0, S.d[2]), S.d[3]);
             } else {
                 double u = 0.0, v = 0.0;
 #pragma unroll
@@ -202,9 +204,21 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
                 for (int r = QPB_T_PF; r < R; r++) u = term(u, desc[S.doff + r * act + l]);   // rare
                 acc = u + v;
             }
-            acc = qpb_gsum_act(acc, g);
+#if QPB_T_EXP != 4
+            acc = qpb_gsum(acc, g);
+#endif
+#if QPB_T_EXP != 5
             if ((l & ((1 << g) - 1)) == (1 << g) - 1) post(S.h, acc, e);
+#else
+            asm volatile("" ::"v"(acc), "v"(e.a));
+#endif
         }
+        // a use of every prefetched value on every path: otherwise the compiler
+        // sinks each load into the one branch that reads it, right before its use,
+        // and the prefetch no longer runs ahead
+        static_assert(QPB_T_PF == 8, "qpb_keep lists eight descriptor slots");
+        asm volatile("" ::"v"(S.h), "v"(S.d[0]), "v"(S.d[1]), "v"(S.d[2]), "v"(S.d[3]), "v"(S.d[4]), "v"(S.d[5]),
+                     "v"(S.d[6]), "v"(S.d[7]));
 #if QPB_T_EXP != 2
         if (S.rb >> 16) qpb_bar();
 #endif
@@ -253,18 +267,28 @@ static __device__ __forceinline__ void qpb_bmin(double (&v)[K], double *red) {
     __syncthreads();
 }
 
+// XCD-aware block order: blocks b and b + 8 share an XCD (and its L2), so
+// logical block (b % 8) * (nb / 8) + b / 8 gives each XCD a contiguous run of
+// QPs -- the 64 QPs of a tile, whose values share cache lines, stay on one L2.
+// The host pads the grid to a multiple of 8 (surplus blocks find no QPs).
+static __device__ __forceinline__ long qpb_xcd_block() {
+    const unsigned b = blockIdx.x, nb = gridDim.x;
+    return (nb & 7) ? (long)b : (long)(b & 7) * (nb >> 3) + (b >> 3);
+}
+
 extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double L[LDS_QP];
     __shared__ __attribute__((aligned(16))) int MS[QPB_MS_TOTAL];      // program step tables
     const int t = threadIdx.x;
-    const long q = blockIdx.x;
+    const long q = qpb_xcd_block();
     if (q >= a.B) return;                        // workgroup-uniform
     const long tile = q >> 6;
     const int ql = (int)(q & 63);
     double tm_fac = 0.0, tm_sol = 0.0, tm_mv = 0.0, tm_all = 0.0;
     (void)tm_fac; (void)tm_sol; (void)tm_mv; (void)tm_all;
     const unsigned long long *__restrict__ TD = (const unsigned long long *)a.tab;
-    const int *__restrict__ TI = (const int *)(TD + QPB_NDESC);
+    const unsigned *__restrict__ TD32 = (const unsigned *)(TD + QPB_NDESC);
+    const int *__restrict__ TI = (const int *)(TD32 + QPB_NDESC32);
 #define qpb_pinv (TI + QPB_I_pinv)
 #define qpb_asrc_i (TI + QPB_I_asrc_i)
 #define qpb_asrc_l (TI + QPB_I_asrc_l)
@@ -319,9 +343,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     };
     auto factor = [&]() {
         QPB_TIC();
-        qpb_run(MS + QPB_MS_FAC, QPB_fac_NSTEPS, TI + QPB_I_fac_hdr, TD + QPB_D_fac, QPB_DUMMY_FAC,
+        qpb_run(MS + QPB_MS_FAC, QPB_fac_NSTEPS, TI + QPB_I_fac_hdr, TD + QPB_D_fac,
                 [&](double acc, unsigned long long d) {
-                    return __builtin_fma(-LD[qpb_f0(d)] * rD[qpb_f2(d)], LD[qpb_f1(d)], acc);
+                    const unsigned lo = (unsigned)d, hi = (unsigned)(d >> 32);
+                    return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(lo)) * QPB_AT(O_RD, qpb_lo16(hi)),
+                                         QPB_AT(O_LD, qpb_hi16(lo)), acc);
                 },
                 [&](int out) { return qpb_pre{out >= 0 ? LD[out] : rD[-1 - out], 0.0}; },
                 [&](int out, double acc, qpb_pre e) {
@@ -333,12 +359,16 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     // W (permuted rhs) -> W (permuted solution)
     auto solve = [&]() {
         QPB_TIC();
-        qpb_run(MS + QPB_MS_FWD, QPB_fwd_NSTEPS, TI + QPB_I_fwd_hdr, TD + QPB_D_fwd, QPB_DUMMY_SOLVE,
-                [&](double acc, unsigned long long d) { return __builtin_fma(-LD[qpb_f0(d)], W[qpb_f1(d)], acc); },
+        qpb_run(MS + QPB_MS_FWD, QPB_fwd_NSTEPS, TI + QPB_I_fwd_hdr, TD32 + QPB_D_fwd,
+                [&](double acc, unsigned d) {
+                    return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(d)), QPB_AT(O_W, qpb_hi16(d)), acc);
+                },
                 [&](int i) { return qpb_pre{W[i], rD[i]}; },
                 [&](int i, double acc, qpb_pre e) { W[i] = e.b * (e.a + acc); });
-        qpb_run(MS + QPB_MS_BWD, QPB_bwd_NSTEPS, TI + QPB_I_bwd_hdr, TD + QPB_D_bwd, QPB_DUMMY_SOLVE,
-                [&](double acc, unsigned long long d) { return __builtin_fma(-LD[qpb_f0(d)], W[qpb_f1(d)], acc); },
+        qpb_run(MS + QPB_MS_BWD, QPB_bwd_NSTEPS, TI + QPB_I_bwd_hdr, TD32 + QPB_D_bwd,
+                [&](double acc, unsigned d) {
+                    return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(d)), QPB_AT(O_W, qpb_hi16(d)), acc);
+                },
                 [&](int k) { return qpb_pre{W[k], rD[k]}; },
                 [&](int k, double acc, qpb_pre e) { W[k] = __builtin_fma(e.b, acc, e.a); });
         QPB_TOC(tm_sol);
@@ -346,8 +376,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     // R = [P A' G'; A 0 0; G 0 0] V (raw products)
     auto products = [&](const double *__restrict__ vec) {
         QPB_TIC();
-        qpb_run(MS + QPB_MS_MV, QPB_mv_NSTEPS, TI + QPB_I_mv_hdr, TD + QPB_D_mv, QPB_DUMMY_MV,
-                [&](double acc, unsigned long long d) { return __builtin_fma(PAG[qpb_f0(d)], vec[qpb_f1(d)], acc); },
+        qpb_run(MS + QPB_MS_MV, QPB_mv_NSTEPS, TI + QPB_I_mv_hdr, TD32 + QPB_D_mv,
+                [&](double acc, unsigned d) {
+                    return __builtin_fma(QPB_AT(O_PAG, qpb_lo16(d)),
+                                         *(const double *)((const char *)vec + qpb_hi16(d)), acc);
+                },
                 [&](int) { return qpb_pre{0.0, 0.0}; },
                 [&](int r, double acc, qpb_pre) { R[r] = acc; });
         QPB_TOC(tm_mv);
@@ -511,8 +544,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
 
     // ---- objective of the x the last residuals were computed at (qpSWIFT.c:515)
     const double *xo = flag == 0 ? V : XP;
-    qpb_run(MS + QPB_MS_OBJ, QPB_obj_NSTEPS, TI + QPB_I_obj_hdr, TD + QPB_D_obj, QPB_DUMMY_MV,
-            [&](double acc, unsigned long long d) { return __builtin_fma(PAG[qpb_f0(d)], xo[qpb_f1(d)], acc); },
+    qpb_run(MS + QPB_MS_OBJ, QPB_obj_NSTEPS, TI + QPB_I_obj_hdr, TD32 + QPB_D_obj,
+            [&](double acc, unsigned d) {
+                return __builtin_fma(QPB_AT(O_PAG, qpb_lo16(d)), *(const double *)((const char *)xo + qpb_hi16(d)),
+                                     acc);
+            },
             [&](int) { return qpb_pre{0.0, 0.0}; },
             [&](int r, double acc, qpb_pre) { R[r] = acc; });
     double fv[1] = {0.0};

@@ -231,11 +231,20 @@ template <int J0, int J1, class F> static __device__ __forceinline__ void qpb_fo
 #define QPB_TS(k) do { } while (0)
 #endif
 
+// XCD-aware block order: blocks b and b + 8 share an XCD (and its L2), so
+// logical block (b % 8) * (nb / 8) + b / 8 gives each XCD a contiguous run of
+// QPs -- the 64 QPs of a tile, whose values share cache lines, stay on one L2.
+// The host pads the grid to a multiple of 8 (surplus blocks find no QPs).
+static __device__ __forceinline__ long qpb_xcd_block() {
+    const unsigned b = blockIdx.x, nb = gridDim.x;
+    return (nb & 7) ? (long)b : (long)(b & 7) * (nb >> 3) + (b >> 3);
+}
+
 extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * LDS_WAVE];
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long q = (long)blockIdx.x * WPB + wv;
+    const long q = qpb_xcd_block() * WPB + wv;
     if (q >= a.B) return;                    // wave-uniform
     double *__restrict__ Ls = qpb_lds + wv * LDS_WAVE;
     const long tile = q >> 6;

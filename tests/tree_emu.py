@@ -11,7 +11,7 @@ import re
 
 import numpy as np
 
-FB = 21
+FB = 16
 FM = (1 << FB) - 1
 
 
@@ -21,15 +21,15 @@ def parse_tables(src: str, blob: bytes) -> dict:
     out = {}
     for m in re.finditer(r"#define (QPB_\w+) (-?\d+)\n", src):
         out[m.group(1)] = int(m.group(2))
-    nd = out["QPB_NDESC"]
+    nd, nd32 = out["QPB_NDESC"], out["QPB_NDESC32"]
     D = np.frombuffer(blob[:8 * nd], dtype=np.uint64)
-    I = np.frombuffer(blob[8 * nd:], dtype=np.int32).astype(np.int64)
+    D32 = np.frombuffer(blob[8 * nd:8 * nd + 4 * nd32], dtype=np.uint32).astype(np.uint64)
+    I = np.frombuffer(blob[8 * nd + 4 * nd32:], dtype=np.int32).astype(np.int64)
     names = ["fac", "fwd", "bwd", "mv", "obj"]
     for k, name in enumerate(names):
         ns = out[f"QPB_{name}_NSTEPS"]
         d0 = out[f"QPB_D_{name}"]
-        d1 = out[f"QPB_D_{names[k + 1]}"] if k + 1 < len(names) else nd
-        out[f"qpb_{name}_desc"] = D[d0:d1]
+        out[f"qpb_{name}_desc"] = D[d0:] if name == "fac" else D32[d0:]
         s0 = out[f"QPB_I_{name}_steps"]
         out[f"qpb_{name}_steps"] = I[s0:s0 + 4 * ns]
         h0 = out[f"QPB_I_{name}_hdr"]
@@ -50,8 +50,8 @@ def run_prog(T, name, term, epi, wg):
         acc = np.zeros(act)
         for r in range(R):
             for lane in range(act):
-                d = int(desc[doff + r * act + lane])
-                acc[lane] = term(acc[lane], d & FM, (d >> FB) & FM, d >> (2 * FB))
+                d = int(desc[doff + r * act + lane])     # LDS byte offsets -> element indices
+                acc[lane] = term(acc[lane], (d & FM) >> 3, ((d >> FB) & FM) >> 3, ((d >> (2 * FB)) & FM) >> 3)
         for t in range(nt):
             epi(int(hdr[toff + t]), float(acc[t * G:(t + 1) * G].sum()))
 
