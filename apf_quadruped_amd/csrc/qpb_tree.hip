@@ -120,6 +120,15 @@ static __device__ __forceinline__ double qpb_wmin(double v) {
 #ifndef QPB_T_TIMING
 #define QPB_T_TIMING 0  // 1: per-phase cycle counts (s_memtime) into stats instead of the residual norms
 #endif
+#if QPB_T_TIMING == 2
+// in-step segments (wave 0, lane 0 accumulates): [0] waiting for the step's
+// descriptors, [1] terms + group sum, [2] epilogue, [3] barrier; [4] step count
+__shared__ double qpb_seg[8];
+#define QPB_SEG(k, ...) do { asm volatile("" ::__VA_ARGS__); const long qpb_now = (long)__builtin_readcyclecounter(); \
+    if (threadIdx.x == 0) qpb_seg[k] += (double)(qpb_now - qpb_seg_t); qpb_seg_t = qpb_now; } while (0)
+#else
+#define QPB_SEG(k, ...) do { } while (0)
+#endif
 #if QPB_T_TIMING
 #define QPB_TIC() const long qpb_t0 = (long)__builtin_readcyclecounter()
 #define QPB_TOC(v) (v) += (double)((long)__builtin_readcyclecounter() - qpb_t0)
@@ -131,6 +140,9 @@ static __device__ __forceinline__ double qpb_wmin(double v) {
 #ifndef QPB_T_EXP
 #define QPB_T_EXP 0     // timing experiments only (wrong results): 2 no barriers, 3 no terms,
                         // 4 no group sums, 5 no epilogue
+#endif
+#ifndef QPB_T_DEPTH
+#define QPB_T_DEPTH 4   // register sets of prefetched steps (2 or 4): a step's tables are loaded DEPTH steps ahead
 #endif
 #ifndef QPB_T_PF
 #define QPB_T_PF 8      // descriptor rounds prefetched per step
@@ -147,9 +159,9 @@ static __device__ __forceinline__ void qpb_bar() { asm volatile("s_waitcnt lgkmc
 // operands (loaded before the terms are summed); post(code, acc, pre) writes the
 // result.  D: descriptor word (u64 for the factor, u32 otherwise).
 //
-// Descriptors, output codes and step metadata are prefetched two steps ahead
-// into two register sets (A for even, B for odd steps; the loop is unrolled by
-// two so neither is copied).  Every prefetch issues the same loads (rounds past
+// Descriptors, output codes and step metadata are prefetched QPB_T_DEPTH steps
+// ahead into as many register sets (the loop is unrolled by the depth, so no set
+// is ever copied).  Every prefetch issues the same loads (rounds past
 // a step's count re-read round 0, lanes past its active count read padding), so
 // the compiler waits with vmcnt(N) for the set a step consumes instead of
 // vmcnt(0); the step metadata is uniform (readfirstlane) so each load is an
@@ -177,8 +189,12 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
         for (int r = 0; r < QPB_T_PF; r++) S.d[r] = base[(r < R ? r : 0) * act + l];
         S.h = hdr[toff + (l >> g)];
     };
+#if QPB_T_TIMING == 2
+    long qpb_seg_t = (long)__builtin_readcyclecounter();
+#endif
     auto step = [&](const qpb_set<D> &S) {
         const int g = S.ntg & 15, act = (S.ntg >> 4) << g, R = S.rb & 0xffff;
+        QPB_SEG(0, "v"(S.d[0]), "v"(S.h));
         if (l < act) {
 #if QPB_T_EXP == 5
             const qpb_pre e{0.0, 1.0};
@@ -207,6 +223,7 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
 #if QPB_T_EXP != 4
             acc = qpb_gsum(acc, g);
 #endif
+            QPB_SEG(1, "v"(acc));
 #if QPB_T_EXP != 5
             if ((l & ((1 << g) - 1)) == (1 << g) - 1) post(S.h, acc, e);
 #else
@@ -219,10 +236,32 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
         static_assert(QPB_T_PF == 8, "qpb_keep lists eight descriptor slots");
         asm volatile("" ::"v"(S.h), "v"(S.d[0]), "v"(S.d[1]), "v"(S.d[2]), "v"(S.d[3]), "v"(S.d[4]), "v"(S.d[5]),
                      "v"(S.d[6]), "v"(S.d[7]));
+        QPB_SEG(2, "s"(0));
 #if QPB_T_EXP != 2
         if (S.rb >> 16) qpb_bar();
 #endif
+        QPB_SEG(3, "s"(0));
+#if QPB_T_TIMING == 2
+        if (threadIdx.x == 0) qpb_seg[4] += 1.0;
+#endif
     };
+#if QPB_T_DEPTH == 4
+    qpb_set<D> C, E;
+    prefetch(0, A);
+    prefetch(1, B);
+    prefetch(2, C);
+    prefetch(3, E);
+    for (int st = 0; st < nsteps; st += 4) {
+        step(A);
+        prefetch(st + 4, A);
+        if (st + 1 < nsteps) step(B);
+        prefetch(st + 5, B);
+        if (st + 2 < nsteps) step(C);
+        prefetch(st + 6, C);
+        if (st + 3 < nsteps) step(E);
+        prefetch(st + 7, E);
+    }
+#else
     prefetch(0, A);
     prefetch(1, B);
     for (int st = 0; st < nsteps; st += 2) {
@@ -231,6 +270,7 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
         if (st + 1 < nsteps) step(B);
         prefetch(st + 3, B);
     }
+#endif
 }
 
 // K-value sums over the workgroup (result in every thread)
@@ -321,6 +361,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     for (int j = t; j < NY; j += QPB_WG) Bv[j] = a.b[tile * (NY * 64) + j * 64 + ql];
 #endif
     if (t == 0) { PAG[NPAG] = 0.0; LD[LNZ] = 0.0; }
+#if QPB_T_TIMING == 2
+    if (t < 8) qpb_seg[t] = 0.0;
+#endif
     for (int j = t; j < 4 * QPB_fac_NSTEPS; j += QPB_WG) MS[QPB_MS_FAC + j] = TI[QPB_I_fac_steps + j];
     for (int j = t; j < 4 * QPB_fwd_NSTEPS; j += QPB_WG) MS[QPB_MS_FWD + j] = TI[QPB_I_fwd_steps + j];
     for (int j = t; j < 4 * QPB_bwd_NSTEPS; j += QPB_WG) MS[QPB_MS_BWD + j] = TI[QPB_I_bwd_steps + j];
@@ -570,7 +613,10 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
         a.fval[q] = fv[0];
         if (a.stats) {
             double *st = a.stats + tile * (6 * 64) + ql;
-#if QPB_T_TIMING
+#if QPB_T_TIMING == 2
+            st[0] = qpb_seg[0]; st[64] = qpb_seg[1]; st[128] = qpb_seg[2]; st[192] = qpb_seg[3]; st[256] = qpb_seg[4];
+            st[320] = (double)((long)__builtin_readcyclecounter() - qpb_tall);
+#elif QPB_T_TIMING
             tm_all = (double)((long)__builtin_readcyclecounter() - qpb_tall);
             st[0] = tm_fac; st[64] = tm_sol; st[128] = tm_mv; st[192] = tm_all; st[256] = (double)QPB_fac_NSTEPS;
             st[320] = (double)(QPB_fwd_NSTEPS + QPB_bwd_NSTEPS);

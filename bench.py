@@ -260,8 +260,8 @@ def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
 def traffic_for(kname, B):
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
-        t = json.load(open(tfile)).get(kname)
-        if t and int(t.get("batch", -1)) == B:
+        t = json.load(open(tfile)).get(f"{kname}@{B}")
+        if t:
             return float(t["hbm_bytes_per_launch"])
     return None
 

@@ -48,10 +48,10 @@ def main():
         w = per_kernel(write, "WRITE_SIZE", batch)
         for k in f:
             if k in w:
-                data[k] = dict(batch=batch, fetch_kb=f[k], write_kb=w[k],
+                data[f"{k}@{batch}"] = dict(kernel=k, batch=batch, fetch_kb=f[k], write_kb=w[k],
                                hbm_bytes_per_launch=(2 * f[k] + w[k]) * 1024.0,
                                calibrated=k.startswith("qpb_ipm"))
-                print(k, data[k])
+                print(k, batch, data[f"{k}@{batch}"])
     json.dump(data, open(out_path, "w"), indent=1, sort_keys=True)
 
 
