@@ -55,11 +55,28 @@ struct Task {
     std::vector<uint64_t> con;
 };
 
+constexpr int32_t STEP_BARRIER = 1 << 16, STEP_PANEL = 1 << 17;
+
 struct Prog {
-    std::vector<int32_t> steps;   // 4 per step: desc offset, task offset, ntask << 4 | log2 G, R | barrier << 16
+    // 4 ints per step: desc offset, task offset, ntask << 4 | log2 G, R | flags.  A panel
+    // step (STEP_PANEL, no gather lanes) holds a panel-list index and a count instead.
+    std::vector<int32_t> steps;
     std::vector<int32_t> hdr;     // one output code per task
     std::vector<uint64_t> desc;   // [R][ntask * G] per step
+    std::vector<std::vector<int32_t>> panels;   // supernode ids of every panel step
     long nsteps() const { return (long)steps.size() / 4; }
+    void panel_step(const std::vector<int32_t> &ids) {
+        if (ids.empty()) return;
+        steps.insert(steps.end(), {(int32_t)panels.size(), (int32_t)ids.size(), 0, 1 | STEP_BARRIER | STEP_PANEL});
+        panels.push_back(ids);
+    }
+};
+
+// A relaxed supernode: columns j0 .. j0+w-1 with parent(j) = j+1 and nested
+// structure (colcount(j) = colcount(j+1) + 1).  Its panel has R = colcount(j0) + 1
+// rows (the supernode's own w and the rows below), one per lane of a wavefront.
+struct Snode {
+    long j0, w, R;
 };
 
 // One level's tasks -> steps.  Tasks are sorted by term count; the lanes-per-task
@@ -76,7 +93,9 @@ void pack_level(std::vector<Task> &tasks, int wg, uint64_t dummy, Prog &P) {
         double cost = 0;
         for (size_t s = 0; s < tasks.size(); s += per) {
             const long R = round_bucket(((long)tasks[s].con.size() + G - 1) / G);
-            cost += 3.0 * R + 3.0 * g + 30.0;
+            // per step: one round per term a lane sums, the butterfly, a fixed cost;
+            // rounds past the 8 prefetched ones add a memory latency per 24 (qpb_run)
+            cost += 3.0 * R + 3.0 * g + 30.0 + (R > 8 ? 12.0 * (double)((R - 8 + 23) / 24) : 0.0);
         }
         if (cost < best_cost - 1e-9) { best_cost = cost; best_g = g; }
     }
@@ -98,7 +117,7 @@ void pack_level(std::vector<Task> &tasks, int wg, uint64_t dummy, Prog &P) {
         }
         const bool last = e == tasks.size();
         P.steps.insert(P.steps.end(), {(int32_t)doff, (int32_t)toff, (int32_t)((nt << 4) | g),
-                                       (int32_t)(R | (last ? 1 << 16 : 0))});
+                                       (int32_t)(R | (last ? STEP_BARRIER : 0))});
     }
 }
 
@@ -118,7 +137,17 @@ struct Blob {
     // lanes past a step's active count and rounds past its count read (and
     // ignore) entries beyond the program's end: wg entries of padding keep
     // those reads inside the buffer
-    void prog(const char *name, const Prog &P, bool wide) {
+    std::vector<int32_t> snrec;   // TI offset of every supernode record [j0, w, R, Lp[j0] .. Lp[j0+w-1]]
+    void prog(const char *name, const Prog &P0, bool wide) {
+        Prog P = P0;
+        // panel lists -> int section; panel steps point at them
+        for (long st = 0; st < P.nsteps(); st++) {
+            int32_t *m = &P.steps[4 * st];
+            if (!(m[3] & STEP_PANEL)) continue;
+            const int32_t off = (int32_t)i.size();
+            for (int32_t id : P.panels[m[0]]) i.push_back(snrec[id]);
+            m[0] = off;
+        }
         macros << "#define QPB_" << name << "_NSTEPS " << P.nsteps() << "\n";
         if (wide) {
             macros << "#define QPB_D_" << name << " " << d.size() << "\n";
@@ -189,32 +218,61 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
         }
     }
 
-    // levels: height above the leaves of the elimination tree (parent > child)
-    std::vector<long> level(N, 0);
-    for (long j = 0; j < N; j++)
-        if (pl.parent[j] >= 0) level[pl.parent[j]] = std::max(level[pl.parent[j]], level[j] + 1);
-    const long H = N ? *std::max_element(level.begin(), level.end()) + 1 : 0;
+    // supernodes and node levels.  A node is a supernode or a single column; its
+    // level is its height above the leaves of the node tree (parent > child).
+    std::vector<long> cc(N);
+    for (long k = 0; k < N; k++) cc[k] = pl.Lp[k + 1] - pl.Lp[k];
+    std::vector<Snode> sns;
+    std::vector<long> sn_of(N, -1);
+    const bool panels = !getenv("QPB_TREE_NOPANEL");
+    const long maxw = 48;                         // registers per lane of the panel kernels
+    for (long j = 0; j < N;) {
+        long e = j;
+        if (panels && cc[j] + 1 <= 64)
+            while (e + 1 < N && pl.parent[e] == e + 1 && cc[e] == cc[e + 1] + 1 && e + 2 - j <= maxw) e++;
+        if (e > j) {
+            for (long c = j; c <= e; c++) sn_of[c] = (long)sns.size();
+            sns.push_back({j, e - j + 1, cc[j] + 1});
+        }
+        j = e + 1;
+    }
+    auto key = [&](long j) { return sn_of[j] >= 0 ? N + sn_of[j] : j; };
+    std::vector<long> nlev(N + sns.size(), 0);
+    for (long k = 0; k < N; k++) {
+        const long par = pl.parent[k];
+        if (par >= 0 && key(par) != key(k)) nlev[key(par)] = std::max(nlev[key(par)], nlev[key(k)] + 1);
+    }
+    std::vector<long> level(N);
+    long H = 0;
+    for (long j = 0; j < N; j++) { level[j] = nlev[key(j)]; H = std::max(H, level[j] + 1); }
+    std::vector<std::vector<int32_t>> lvl_sn(H);
+    for (size_t t = 0; t < sns.size(); t++) lvl_sn[level[sns[t].j0]].push_back((int32_t)t);
+    auto j0_of = [&](long j) { return sn_of[j] >= 0 ? sns[sn_of[j]].j0 : j; };   // external terms: k < j0
     // row structures of L: rs[i] = (k, position of L(i,k)), k ascending
     std::vector<std::vector<std::pair<long, long>>> rs(N);
     for (long k = 0; k < N; k++)
         for (long e = pl.Lp[k]; e < pl.Lp[k + 1]; e++) rs[pl.Li[e]].push_back({k, e});
 
-    // fac
+    // fac: single columns complete here (diagonal -> 1/D); supernode columns get
+    // their external updates only (diagonal kept raw), then the level's panel step
     Prog fac, fwd, bwd, mv, obj;
     long fac_contrib = 0;
     {
         std::vector<std::vector<Task>> lv(H);
         for (long j = 0; j < N; j++) {
-            Task d{(int32_t)(-1 - j), {}};
-            for (auto &kp : rs[j]) d.con.push_back(pk(kp.second, kp.second, kp.first));
+            const bool sn = sn_of[j] >= 0;
+            const long lim = j0_of(j);
+            Task d{(int32_t)(sn ? -1 - N - j : -1 - j), {}};
+            for (auto &kp : rs[j])
+                if (kp.first < lim) d.con.push_back(pk(kp.second, kp.second, kp.first));
             fac_contrib += (long)d.con.size();
-            lv[level[j]].push_back(std::move(d));
+            if (!sn || !d.con.empty()) lv[level[j]].push_back(std::move(d));
             for (long e = pl.Lp[j]; e < pl.Lp[j + 1]; e++) {
                 const long i = pl.Li[e];
                 Task t{(int32_t)e, {}};
                 size_t a = 0, b = 0;
                 const auto &ri = rs[i], &rj = rs[j];
-                while (a < ri.size() && b < rj.size() && ri[a].first < j && rj[b].first < j) {
+                while (a < ri.size() && b < rj.size() && ri[a].first < lim && rj[b].first < lim) {
                     if (ri[a].first < rj[b].first) a++;
                     else if (ri[a].first > rj[b].first) b++;
                     else { t.con.push_back(pk(ri[a].second, rj[b].second, ri[a].first)); a++; b++; }
@@ -223,21 +281,35 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
                 if (!t.con.empty()) lv[level[j]].push_back(std::move(t));   // else LD(i,j) = K(i,j) as assembled
             }
         }
-        for (auto &l : lv) pack_level(l, wg, pk(lnz, lnz, 0), fac);
+        for (long h = 0; h < H; h++) {
+            pack_level(lv[h], wg, pk(lnz, lnz, 0), fac);
+            fac.panel_step(lvl_sn[h]);
+        }
     }
     // fwd / bwd
     {
         std::vector<std::vector<Task>> lf(H), lb(H);
         for (long i = 0; i < N; i++) {
-            Task t{(int32_t)i, {}};
-            for (auto &kp : rs[i]) t.con.push_back(pk(kp.second, kp.first));
-            lf[level[i]].push_back(std::move(t));
+            const bool sn = sn_of[i] >= 0;
+            const long lim = j0_of(i);
+            Task t{(int32_t)(sn ? -1 - i : i), {}};          // supernode rows: raw external sum
+            for (auto &kp : rs[i])
+                if (kp.first < lim) t.con.push_back(pk(kp.second, kp.first));
+            if (!sn || !t.con.empty()) lf[level[i]].push_back(std::move(t));
+            const long rowlim = sn ? sns[sn_of[i]].j0 + sns[sn_of[i]].w : 0;   // bwd: rows below the supernode
             Task u{(int32_t)i, {}};
-            for (long e = pl.Lp[i]; e < pl.Lp[i + 1]; e++) u.con.push_back(pk(e, pl.Li[e]));
+            for (long e = pl.Lp[i]; e < pl.Lp[i + 1]; e++)
+                if (pl.Li[e] >= rowlim) u.con.push_back(pk(e, pl.Li[e]));
             if (!u.con.empty()) lb[level[i]].push_back(std::move(u));
         }
-        for (auto &l : lf) pack_level(l, wg, pk(lnz, 0), fwd);
-        for (long h = H - 1; h >= 0; h--) pack_level(lb[h], wg, pk(lnz, 0), bwd);
+        for (long h = 0; h < H; h++) {
+            pack_level(lf[h], wg, pk(lnz, 0), fwd);
+            fwd.panel_step(lvl_sn[h]);
+        }
+        for (long h = H - 1; h >= 0; h--) {
+            pack_level(lb[h], wg, pk(lnz, 0), bwd);
+            bwd.panel_step(lvl_sn[h]);
+        }
     }
     // mv / obj (natural KKT rows; K is symmetric in pattern and, before the z
     // diagonal update, in value: column r lists row r)
@@ -282,6 +354,19 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
     }
     Blob bl;
     bl.wg = wg;
+    {
+        std::vector<long> widths;
+        for (auto &sn : sns) {
+            bl.snrec.push_back((int32_t)bl.i.size());
+            bl.i.insert(bl.i.end(), {(int32_t)sn.j0, (int32_t)sn.w, (int32_t)sn.R});
+            for (long c = 0; c < sn.w; c++) bl.i.push_back((int32_t)pl.Lp[sn.j0 + c]);
+            if (std::find(widths.begin(), widths.end(), sn.w) == widths.end()) widths.push_back(sn.w);
+        }
+        std::sort(widths.begin(), widths.end());
+        o << "#define QPB_NSNODE " << sns.size() << "\n#define QPB_PANEL_WIDTHS(X)";
+        for (long w : widths) o << " X(" << w << ")";
+        o << "\n";
+    }
     bl.prog("fac", fac, true);
     bl.prog("fwd", fwd, false);
     bl.prog("bwd", bwd, false);
@@ -310,6 +395,7 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
     }
     if (stats) {
         stats->levels = H;
+        stats->supernodes = (long)sns.size();
         stats->fac_steps = fac.nsteps(); stats->fwd_steps = fwd.nsteps();
         stats->bwd_steps = bwd.nsteps(); stats->mv_steps = mv.nsteps();
         stats->fac_contrib = fac_contrib;

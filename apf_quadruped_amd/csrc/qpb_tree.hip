@@ -142,7 +142,10 @@ __shared__ double qpb_seg[8];
                         // 4 no group sums, 5 no epilogue
 #endif
 #ifndef QPB_T_DEPTH
-#define QPB_T_DEPTH 4   // register sets of prefetched steps (2 or 4): a step's tables are loaded DEPTH steps ahead
+#define QPB_T_DEPTH 2   // register sets of prefetched steps (2 or 4): a step's tables are loaded DEPTH steps ahead
+#endif
+#ifndef QPB_T_XR
+#define QPB_T_XR 24     // extra rounds a step loads at its start (beyond the prefetched ones)
 #endif
 #ifndef QPB_T_PF
 #define QPB_T_PF 8      // descriptor rounds prefetched per step
@@ -169,10 +172,11 @@ static __device__ __forceinline__ void qpb_bar() { asm volatile("s_waitcnt lgkmc
 // dummy terms (they read the zero entries), so a step sums its terms without
 // branches and their LDS reads issue back to back.
 struct qpb_pre { double a, b; };
-template <class D> struct qpb_set { D d[QPB_T_PF]; int h, doff, ntg, rb; };
-template <class D, class Term, class Pre, class Post>
+template <class D> struct qpb_set { D d[QPB_T_PF]; int h, doff, toff, ntg, rb; };
+template <class D, class Term, class Pre, class Post, class Panel>
 static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const int *__restrict__ hdr,
-                                               const D *__restrict__ desc, Term term, Pre pre, Post post) {
+                                               const D *__restrict__ desc, Term term, Pre pre, Post post,
+                                               Panel panel) {
     if (nsteps <= 0) return;
     const int l = threadIdx.x;
     qpb_set<D> A, B;
@@ -181,13 +185,14 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
         const int4 m = *(const int4 *)(ms + 4 * st);
         S.doff = __builtin_amdgcn_readfirstlane(m.x);
         const int toff = __builtin_amdgcn_readfirstlane(m.y);
+        S.toff = toff;
         S.ntg = __builtin_amdgcn_readfirstlane(m.z);
         S.rb = __builtin_amdgcn_readfirstlane(m.w);
         const int g = S.ntg & 15, act = (S.ntg >> 4) << g, R = S.rb & 0xffff;
-        const D *base = desc + S.doff;
+        const D *base = desc + (act ? S.doff : 0);       // panel steps have no gather lanes
 #pragma unroll
         for (int r = 0; r < QPB_T_PF; r++) S.d[r] = base[(r < R ? r : 0) * act + l];
-        S.h = hdr[toff + (l >> g)];
+        S.h = hdr[act ? toff + (l >> g) : 0];
     };
 #if QPB_T_TIMING == 2
     long qpb_seg_t = (long)__builtin_readcyclecounter();
@@ -213,11 +218,28 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
                 acc = term(term(0.0, S.d[0]), S.d[1]);
             } else if (R == 4) {
                 acc = term(term(0.0, S.d[0]), S.d[1]) + term(term(0.0, S.d[2]), S.d[3]);
-            } else {
+            } else if (R == QPB_T_PF) {
                 double u = 0.0, v = 0.0;
 #pragma unroll
                 for (int r = 0; r < QPB_T_PF; r += 2) { u = term(u, S.d[r]); v = term(v, S.d[r + 1]); }
-                for (int r = QPB_T_PF; r < R; r++) u = term(u, desc[S.doff + r * act + l]);   // rare
+                acc = u + v;
+            } else {
+                // more rounds than prefetched: load up to QPB_T_XR more at once (one
+                // memory latency, overlapped with the prefetched rounds' terms), a
+                // rolled loop beyond that
+                D dx[QPB_T_XR];
+#pragma unroll
+                for (int r = 0; r < QPB_T_XR; r++)
+                    if (QPB_T_PF + r < R) dx[r] = desc[S.doff + (QPB_T_PF + r) * act + l];
+                double u = 0.0, v = 0.0;
+#pragma unroll
+                for (int r = 0; r < QPB_T_PF; r += 2) { u = term(u, S.d[r]); v = term(v, S.d[r + 1]); }
+#pragma unroll
+                for (int r = 0; r < QPB_T_XR; r += 2) {
+                    if (QPB_T_PF + r < R) u = term(u, dx[r]);
+                    if (QPB_T_PF + r + 1 < R) v = term(v, dx[r + 1]);
+                }
+                for (int r = QPB_T_PF + QPB_T_XR; r < R; r++) u = term(u, desc[S.doff + r * act + l]);   // rare
                 acc = u + v;
             }
 #if QPB_T_EXP != 4
@@ -237,8 +259,9 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
         asm volatile("" ::"v"(S.h), "v"(S.d[0]), "v"(S.d[1]), "v"(S.d[2]), "v"(S.d[3]), "v"(S.d[4]), "v"(S.d[5]),
                      "v"(S.d[6]), "v"(S.d[7]));
         QPB_SEG(2, "s"(0));
+        if (S.rb & (1 << 17)) panel(S.doff, S.toff);    // supernode panels of this level (list, count)
 #if QPB_T_EXP != 2
-        if (S.rb >> 16) qpb_bar();
+        if (S.rb & (1 << 16)) qpb_bar();
 #endif
         QPB_SEG(3, "s"(0));
 #if QPB_T_TIMING == 2
@@ -306,6 +329,89 @@ static __device__ __forceinline__ void qpb_bmin(double (&v)[K], double *red) {
     }
     __syncthreads();
 }
+
+
+// ---- supernode panels (qpb_tree.cpp Snode): one wavefront per supernode, one
+// panel row per lane, the panel's columns in registers (W is a compile-time
+// width; the plan's widths are listed in QPB_PANEL_WIDTHS).  Record layout in the
+// int tables: j0, W, R (rows), then Lp of the W columns; column c's entries are
+// the panel rows after c, so row r of column c sits at LD[Lp(j0+c) + r - c - 1].
+
+// value of lane `lane` (a compile-time constant after unrolling), in every lane
+static __device__ __forceinline__ double qpb_rl(double v, int lane) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// right-looking LDL' of the panel (the supernode's external updates are already
+// applied; its diagonal arrives raw in rD): pivot k -> 1/D_k with the reference's
+// regularisation (ldl.c:273-274, 319-320), then A(r,c) -= A(r,k) A(c,k) / D_k for
+// k < c <= r.  LD keeps the unscaled column (A(r,k) at pivot k), as the gather
+// programs do.  Lanes above a column's diagonal compute values never stored.
+template <int W>
+static __device__ __forceinline__ void qpb_pfac(double *__restrict__ L, const int *__restrict__ rec, int lane) {
+    const int j0 = rec[0], R = rec[2];
+    const int *lp = rec + 3;
+    const bool on = lane < R;
+    double P[W];
+#pragma unroll
+    for (int c = 0; c < W; c++)
+        P[c] = L[lane == c ? O_RD + j0 + c : O_LD + ((on && lane > c) ? lp[c] + lane - c - 1 : LNZ)];
+    double myr = 0.0;
+#pragma unroll
+    for (int k = 0; k < W; k++) {
+        const double rk = qpb_rcp_reg(qpb_rl(P[k], k));
+        myr = lane == k ? rk : myr;
+        const double f = -P[k] * rk;
+#pragma unroll
+        for (int c = k + 1; c < W; c++) P[c] = __builtin_fma(f, qpb_rl(P[k], c), P[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < W; c++)
+        if (on && lane > c) L[O_LD + lp[c] + lane - c - 1] = P[c];
+    if (lane < W) L[O_RD + j0 + lane] = myr;
+}
+
+// forward solve inside the supernode: W holds b minus the external terms (raw);
+// w_k = t_k / D_k, then t_c -= LD(c,k) w_k for c > k
+template <int W>
+static __device__ __forceinline__ void qpb_pfwd(double *__restrict__ L, const int *__restrict__ rec, int lane) {
+    const int j0 = rec[0];
+    const int *lp = rec + 3;
+    const bool on = lane < W;
+    double Lr[W];
+#pragma unroll
+    for (int k = 0; k < W; k++) Lr[k] = -L[O_LD + ((on && lane > k) ? lp[k] + lane - k - 1 : LNZ)];
+    double t = L[O_W + j0 + (on ? lane : 0)];
+    const double rd = L[O_RD + j0 + (on ? lane : 0)];
+#pragma unroll
+    for (int k = 0; k < W; k++) t = __builtin_fma(Lr[k], qpb_rl(t, k) * qpb_rl(rd, k), t);
+    if (on) L[O_W + j0 + lane] = rd * t;
+}
+
+// backward solve inside the supernode: W holds w minus D^-1 times the terms of
+// the rows below; x_k final in descending k, then v_c -= LD(k,c) x_k / D_c for c < k
+template <int W>
+static __device__ __forceinline__ void qpb_pbwd(double *__restrict__ L, const int *__restrict__ rec, int lane) {
+    const int j0 = rec[0];
+    const int *lp = rec + 3;
+    const bool on = lane < W;
+    const int lpl = lp[on ? lane : 0];
+    const double rd = L[O_RD + j0 + (on ? lane : 0)];
+    double Lc[W];
+#pragma unroll
+    for (int i = 0; i < W; i++) Lc[i] = -rd * L[O_LD + ((on && i > lane) ? lpl + i - lane - 1 : LNZ)];
+    double v = L[O_W + j0 + (on ? lane : 0)];
+#pragma unroll
+    for (int k = W - 1; k >= 0; k--) v = __builtin_fma(Lc[k], qpb_rl(v, k), v);
+    if (on) L[O_W + j0 + lane] = v;
+}
+
+#ifndef QPB_PANEL_WIDTHS
+#define QPB_PANEL_WIDTHS(X)
+#endif
 
 // XCD-aware block order: blocks b and b + 8 share an XCD (and its L2), so
 // logical block (b % 8) * (nb / 8) + b / 8 gives each XCD a contiguous run of
@@ -392,10 +498,21 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(lo)) * QPB_AT(O_RD, qpb_lo16(hi)),
                                          QPB_AT(O_LD, qpb_hi16(lo)), acc);
                 },
-                [&](int out) { return qpb_pre{out >= 0 ? LD[out] : rD[-1 - out], 0.0}; },
+                [&](int out) { return qpb_pre{out >= 0 ? LD[out] : rD[out >= -NN ? -1 - out : -1 - NN - out], 0.0}; },
                 [&](int out, double acc, qpb_pre e) {
                     if (out >= 0) LD[out] = e.a + acc;
-                    else rD[-1 - out] = qpb_rcp_reg(e.a + acc);
+                    else if (out >= -NN) rD[-1 - out] = qpb_rcp_reg(e.a + acc);
+                    else rD[-1 - NN - out] = e.a + acc;          // supernode diagonal: raw, the panel pivots
+                },
+                [&](int list, int count) {
+                    for (int i = threadIdx.x >> 6; i < count; i += NW) {
+                        const int *rec = TI + TI[list + i];
+                        switch (rec[1]) {
+#define QPB_PF(w) case w: qpb_pfac<w>(L, rec, threadIdx.x & 63); break;
+                            QPB_PANEL_WIDTHS(QPB_PF)
+#undef QPB_PF
+                        }
+                    }
                 });
         QPB_TOC(tm_fac);
     };
@@ -406,14 +523,37 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
                 [&](double acc, unsigned d) {
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(d)), QPB_AT(O_W, qpb_hi16(d)), acc);
                 },
-                [&](int i) { return qpb_pre{W[i], rD[i]}; },
-                [&](int i, double acc, qpb_pre e) { W[i] = e.b * (e.a + acc); });
+                [&](int i) { const int j = i >= 0 ? i : -1 - i; return qpb_pre{W[j], rD[j]}; },
+                [&](int i, double acc, qpb_pre e) {
+                    if (i >= 0) W[i] = e.b * (e.a + acc);
+                    else W[-1 - i] = e.a + acc;                  // supernode row: raw, the panel solves
+                },
+                [&](int list, int count) {
+                    for (int i = threadIdx.x >> 6; i < count; i += NW) {
+                        const int *rec = TI + TI[list + i];
+                        switch (rec[1]) {
+#define QPB_PF(w) case w: qpb_pfwd<w>(L, rec, threadIdx.x & 63); break;
+                            QPB_PANEL_WIDTHS(QPB_PF)
+#undef QPB_PF
+                        }
+                    }
+                });
         qpb_run(MS + QPB_MS_BWD, QPB_bwd_NSTEPS, TI + QPB_I_bwd_hdr, TD32 + QPB_D_bwd,
                 [&](double acc, unsigned d) {
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(d)), QPB_AT(O_W, qpb_hi16(d)), acc);
                 },
                 [&](int k) { return qpb_pre{W[k], rD[k]}; },
-                [&](int k, double acc, qpb_pre e) { W[k] = __builtin_fma(e.b, acc, e.a); });
+                [&](int k, double acc, qpb_pre e) { W[k] = __builtin_fma(e.b, acc, e.a); },
+                [&](int list, int count) {
+                    for (int i = threadIdx.x >> 6; i < count; i += NW) {
+                        const int *rec = TI + TI[list + i];
+                        switch (rec[1]) {
+#define QPB_PF(w) case w: qpb_pbwd<w>(L, rec, threadIdx.x & 63); break;
+                            QPB_PANEL_WIDTHS(QPB_PF)
+#undef QPB_PF
+                        }
+                    }
+                });
         QPB_TOC(tm_sol);
     };
     // R = [P A' G'; A 0 0; G 0 0] V (raw products)
@@ -425,7 +565,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
                                          *(const double *)((const char *)vec + qpb_hi16(d)), acc);
                 },
                 [&](int) { return qpb_pre{0.0, 0.0}; },
-                [&](int r, double acc, qpb_pre) { R[r] = acc; });
+                [&](int r, double acc, qpb_pre) { R[r] = acc; }, [](int, int) {});
         QPB_TOC(tm_mv);
     };
 
@@ -593,7 +733,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
                                      acc);
             },
             [&](int) { return qpb_pre{0.0, 0.0}; },
-            [&](int r, double acc, qpb_pre) { R[r] = acc; });
+            [&](int r, double acc, qpb_pre) { R[r] = acc; }, [](int, int) {});
     double fv[1] = {0.0};
     for (int r = t; r < NX; r += QPB_WG) fv[0] += xo[r] * (0.5 * R[r] + Cv[r]);
     qpb_bsum(fv, RED);

@@ -9,7 +9,8 @@
 namespace qpb {
 // Shape statistics of the level-scheduled programs of a plan's tree kernel.
 struct TreeStats {
-    long levels = 0;          // height of the elimination tree
+    long levels = 0;          // height of the (supernodal) elimination tree
+    long supernodes = 0;      // relaxed supernodes factored / solved as dense panels
     long fac_steps = 0, fwd_steps = 0, bwd_steps = 0, mv_steps = 0;
     long fac_contrib = 0;     // factor update terms per factorisation
     long desc_words = 0;      // descriptor table size (8-byte words, all programs)

@@ -36,13 +36,25 @@ def parse_tables(src: str, blob: bytes) -> dict:
         out[f"qpb_{name}_hdr"] = I[h0:]
     for name in ("pinv", "asrc_i", "asrc_l"):
         out[f"qpb_{name}"] = I[out[f"QPB_I_{name}"]:]
+    out["I"] = I
     return out
 
 
-def run_prog(T, name, term, epi, wg):
+PANEL = 1 << 17
+
+
+def run_prog(T, name, term, epi, wg, panel=None):
+    """Execute a program; panel(record) runs a supernode panel (qpb_tree.hip)."""
     steps = T[f"qpb_{name}_steps"].reshape(-1, 4)[:T[f"QPB_{name}_NSTEPS"]]
     hdr, desc = T[f"qpb_{name}_hdr"], T[f"qpb_{name}_desc"]
+    I = T["I"]
     for doff, toff, ntg, rb in steps:
+        if int(rb) & PANEL:
+            for k in range(int(toff)):
+                r0 = int(I[int(doff) + k])
+                w = int(I[r0 + 1])
+                panel(int(I[r0]), w, int(I[r0 + 2]), [int(v) for v in I[r0 + 3:r0 + 3 + w]])
+            continue
         g = int(ntg) & 15
         G, nt, R = 1 << g, int(ntg) >> 4, int(rb) & 0xFFFF
         act = nt * G
@@ -85,16 +97,36 @@ class TreeEmu:
         return LD, rD
 
     def factor(self, LD, rD):
+        N = self.N
+
         def term(acc, a, b, k):
             return acc - LD[a] * rD[k] * LD[b]
 
         def epi(out, acc):
             if out >= 0:
                 LD[out] += acc
-            else:
+            elif out >= -N:
                 j = -1 - out
                 rD[j] = rcp_reg(rD[j] + acc)
-        run_prog(self.T, "fac", term, epi, self.wg)
+            else:
+                rD[-1 - N - out] += acc          # supernode diagonal: raw
+
+        def panel(j0, w, R, lp):
+            # dense right-looking LDL' of the R x w panel (qpb_pfac)
+            P = np.zeros((R, w))
+            for c in range(w):
+                P[c, c] = rD[j0 + c]
+                for r in range(c + 1, R):
+                    P[r, c] = LD[lp[c] + r - c - 1]
+            for k in range(w):
+                rk = rcp_reg(P[k, k])
+                rD[j0 + k] = rk
+                for c in range(k + 1, w):
+                    P[c:, c] -= P[c:, k] * rk * P[c, k]
+            for c in range(w):
+                for r in range(c + 1, R):
+                    LD[lp[c] + r - c - 1] = P[r, c]
+        run_prog(self.T, "fac", term, epi, self.wg, panel)
 
     def solve(self, LD, rD, rhs_natural):
         W = np.zeros(self.N)
@@ -104,12 +136,26 @@ class TreeEmu:
             return acc - LD[a] * W[k]
 
         def ef(i, acc):
-            W[i] = rD[i] * (W[i] + acc)
+            if i >= 0:
+                W[i] = rD[i] * (W[i] + acc)
+            else:
+                W[-1 - i] += acc                 # supernode row: raw
 
         def eb(k, acc):
             W[k] = W[k] + rD[k] * acc
-        run_prog(self.T, "fwd", tf, ef, self.wg)
-        run_prog(self.T, "bwd", tf, eb, self.wg)
+
+        def pf(j0, w, R, lp):                    # qpb_pfwd
+            for k in range(w):
+                W[j0 + k] *= rD[j0 + k]
+                for c in range(k + 1, w):
+                    W[j0 + c] -= LD[lp[k] + c - k - 1] * W[j0 + k]
+
+        def pb(j0, w, R, lp):                    # qpb_pbwd
+            for k in range(w - 1, -1, -1):
+                for c in range(k):
+                    W[j0 + c] -= rD[j0 + c] * LD[lp[c] + k - c - 1] * W[j0 + k]
+        run_prog(self.T, "fwd", tf, ef, self.wg, pf)
+        run_prog(self.T, "bwd", tf, eb, self.wg, pb)
         return W[self.pinv]
 
     def products(self, pag, v, prog="mv"):
