@@ -114,7 +114,10 @@ class Plan:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
-            _lib.lib().qpb_plan_destroy(h)
+            try:
+                _lib.lib().qpb_plan_destroy(h)
+            except Exception:       # interpreter shutdown: the library may be gone
+                pass
             self._h = None
 
     @classmethod

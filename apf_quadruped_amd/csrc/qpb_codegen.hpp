@@ -34,6 +34,9 @@ struct KernelArgs {
     double abstol, sigma_d;
     long maxit;
     const void *tab = nullptr;              // tree kernel only: plan tables on the device
+    double *best = nullptr;                 // row kernel: fused argmin output {fval, index}
+    unsigned long long *part = nullptr;     //   per-wave partials
+    unsigned *ctr = nullptr;                //   arrival counter (zero between launches)
 };
 
 std::string kernel_name(const Plan &pl, const GenOptions &opt);

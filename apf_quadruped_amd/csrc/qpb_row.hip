@@ -32,6 +32,10 @@ struct qpb_args {
     long B;
     double tol, abstol, sigma_d;
     long maxit;
+    const void *tab;          // (tree kernel tables; unused here)
+    double *best;             // fused argmin (qpb_solve_best): {fval, index}, or NULL
+    unsigned long long *part; // per-wave partials {fval bits, index}
+    unsigned *ctr;            // arrival counter (zero between launches)
 };
 
 #ifndef QPB_R_TIMING
@@ -157,12 +161,66 @@ static __device__ __forceinline__ long qpb_xcd_block() {
     return (nb & 7) ? (long)b : (long)(b & 7) * (nb >> 3) + (b >> 3);
 }
 
+
+// Fused argmin of qpb_solve_best (lowest fval among optimal QPs, ties -> lowest
+// index, as qpb_argmin).  Every wave of the grid arrives once with the best of its
+// QPs: its partial goes out with agent-scope (write-through) stores, `s_waitcnt
+// vmcnt(0)` makes it visible, then an agent-scope add on the arrival counter; the
+// wave that arrives last reads every partial with agent-scope loads, reduces them
+// and writes {fval, index}, and re-arms the counter.  No cache write-back or
+// invalidate is needed (the partials never sit in a non-coherent L2 line).
+static __device__ __forceinline__ double qpb_rl64(double v, int lane) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+static __device__ __forceinline__ bool qpb_better(double va, long ia, double vb, long ib) {
+    return ia >= 0 && (ib < 0 || va < vb || (va == vb && ia < ib));
+}
+static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, double bv, long bi) {
+    const unsigned nw = gridDim.x * WPB, w = blockIdx.x * WPB + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    unsigned old = 0;
+    if (lane == 0) {
+        __hip_atomic_store(&a.part[2 * w], __builtin_bit_cast(unsigned long long, bv), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&a.part[2 * w + 1], (unsigned long long)bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        old = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old != nw - 1) return;                 // wave-uniform: not the last arrival
+    asm volatile("" ::: "memory");
+    double v = __builtin_huge_val();
+    long i = -1;
+    for (unsigned k = lane; k < nw; k += 64) {
+        const double pv = __builtin_bit_cast(double, __hip_atomic_load(&a.part[2 * k], __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT));
+        const long pi = (long)__hip_atomic_load(&a.part[2 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (qpb_better(pv, pi, v, i)) { v = pv; i = pi; }
+    }
+    for (int o = 1; o < 64; o <<= 1) {
+        const double ov = __shfl_xor(v, o, 64);
+        const long oi = __shfl_xor(i, o, 64);
+        if (qpb_better(ov, oi, v, i)) { v = ov; i = oi; }
+    }
+    if (lane == 0) {
+        a.best[0] = v;
+        a.best[1] = (double)i;
+        __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * 4 * LDS_ROW];
     const int lane = threadIdx.x & 63, row = lane >> 4, c = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long q0 = (qpb_xcd_block() * WPB + wv) * 4;
-    if (q0 >= a.B) return;                     // wave-uniform
+    if (q0 >= a.B) {                           // wave-uniform
+        if (a.best) qpb_argmin_arrive(a, __builtin_huge_val(), -1);
+        return;
+    }
 #if QPB_R_TIMING == 2
     const double t_rt0 = (double)__builtin_amdgcn_s_memrealtime(), t_cy0 = (double)__builtin_readcyclecounter();
 #endif
@@ -522,5 +580,17 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             }
 #endif
         }
+    }
+    if (a.best) {
+        // this wave's best: rows are QPs (fval / flag uniform within a row)
+        double bv = __builtin_huge_val();
+        long bi = -1;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const double v = qpb_rl64(fr[0], 16 * r);
+            const int f = __builtin_amdgcn_readlane(valid && flag == 0 ? 0 : 1, 16 * r);
+            if (f == 0 && qpb_better(v, q0 + r, bv, bi)) { bv = v; bi = q0 + r; }
+        }
+        qpb_argmin_arrive(a, bv, bi);
     }
 }

@@ -225,6 +225,31 @@ int tree_tables_on_device(qpb_plan *plan, const void **out) {
     return QPB_OK;
 }
 
+// per-(device, stream) partials + arrival counter of the fused argmin (the counter
+// is zeroed once here and re-armed by every launch's last wave; launches on one
+// stream are ordered, launches on different streams use different scratch)
+int argmin_scratch(void *stream, long nw, unsigned long long **part, unsigned **ctr) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(QPB_EHIP, "hipGetDevice failed (no GPU?)");
+    struct Scratch { void *p = nullptr; long cap = 0; };
+    static std::map<std::pair<int, void *>, Scratch> pool;
+    std::lock_guard<std::mutex> lk(g_mu);
+    Scratch &sc = pool[{dev, stream}];
+    if (sc.cap < nw) {
+        if (sc.p) {
+            (void)hipStreamSynchronize((hipStream_t)stream);
+            (void)hipFree(sc.p);
+        }
+        const long cap = std::max(nw, 4096L);
+        if (hipMalloc(&sc.p, 256 + (size_t)cap * 16) != hipSuccess) { sc = Scratch(); return fail(QPB_ENOMEM, "argmin scratch"); }
+        if (hipMemset(sc.p, 0, 256) != hipSuccess) return fail(QPB_EHIP, "argmin scratch: memset failed");
+        sc.cap = cap;
+    }
+    *ctr = (unsigned *)sc.p;
+    *part = (unsigned long long *)((char *)sc.p + 256);
+    return QPB_OK;
+}
+
 int compile_tree(qpb_plan *plan) {
     if (!plan->tree_ok) return fail(QPB_EINVAL, "plan is not eligible for the tree kernel");
     return compile_kernel(plan->tree_kname, [plan] { return generate_tree_kernel(plan->pl, plan->tree_wg, nullptr); },
@@ -327,6 +352,10 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
             qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
         }
     }
+    // beyond the wave kernel's batch range the alternative for a large KKT system
+    // is the tree kernel, which the wave kernel beats at every measured batch size
+    // (30/68/18: 1.34 vs 2.20 ms per 1 024 QPs, 9.0 vs 13.3 ms per 8 192)
+    if (plan->wave_ok && plan->large_tree) plan->wave_max_batch = -1;
     if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
     *out = plan.release();
     return QPB_OK;
@@ -448,16 +477,28 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     a.sigma_d = st->sigma_d;
     a.maxit = st->maxit;
     if (tree && (rc = qpb::tree_tables_on_device(plan, &a.tab))) return rc;
+    // qpb_solve_best on the row kernel: the argmin runs inside the solve launch
+    // (its last wave reduces the per-wave partials), saving the separate launch
+    // and the gap between two dependent launches; up to 4 096 waves
+    bool fused = false;
     void *params[] = {&a};
     const unsigned wg = (unsigned)(wave ? plan->wave_wg : tree ? plan->tree_wg : plan->gen.wg);
     const long per_block = wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup
     unsigned grid = (unsigned)((B + per_block - 1) / per_block);
     if (wave || tree) grid = (grid + 7) & ~7u;      // XCD-aware block order (qpb_xcd_block)
+    if (best && wave && plan->wave_qpw == 4 && !getenv("QPB_NO_FUSED_ARGMIN")) {
+        const long nw = (long)grid * (wg / 64);
+        if (nw <= 4096) {
+            if ((rc = qpb::argmin_scratch(stream, nw, &a.part, &a.ctr))) return rc;
+            a.best = best;
+            fused = true;
+        }
+    }
     hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, wg, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("launch: ") + hipGetErrorString(e));
     // an in-kernel "last wave reduces" argmin was measured slower than this
     // separate single-block launch (agent-coherent stores + counter tail), DESIGN.md
-    if (best) return qpb_argmin(B, fval, flag, best, stream);
+    if (best && !fused) return qpb_argmin(B, fval, flag, best, stream);
     return QPB_OK;
 }
 

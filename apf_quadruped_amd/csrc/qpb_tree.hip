@@ -29,6 +29,9 @@ struct qpb_args {
     double tol, abstol, sigma_d;
     long maxit;
     const void *tab;        // plan tables (qpb_tree.cpp Blob): u64 descriptors, then int32 tables
+    double *best;           // (row kernel's fused argmin; unused here)
+    unsigned long long *part;
+    unsigned *ctr;
 };
 
 #define NX QPB_NX

@@ -157,62 +157,71 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
     vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
     del host
     out = plan.alloc_outputs(B, device=dev)
-    best = torch.zeros(2, dtype=torch.float64, device=dev)     # {fval, index}
-    gathered = torch.empty(2 * world, dtype=torch.float64, device=dev)
+    # {fval, index} of the rank's winner, double-buffered: step i writes bests[i % 2]
+    # while step i-1's all_gather may still read the other buffer
+    bests = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]
+    gathered = [torch.empty(2 * world, dtype=torch.float64, device=dev) for _ in range(2)]
     stream = torch.cuda.current_stream(dev)
-    # one step = solve + argmin, stream-ordered (an overlapped two-stream variant
-    # was CPU-bound on the per-step event calls: 65.8 vs 50.8 us per step)
-    from apf_quadruped_amd.batch import argmin_launcher
-    solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream)
-    post = argmin_launcher(out["fval"], out["flag"], best, stream=stream)
+    # one step = qpb_solve_best: the batched solve and the argmin {fval, index}
+    # (inside the solve launch for the row kernel -- its last wave reduces the
+    # per-wave partials -- else a separate single-block launch on the same stream)
+    solves = [plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream, best=b) for b in bests]
     coll = gather and world > 1
+    works = [None, None]
 
-    def exchange():
-        # 16 B per rank; async so step i's gather overlaps step i+1's solve
-        return dist.all_gather_into_tensor(gathered, best, async_op=True)
-
-    for _ in range(warmup):
-        solve()
-        post()
+    def step(i):
+        k = i & 1
+        if works[k] is not None:
+            works[k].wait()          # stream-side: the gather that read bests[k] is done
+        solves[k]()
         if coll:
-            exchange().wait()
+            # 16 B per rank, RCCL; async so it overlaps the next step's solve
+            works[k] = dist.all_gather_into_tensor(gathered[k], bests[k], async_op=True)
+
+    for i in range(warmup):
+        step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # kernel duration: HIP events on the launch stream, around every solve
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
-    work = None
     for i in range(steps):
-        ev[i][0].record(stream)
-        solve()
-        ev[i][1].record(stream)
-        post()
-        if coll:
-            work = exchange()
-    if work is not None:
-        work.wait()
+        step(i)
+    for w in works:
+        if w is not None:
+            w.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # kernel duration: HIP events on the launch stream around each of a further
+    # kev launches (per-step event records inside the timed loop cost ~8 us of host
+    # time per step, more than the gap they measure, so they stay out of it)
+    kev = min(steps, 50)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(kev)]
+    for i in range(kev):
+        ev[i][0].record(stream)
+        solves[0]()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-    return elapsed, kern_ms, out, (gathered if coll else best.reshape(1, 2))
+    last = (steps - 1) & 1
+    return elapsed, kern_ms, out, (gathered[last] if coll else bests[last].reshape(1, 2))
 
 
 def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
     """configs[2]: 4 x 1024 QPs, one sparsity pattern per gait phase (stance4,
     trot BL+FR, trot BR+FL, crawl), bucketed into one plan each and launched
-    on one stream each; a step = all four solves (+ argmins) complete."""
+    on one stream each (qpb_solve_best: solve + argmin); a step = all four
+    complete."""
     import torch
     from apf_quadruped_amd import plans, workloads as W
-    from apf_quadruped_amd.batch import Plan, argmin_launcher
+    from apf_quadruped_amd.batch import Plan
     legs = []
     for k, name in enumerate(("stance4", "trot_blfr", "trot_brfl", "crawl_blflfr")):
         stance = W.STANCE_SETS[name]
@@ -226,8 +235,7 @@ def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
         best = torch.zeros(2, dtype=torch.float64, device=dev)
         st = torch.cuda.Stream(dev)
         legs.append(dict(name=name, plan=plan, out=out, stream=st, vals=vals,
-                         solve=plan.launcher(vals, out, per_pattern, reltol=tol, abstol=tol, stream=st),
-                         post=argmin_launcher(out["fval"], out["flag"], best, stream=st)))
+                         solve=plan.launcher(vals, out, per_pattern, reltol=tol, abstol=tol, stream=st, best=best)))
     main = torch.cuda.current_stream(dev)
 
     def step():
@@ -236,7 +244,6 @@ def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
         for L in legs:
             L["stream"].wait_event(ev)
             L["solve"]()
-            L["post"]()
         for L in legs:
             e = torch.cuda.Event()
             e.record(L["stream"])
