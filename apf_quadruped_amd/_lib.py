@@ -71,6 +71,8 @@ def lib() -> C.CDLL:
     L.qpb_solve.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp]
     L.qpb_solve_best.restype = C.c_int
     L.qpb_solve_best.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp, vp]
+    L.qpb_assemble_contact.restype = C.c_int
+    L.qpb_assemble_contact.argtypes = [vp, C.c_long, vp, vp, C.c_int, C.c_double] + [vp] * 7
     L.qpb_argmin.restype = C.c_int
     L.qpb_argmin.argtypes = [C.c_long, vp, vp, vp, vp]
     if hasattr(L, "QP_SETUP"):

@@ -216,6 +216,30 @@ class Plan:
                     iters=torch.empty(B, dtype=torch.int32, device=device),
                     fval=torch.empty(B, **f), stats=torch.empty(6 * T, **f))
 
+    def assemble_contact(self, feet, wrench, stance=0xF, mu=0.5, B=None, out=None, stream=None):
+        """On-device assembly of contact-force QPs (qpb_assemble_contact): feet
+        [tiled nv=12] and wrench [tiled nv=6] float64 device tensors -> dict of the
+        plan's tiled inputs P, A, G, c, h, b (device tensors, reused from `out`)."""
+        import torch
+        if B is None:
+            B = wrench.numel() // 6
+        B = int(B)
+        T = ntiles(B) * TILE
+        dev = wrench.device
+        if out is None:
+            f = dict(dtype=torch.float64, device=dev)
+            out = dict(P=torch.empty(self.info.nnzP * T, **f), A=torch.empty(self.info.nnzA * T, **f),
+                       G=torch.empty(self.info.nnzG * T, **f), c=torch.empty(self.n * T, **f),
+                       h=torch.empty(self.m * T, **f), b=torch.empty(self.p * T, **f))
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda a: C.c_void_p(a.data_ptr())
+        check(_lib.lib().qpb_assemble_contact(self._h, B, ptr(feet), ptr(wrench), int(stance), float(mu),
+                                              ptr(out["P"]), ptr(out["A"]), ptr(out["G"]), ptr(out["c"]),
+                                              ptr(out["h"]), ptr(out["b"]), C.c_void_p(stream.cuda_stream)),
+              "qpb_assemble_contact")
+        return out
+
     def unpack(self, out, B):
         """Device tiled outputs -> dict of host numpy arrays [B, n] etc."""
         r = dict(x=from_tiled(out["x"], B, self.n).cpu().numpy(),

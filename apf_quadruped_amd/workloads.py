@@ -75,8 +75,9 @@ def friction_block(mu: float = MU) -> np.ndarray:
                      [0.0, 0.0, -1.0]])
 
 
-def contact_terms(seed: int, qp_ids: np.ndarray):
-    """Per-QP contact Jacobian Jc [B,12,6] and desired wrench W [B,6]."""
+def contact_inputs(seed: int, qp_ids: np.ndarray):
+    """Per-QP robot terms: foot positions relative to the CoM r [B,4,3] (BR, BL,
+    FL, FR) and desired wrench W [B,6] (the inputs of qpb_assemble_contact)."""
     u = uniforms(seed, qp_ids, 19)
     h_com = 0.36 + 0.06 * u[:, 0]
     jit = (0.06 * u[:, 1:13] - 0.03).reshape(-1, 4, 3)
@@ -89,7 +90,13 @@ def contact_terms(seed: int, qp_ids: np.ndarray):
     tau = 4.0 * u[:, 16:19] - 2.0
     W = np.concatenate([ROBOT_MASS * acc[:, :2],
                         (ROBOT_MASS * (9.81 + acc[:, 2]))[:, None], tau], -1)
-    Jc = np.zeros((len(u), 12, 6))
+    return r, W
+
+
+def contact_terms(seed: int, qp_ids: np.ndarray):
+    """Per-QP contact Jacobian Jc [B,12,6] and desired wrench W [B,6]."""
+    r, W = contact_inputs(seed, qp_ids)
+    Jc = np.zeros((len(r), 12, 6))
     eye = np.eye(3)
     sk = _skew(r)
     for i in range(4):

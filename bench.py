@@ -264,6 +264,44 @@ def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
             "optimal_frac": float(np.mean([(L["out"]["flag"] == 0).float().mean().item() for L in legs]))}
 
 
+def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
+    """Config 5's per-GPU share (8 192 APF-sampled contact-force QPs) end to end on
+    the device: each step assembles the QPs from the robot terms
+    (qpb_assemble_contact: 18 doubles per QP in) and solves them
+    with the argmin (qpb_solve_best)."""
+    import torch
+    from apf_quadruped_amd import plans, workloads as W
+    from apf_quadruped_amd.batch import to_tiled
+    plan = plans.standard_plan("c1")
+    plan.compile()
+    ids = np.arange(B)
+    r, Wr = W.contact_inputs(plans.SEED + 5, ids)
+    feet = torch.from_numpy(to_tiled(r.reshape(B, 12))).to(dev)
+    wrench = torch.from_numpy(to_tiled(Wr)).to(dev)
+    vals = plan.assemble_contact(feet, wrench, stance=0xF, mu=W.MU, B=B)
+    out = plan.alloc_outputs(B, device=dev)
+    best = torch.zeros(2, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    solve = plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream, best=best)
+
+    def step():
+        plan.assemble_contact(feet, wrench, stance=0xF, mu=W.MU, B=B, out=vals, stream=stream)
+        solve()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"workload": f"configs[4] per-GPU share: {B} APF-sampled C1 QPs assembled on the device + solved + argmin",
+            "batch": B, "value": B * steps / el, "unit": "QP solves/s", "ms_per_step": el * 1e3 / steps,
+            "input_bytes_per_qp": 18 * 8, "kernel": plan.kernel_name(B),
+            "optimal_frac": float((out["flag"] == 0).float().mean().item())}
+
+
 def traffic_for(kname, B):
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
@@ -343,6 +381,7 @@ def main():
             shape_leg("controller stance QP 30/68/18 (main.cpp:1649), batch 1024",
                       lambda ids: W.controller_qp(plans.SEED + 30, ids), 1024, args.tol, dev,
                       cpu=None if args.no_cpu else (512, 16)),
+            apf_leg(args.tol, dev),
         ]
 
     if rank == 0:

@@ -132,6 +132,18 @@ int  qpb_solve_best(qpb_plan *plan, long B,
  * none -> {+inf, -1}) to out2 (device, 2 doubles; the index as a double). */
 int  qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *stream);
 
+/* On-device assembly of contact-force QPs (the controller's
+ * stance-QP force block, main.cpp:1471-1647): for QP q, feet = foot positions
+ * relative to the CoM (tiled, nv = 12: BR, BL, FL, FR, x y z each) and wrench =
+ * desired wrench W (nv = 6); stance = bitmask of the feet in contact (bit i =
+ * foot i), mu = friction coefficient.  Writes the plan's tiled inputs
+ *   P = 50 Jc Jc' + I,  c = -50 Jc W,  A = Jc',  b = W,  G = friction blocks,  h = 0
+ * with Jc,i = [I3, -[r_i]x] (zero for a swing foot).  The plan must have the
+ * pattern of such a QP (QPB_ESHAPE otherwise; checked without touching the GPU). */
+int  qpb_assemble_contact(const qpb_plan *plan, long B, const double *feet, const double *wrench,
+                          int stance, double mu, double *P, double *A, double *G,
+                          double *c, double *h, double *b, void *stream);
+
 const char *qpb_last_error(void);
 const char *qpb_version(void);
 

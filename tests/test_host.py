@@ -105,3 +105,15 @@ def test_controller_shape_keeps_one_qp_per_wave():
     d = W.controller_qp(plans.SEED + 30, [0])
     plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel="wave")
     assert plan.info.wave_ok == 1 and plan.info.wave_qpw == 1
+
+
+@pytest.mark.parametrize("name,mask,ok", [("c1", 0b1111, True), ("trot_blfr", 0b1010, True),
+                                          ("trot_brfl", 0b0101, True), ("crawl_blflfr", 0b1110, True),
+                                          ("trot_blfr", 0b1111, False), ("mpc_h10", 0b1111, False)])
+def test_assemble_contact_checks_the_plan_pattern(name, mask, ok):
+    """qpb_assemble_contact accepts exactly the plans whose P/A/G patterns are those
+    of a contact-force QP with the given stance (checked on the host, no GPU)."""
+    from apf_quadruped_amd import _lib, plans
+    p = plans.standard_plan(name)
+    rc = _lib.lib().qpb_assemble_contact(p._h, 0, None, None, mask, 0.5, *([None] * 7))
+    assert (rc == 0) == ok, _lib.lib().qpb_last_error()
