@@ -15,7 +15,7 @@ PATTERNS = [("stance4", 0b1111, False), ("trot_blfr", 0b1010, True), ("trot_brfl
 def test_assemble_contact_matches_host_assembly(name, mask, feasible, B):
     import torch
     from apf_quadruped_amd import plans, workloads as W
-    from apf_quadruped_amd.batch import to_tiled
+    from apf_quadruped_amd.batch import from_tiled, to_tiled
     seed = plans.SEED + (3 if name != "c1" else 1)
     stance = tuple(i for i in range(4) if (mask >> i) & 1)
     ids = np.arange(B)
@@ -27,9 +27,10 @@ def test_assemble_contact_matches_host_assembly(name, mask, feasible, B):
     wrench = torch.from_numpy(to_tiled(d["b"])).cuda()      # b = W (main.cpp:1580-1587)
     dev = plan.assemble_contact(feet, wrench, stance=mask, mu=W.MU, B=B)
     torch.cuda.synchronize()
-    for k in ("P", "A", "G", "c", "h", "b"):
-        got = dev[k].cpu().numpy()[:host[k].size]
-        np.testing.assert_allclose(got, host[k], rtol=1e-13, atol=1e-11, err_msg=f"{name}.{k}")
+    nv = dict(P=plan.info.nnzP, A=plan.info.nnzA, G=plan.info.nnzG, c=12, h=plan.m, b=6)
+    for k in ("P", "A", "G", "c", "h", "b"):          # the valid QPs (padding lanes are not written)
+        got = from_tiled(dev[k].cpu().numpy(), B, nv[k])
+        np.testing.assert_allclose(got, from_tiled(host[k], B, nv[k]), rtol=1e-13, atol=1e-11, err_msg=f"{name}.{k}")
     r1 = plan.unpack(plan.solve(**{k: v for k, v in dev.items()}, B=B), B)
     r2 = plan.unpack(plan.solve(**host, B=B), B)
     np.testing.assert_array_equal(r1["flag"], r2["flag"])
