@@ -352,10 +352,10 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
             qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
         }
     }
-    // beyond the wave kernel's batch range the alternative for a large KKT system
-    // is the tree kernel, which the wave kernel beats at every measured batch size
-    // (30/68/18: 1.34 vs 2.20 ms per 1 024 QPs, 9.0 vs 13.3 ms per 8 192)
-    if (plan->wave_ok && plan->large_tree) plan->wave_max_batch = -1;
+    // for a large KKT system the alternative is the tree kernel: on 30/68/18 the
+    // two tie at 1 024 QPs (1.34 vs 1.38 ms) and the tree kernel wins at 8 192
+    // (7.7 vs 9.0 ms), so the wave kernel keeps the small batches
+    if (plan->wave_ok && plan->large_tree) plan->wave_max_batch = 2048;
     if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
     *out = plan.release();
     return QPB_OK;

@@ -225,7 +225,11 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
     std::vector<Snode> sns;
     std::vector<long> sn_of(N, -1);
     const bool panels = !getenv("QPB_TREE_NOPANEL");
-    const long maxw = 48;                         // registers per lane of the panel kernels
+    // widest panel: 24 columns (48 VGPRs per lane for its register row); wider
+    // supernodes split into 24-column panels.  Measured on 30/68/18 (one 36-wide
+    // supernode): 24 -> 1.38 ms per 1 024 QPs, 48 -> 2.21 ms (VGPRs 209 vs 264)
+    long maxw = 24;
+    if (const char *e = getenv("QPB_TREE_MAXW")) maxw = std::max(2L, std::min(48L, atol(e)));
     for (long j = 0; j < N;) {
         long e = j;
         if (panels && cc[j] + 1 <= 64)
