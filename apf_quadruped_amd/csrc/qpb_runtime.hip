@@ -352,10 +352,10 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
             qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
         }
     }
-    // for a large KKT system the alternative is the tree kernel: on 30/68/18 the
-    // two tie at 1 024 QPs (1.34 vs 1.38 ms) and the tree kernel wins at 8 192
-    // (7.7 vs 9.0 ms), so the wave kernel keeps the small batches
-    if (plan->wave_ok && plan->large_tree) plan->wave_max_batch = 2048;
+    // for a large KKT system the alternative is the tree kernel: on 30/68/18 it
+    // wins at 1 024 QPs (1.26 vs 1.34 ms) and 8 192 (7.0 vs 9.0 ms), so the wave
+    // kernel keeps only small batches (a single QP: the drop-in)
+    if (plan->wave_ok && plan->large_tree) plan->wave_max_batch = 512;
     if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
     *out = plan.release();
     return QPB_OK;

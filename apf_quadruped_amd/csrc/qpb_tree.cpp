@@ -138,15 +138,23 @@ struct Blob {
     // ignore) entries beyond the program's end: wg entries of padding keep
     // those reads inside the buffer
     std::vector<int32_t> snrec;   // TI offset of every supernode record [j0, w, R, Lp[j0] .. Lp[j0+w-1]]
+    std::vector<std::vector<int32_t>> list_off;   // per program: TI offset of each panel list
+    // the panel lists of a program, right after the records: the kernel stages
+    // TI[0, QPB_PANEL_INTS) -- records and lists -- in LDS once
+    void lists(const Prog &P) {
+        list_off.emplace_back();
+        for (auto &ids : P.panels) {
+            list_off.back().push_back((int32_t)i.size());
+            for (int32_t id : ids) i.push_back(snrec[id]);
+        }
+    }
+    int nprog = 0;
     void prog(const char *name, const Prog &P0, bool wide) {
         Prog P = P0;
-        // panel lists -> int section; panel steps point at them
+        const std::vector<int32_t> &lo = list_off[nprog++];
         for (long st = 0; st < P.nsteps(); st++) {
             int32_t *m = &P.steps[4 * st];
-            if (!(m[3] & STEP_PANEL)) continue;
-            const int32_t off = (int32_t)i.size();
-            for (int32_t id : P.panels[m[0]]) i.push_back(snrec[id]);
-            m[0] = off;
+            if (m[3] & STEP_PANEL) m[0] = lo[m[0]];
         }
         macros << "#define QPB_" << name << "_NSTEPS " << P.nsteps() << "\n";
         if (wide) {
@@ -371,6 +379,8 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
         for (long w : widths) o << " X(" << w << ")";
         o << "\n";
     }
+    for (const Prog *P : {&fac, &fwd, &bwd, &mv, &obj}) bl.lists(*P);
+    o << "#define QPB_PANEL_INTS " << bl.i.size() << "\n";
     bl.prog("fac", fac, true);
     bl.prog("fwd", fwd, false);
     bl.prog("bwd", bwd, false);

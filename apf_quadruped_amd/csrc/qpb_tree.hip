@@ -262,7 +262,13 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
         asm volatile("" ::"v"(S.h), "v"(S.d[0]), "v"(S.d[1]), "v"(S.d[2]), "v"(S.d[3]), "v"(S.d[4]), "v"(S.d[5]),
                      "v"(S.d[6]), "v"(S.d[7]));
         QPB_SEG(2, "s"(0));
-        if (S.rb & (1 << 17)) panel(S.doff, S.toff);    // supernode panels of this level (list, count)
+        if (S.rb & (1 << 17)) {
+            panel(S.doff, S.toff);                      // supernode panels of this level (list, count)
+            QPB_SEG(5, "s"(0));
+#if QPB_T_TIMING == 2
+            if (threadIdx.x == 0) qpb_seg[6] += 1.0;
+#endif
+        }
 #if QPB_T_EXP != 2
         if (S.rb & (1 << 16)) qpb_bar();
 #endif
@@ -428,6 +434,8 @@ static __device__ __forceinline__ long qpb_xcd_block() {
 extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double L[LDS_QP];
     __shared__ __attribute__((aligned(16))) int MS[QPB_MS_TOTAL];      // program step tables
+    __shared__ int SN[QPB_PANEL_INTS > 0 ? QPB_PANEL_INTS : 1];       // supernode records + panel lists
+    __shared__ int PINV[NN];                                           // KKT row -> factor position
     const int t = threadIdx.x;
     const long q = qpb_xcd_block();
     if (q >= a.B) return;                        // workgroup-uniform
@@ -438,7 +446,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     const unsigned long long *__restrict__ TD = (const unsigned long long *)a.tab;
     const unsigned *__restrict__ TD32 = (const unsigned *)(TD + QPB_NDESC);
     const int *__restrict__ TI = (const int *)(TD32 + QPB_NDESC32);
-#define qpb_pinv (TI + QPB_I_pinv)
+#define qpb_pinv PINV
 #define qpb_asrc_i (TI + QPB_I_asrc_i)
 #define qpb_asrc_l (TI + QPB_I_asrc_l)
     double *__restrict__ PAG = L + O_PAG;
@@ -473,6 +481,8 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
 #if QPB_T_TIMING == 2
     if (t < 8) qpb_seg[t] = 0.0;
 #endif
+    for (int j = t; j < QPB_PANEL_INTS; j += QPB_WG) SN[j] = TI[j];
+    for (int j = t; j < NN; j += QPB_WG) PINV[j] = TI[QPB_I_pinv + j];
     for (int j = t; j < 4 * QPB_fac_NSTEPS; j += QPB_WG) MS[QPB_MS_FAC + j] = TI[QPB_I_fac_steps + j];
     for (int j = t; j < 4 * QPB_fwd_NSTEPS; j += QPB_WG) MS[QPB_MS_FWD + j] = TI[QPB_I_fwd_steps + j];
     for (int j = t; j < 4 * QPB_bwd_NSTEPS; j += QPB_WG) MS[QPB_MS_BWD + j] = TI[QPB_I_bwd_steps + j];
@@ -509,7 +519,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
                 },
                 [&](int list, int count) {
                     for (int i = threadIdx.x >> 6; i < count; i += NW) {
-                        const int *rec = TI + TI[list + i];
+                        const int *rec = SN + SN[list + i];
                         switch (rec[1]) {
 #define QPB_PF(w) case w: qpb_pfac<w>(L, rec, threadIdx.x & 63); break;
                             QPB_PANEL_WIDTHS(QPB_PF)
@@ -533,7 +543,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
                 },
                 [&](int list, int count) {
                     for (int i = threadIdx.x >> 6; i < count; i += NW) {
-                        const int *rec = TI + TI[list + i];
+                        const int *rec = SN + SN[list + i];
                         switch (rec[1]) {
 #define QPB_PF(w) case w: qpb_pfwd<w>(L, rec, threadIdx.x & 63); break;
                             QPB_PANEL_WIDTHS(QPB_PF)
@@ -549,7 +559,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
                 [&](int k, double acc, qpb_pre e) { W[k] = __builtin_fma(e.b, acc, e.a); },
                 [&](int list, int count) {
                     for (int i = threadIdx.x >> 6; i < count; i += NW) {
-                        const int *rec = TI + TI[list + i];
+                        const int *rec = SN + SN[list + i];
                         switch (rec[1]) {
 #define QPB_PF(w) case w: qpb_pbwd<w>(L, rec, threadIdx.x & 63); break;
                             QPB_PANEL_WIDTHS(QPB_PF)
@@ -758,7 +768,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
             double *st = a.stats + tile * (6 * 64) + ql;
 #if QPB_T_TIMING == 2
             st[0] = qpb_seg[0]; st[64] = qpb_seg[1]; st[128] = qpb_seg[2]; st[192] = qpb_seg[3]; st[256] = qpb_seg[4];
-            st[320] = (double)((long)__builtin_readcyclecounter() - qpb_tall);
+            st[320] = qpb_seg[5] + 1e9 * qpb_seg[6];     // panel cycles + 1e9 x panel steps
 #elif QPB_T_TIMING
             tm_all = (double)((long)__builtin_readcyclecounter() - qpb_tall);
             st[0] = tm_fac; st[64] = tm_sol; st[128] = tm_mv; st[192] = tm_all; st[256] = (double)QPB_fac_NSTEPS;

@@ -21,5 +21,9 @@ for case in (sys.argv[1:] or ["mpc_h10:1", "c1:1"]):
     r = plan.unpack(out, B)
     n = r["alpha_p"][0]
     seg = [r[k][0] / n for k in ("n_rx", "n_ry", "n_rz", "n_mu")]
+    pv = float(r["alpha_d"][0])
+    npanel = int(pv // 1e9)
+    pcyc = pv - 1e9 * npanel
     print(json.dumps(dict(case=case, steps=float(n), desc_wait=seg[0], terms=seg[1], epilogue=seg[2], barrier=seg[3],
-                          per_step=sum(seg), total=float(r["alpha_d"][0]))), flush=True)
+                          per_step=sum(seg), panel_steps=npanel, cycles_per_panel_step=pcyc / max(npanel, 1),
+                          panel_share=pcyc / (sum(seg) * n))), flush=True)
