@@ -182,6 +182,17 @@ int build_plan(Plan &pl, long n, long m, long p, int pmode,
         }
         pl.perm.assign(perm, perm + N);
         pl.ordering_kind = 0;
+    } else if (n <= 16 && p <= 16 && m <= 32) {
+        // small QPs (the contact-force shapes): z rows, y rows, then x in natural
+        // order.  Every z / y row is then a leaf (its neighbours are x rows, all
+        // later) and the x block is dense -- the elimination of the row kernel
+        // (qpb_row.hip) for every such pattern; the fill is the same as AMD's on C1
+        // (Lnz 138).  Min-degree instead puts isolated rows (the force variables of
+        // swing feet) first, which leaves the x block out of natural order.
+        for (long i = n + p; i < N; i++) pl.perm.push_back(i);
+        for (long i = n; i < n + p; i++) pl.perm.push_back(i);
+        for (long i = 0; i < n; i++) pl.perm.push_back(i);
+        pl.ordering_kind = 3;
     } else {
         pl.perm = min_degree_order(K);
         pl.ordering_kind = 1;

@@ -63,7 +63,7 @@ struct Plan {
     std::vector<Slot> K_loop;                // after updatekktmatrix (IPM loop)
     std::vector<long> perm, pinv, parent, Lp, Li;
     long lnz = 0;
-    int ordering_kind = 0;                   // 0 caller-given, 1 own min-degree, 2 identity
+    int ordering_kind = 0;                   // 0 caller-given, 1 own min-degree, 3 leaves first (z, y, x)
     std::vector<FacStep> fac;                // numeric schedule
     long fac_updates = 0, fac_divs = 0;      // op counts (flop accounting)
     uint64_t hash = 0;

@@ -77,7 +77,8 @@ typedef struct qpb_plan_info {
     long nnzP, nnzA, nnzG;       /* value counts per QP */
     long nnzK, lnz;              /* nnz of the KKT and of its L factor */
     long fac_updates, fac_divs;  /* LDL numeric op counts per factorisation */
-    int  ordering;               /* 0 caller permutation, 1 own minimum degree */
+    int  ordering;               /* 0 caller permutation, 1 own minimum degree, 3 own leaves-first
+                                    (z rows, y rows, x rows; plans with n, p <= 16, m <= 32) */
     int  exact;
     uint64_t hash;               /* pattern + permutation hash */
     int  wave_ok;                /* plan can use the wave-cooperative kernel */

@@ -52,8 +52,15 @@ def test_symbolic_matches_reference(name):
 def test_own_ordering_is_a_permutation_and_sparse():
     _, plan = _c1_plan(perm=None)
     assert sorted(plan.perm.tolist()) == list(range(38))
-    assert plan.info.ordering == 1
+    assert plan.info.ordering == 3       # small QP: leaves first (z, y, then x in natural order)
+    assert plan.perm.tolist() == list(range(18, 38)) + list(range(12, 18)) + list(range(12))
     assert plan.info.lnz <= 138          # no worse than the reference AMD order
+
+
+def test_own_ordering_of_larger_plans_is_min_degree():
+    from apf_quadruped_amd import plans
+    plan = plans.standard_plan("mpc_h10")
+    assert plan.info.ordering == 1 and sorted(plan.perm.tolist()) == list(range(380))
 
 
 def test_plan_rejects_bad_input():
@@ -86,7 +93,8 @@ def test_kernel_compiles_for_gfx950(exact, tmp_path, monkeypatch):
 
 @pytest.mark.parametrize("name,kernel,qpw", [("c1", "wave", 4), ("c1", "wave1", 1), ("c1", "auto", 4),
                                              ("c1", "auto1", 1), ("stance4", "wave", 4),
-                                             ("crawl_blflfr", "wave", 4), ("trot_blfr", "wave", 1)])
+                                             ("crawl_blflfr", "wave", 4), ("trot_blfr", "wave", 4),
+                                             ("trot_brfl", "auto", 4), ("trot_blfr", "wave1", 1)])
 def test_wave_kernel_form(name, kernel, qpw):
     """The wave kernel takes its row form (four QPs per wavefront) exactly for
     patterns whose z / y rows are all leaves with the x block in natural order
