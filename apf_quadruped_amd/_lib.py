@@ -20,6 +20,12 @@ class QpbSettings(C.Structure):
                 ("sigma_d", C.c_double)]
 
 
+class QpbIo(C.Structure):
+    """qpb_io: one member's batch of a plan group (device pointers)."""
+    _fields_ = [("B", C.c_long)] + [(k, C.c_void_p) for k in ("P", "A", "G", "c", "h", "b", "x", "y", "z", "s",
+                                                              "flag", "iters", "fval", "stats")]
+
+
 class QpbPlanInfo(C.Structure):
     _fields_ = [("n", C.c_long), ("m", C.c_long), ("p", C.c_long), ("N", C.c_long),
                 ("nnzP", C.c_long), ("nnzA", C.c_long), ("nnzG", C.c_long),
@@ -73,6 +79,15 @@ def lib() -> C.CDLL:
     L.qpb_solve_best.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp, vp]
     L.qpb_assemble_contact.restype = C.c_int
     L.qpb_assemble_contact.argtypes = [vp, C.c_long, vp, vp, C.c_int, C.c_double] + [vp] * 7
+    L.qpb_group_create.restype = C.c_int
+    L.qpb_group_create.argtypes = [C.POINTER(vp), C.POINTER(vp), C.c_int]
+    L.qpb_group_destroy.argtypes = [vp]
+    L.qpb_group_destroy.restype = None
+    L.qpb_group_source.restype = C.c_long
+    L.qpb_group_source.argtypes = [vp, C.c_char_p, C.c_long]
+    L.qpb_group_compile.argtypes = [vp]
+    L.qpb_group_solve.restype = C.c_int
+    L.qpb_group_solve.argtypes = [vp, C.POINTER(QpbIo), C.POINTER(QpbSettings), vp, vp]
     L.qpb_argmin.restype = C.c_int
     L.qpb_argmin.argtypes = [C.c_long, vp, vp, vp, vp]
     if hasattr(L, "QP_SETUP"):

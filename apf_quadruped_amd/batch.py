@@ -18,7 +18,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import QpbPlanInfo, QpbSettings, check
+from ._lib import QpbIo, QpbPlanInfo, QpbSettings, check
 
 QPB_P_FULL, QPB_P_UPPER, QPB_EXACT = 0x0, 0x1, 0x10
 QPB_KERNEL_LANE, QPB_KERNEL_WAVE, QPB_KERNEL_NOROW, QPB_KERNEL_TREE = 0x100, 0x200, 0x400, 0x800
@@ -67,7 +67,7 @@ def to_tiled(V: np.ndarray) -> np.ndarray:
 def from_tiled(flat, B: int, nv: int):
     """Inverse of to_tiled (numpy or torch): flat tiled array -> [B, nv]."""
     T = ntiles(B)
-    t = flat.reshape(T, nv, TILE)
+    t = flat[:T * nv * TILE].reshape(T, nv, TILE)     # buffers may hold spare tiles
     if hasattr(t, "permute"):
         return t.permute(0, 2, 1).reshape(T * TILE, nv)[:B]
     return t.transpose(0, 2, 1).reshape(T * TILE, nv)[:B]
@@ -245,8 +245,8 @@ class Plan:
         r = dict(x=from_tiled(out["x"], B, self.n).cpu().numpy(),
                  z=from_tiled(out["z"], B, self.m).cpu().numpy(),
                  s=from_tiled(out["s"], B, self.m).cpu().numpy(),
-                 flag=out["flag"].cpu().numpy(), iters=out["iters"].cpu().numpy(),
-                 fval=out["fval"].cpu().numpy())
+                 flag=out["flag"][:B].cpu().numpy(), iters=out["iters"][:B].cpu().numpy(),
+                 fval=out["fval"][:B].cpu().numpy())
         r["y"] = from_tiled(out["y"], B, self.p).cpu().numpy() if self.p else np.zeros((B, 0))
         if out.get("stats") is not None:
             st = from_tiled(out["stats"], B, 6).cpu().numpy()
@@ -334,6 +334,73 @@ class Plan:
             if line.startswith("#define QPB_KERNEL_NAME "):
                 return line.split()[-1]
         return src.split("(qpb_args")[0].split()[-1]
+
+
+class PlanGroup:
+    """Several row-form plans (e.g. one per gait phase) solved as ONE launch
+    (qpb_group_solve, include/qpswift_hip.h): member i's QPs run the exact code
+    of Plan.solve on plans[i], and with `best` the argmin over the concatenated
+    batch (plans[0]'s QPs first) is reduced inside the same launch."""
+
+    def __init__(self, plans):
+        L = _lib.lib()
+        self.plans = list(plans)
+        hs = (C.c_void_p * len(self.plans))(*[p._h.value for p in self.plans])
+        h = C.c_void_p()
+        check(L.qpb_group_create(C.byref(h), hs, len(self.plans)), "qpb_group_create")
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib().qpb_group_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def source(self) -> str:
+        L = _lib.lib()
+        size = L.qpb_group_source(self._h, None, 0)
+        buf = C.create_string_buffer(size + 1)
+        L.qpb_group_source(self._h, buf, size + 1)
+        return buf.value.decode()
+
+    def kernel_name(self) -> str:
+        return self.source().split("\n", 1)[0].split()[-1]
+
+    def compile(self) -> None:
+        check(_lib.lib().qpb_group_compile(self._h), "qpb_group_compile")
+
+    def launcher(self, vals, outs, Bs, reltol=1e-6, abstol=1e-6, maxit=100, sigma_d=0.0, stream=None, best=None):
+        """Zero-argument callable launching qpb_group_solve on fixed device buffers:
+        vals[i] / outs[i] as Plan.launcher's, Bs[i] QPs of member i."""
+        import torch
+        if not (len(vals) == len(outs) == len(Bs) == len(self.plans)):
+            raise ValueError("one vals / outs / B per member plan")
+        if stream is None:
+            stream = torch.cuda.current_stream()
+        ptr = lambda a: None if a is None else a.data_ptr()
+        io = (QpbIo * len(self.plans))()
+        for i, (pl, v, o, B) in enumerate(zip(self.plans, vals, outs, Bs)):
+            io[i] = QpbIo(int(B), ptr(v["P"]), ptr(v.get("A")) if pl.p else None, ptr(v["G"]), ptr(v["c"]),
+                          ptr(v["h"]), ptr(v.get("b")) if pl.p else None, ptr(o["x"]),
+                          ptr(o["y"]) if pl.p else None, ptr(o["z"]), ptr(o["s"]), ptr(o["flag"]),
+                          ptr(o["iters"]), ptr(o["fval"]), ptr(o.get("stats")))
+        st = QpbSettings(int(maxit), float(reltol), float(abstol), float(sigma_d))
+        if best is not None and (best.numel() < 2 or best.dtype != torch.float64):
+            raise ValueError("best must be a float64 device tensor of >= 2 elements")
+        args = (self._h, io, C.byref(st), None if best is None else C.c_void_p(best.data_ptr()),
+                C.c_void_p(stream.cuda_stream))
+        fn = _lib.lib().qpb_group_solve
+        keep = (vals, outs, st, best, io)
+
+        def go():
+            rc = fn(*args)
+            if rc:
+                check(rc, "qpb_group_solve")
+        go.keep = keep
+        return go
 
 
 def argmin_launcher(fval, flag, out, stream=None):

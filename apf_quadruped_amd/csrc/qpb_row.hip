@@ -21,6 +21,8 @@
 // (Auxilary.c:359-393).  Fast mode: FMA contraction, reciprocal pivots.
 #pragma clang fp contract(fast)
 
+#ifndef QPB_ROW_COMMON_DONE
+#define QPB_ROW_COMMON_DONE
 template <int V> struct qpb_ic { static constexpr int value = V; };
 
 struct qpb_args {
@@ -41,22 +43,6 @@ struct qpb_args {
 #ifndef QPB_R_TIMING
 #define QPB_R_TIMING 0    // 2: per-QP start / end (realtime, cycles), iterations, hardware ids into stats
 #endif
-
-#define NX QPB_NX
-#define NZ QPB_NZ
-#define NY QPB_NY
-#define NY1 (NY > 0 ? NY : 1)
-#define WPB (QPB_WG / 64)
-#define ZH (NZ > 16)
-// per-row LDS (doubles): staging Pd[NX*NX] Ad[NY1*NX] Gd[NZ*NX] | Tx[NX*NX]
-// (columns of -L, one contiguous run per lane) | PR[NX*NX] (-P rows) | H0s[NX*NX]
-#define EVEN(v) (((v) + 1) & ~1)
-#define OFF_A (NX * NX)
-#define OFF_G (OFF_A + NY1 * NX)
-#define OFF_T EVEN(OFF_G + NZ * NX)
-#define OFF_PR EVEN(OFF_T + NX * NX)
-#define OFF_H0 EVEN(OFF_PR + NX * NX)
-#define LDS_ROW EVEN(OFF_H0 + NX * NX)
 
 static __device__ __forceinline__ double qpb_rcp(double v) {
     double r = __builtin_amdgcn_rcp(v);
@@ -179,7 +165,7 @@ static __device__ __forceinline__ bool qpb_better(double va, long ia, double vb,
     return ia >= 0 && (ib < 0 || va < vb || (va == vb && ia < ib));
 }
 static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, double bv, long bi) {
-    const unsigned nw = gridDim.x * WPB, w = blockIdx.x * WPB + (threadIdx.x >> 6);
+    const unsigned nw = (gridDim.x * blockDim.x) >> 6, w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int lane = threadIdx.x & 63;
     unsigned old = 0;
     if (lane == 0) {
@@ -212,11 +198,31 @@ static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, doub
     }
 }
 
-extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
-    __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * 4 * LDS_ROW];
+#endif  // QPB_ROW_COMMON_DONE
+
+#ifndef QPB_ROW_COMMON_ONLY
+#define NX QPB_NX
+#define NZ QPB_NZ
+#define NY QPB_NY
+#define NY1 (NY > 0 ? NY : 1)
+#define WPB (QPB_WG / 64)
+#define ZH (NZ > 16)
+// per-row LDS (doubles): staging Pd[NX*NX] Ad[NY1*NX] Gd[NZ*NX] | Tx[NX*NX]
+// (columns of -L, one contiguous run per lane) | PR[NX*NX] (-P rows) | H0s[NX*NX]
+#define EVEN(v) (((v) + 1) & ~1)
+#define OFF_A (NX * NX)
+#define OFF_G (OFF_A + NY1 * NX)
+#define OFF_T EVEN(OFF_G + NZ * NX)
+#define OFF_PR EVEN(OFF_T + NX * NX)
+#define OFF_H0 EVEN(OFF_PR + NX * NX)
+#define LDS_ROW EVEN(OFF_H0 + NX * NX)
+
+// one logical block `lb` of the plan's batch (QPs 4 (lb WPB + wave) ..); qoff
+// offsets the indices the fused argmin reports (the plan's first QP in a group)
+static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, long qoff, double *qpb_lds) {
     const int lane = threadIdx.x & 63, row = lane >> 4, c = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long q0 = (qpb_xcd_block() * WPB + wv) * 4;
+    const long q0 = (lb * WPB + wv) * 4;
     if (q0 >= a.B) {                           // wave-uniform
         if (a.best) qpb_argmin_arrive(a, __builtin_huge_val(), -1);
         return;
@@ -589,8 +595,16 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         for (int r = 0; r < 4; r++) {
             const double v = qpb_rl64(fr[0], 16 * r);
             const int f = __builtin_amdgcn_readlane(valid && flag == 0 ? 0 : 1, 16 * r);
-            if (f == 0 && qpb_better(v, q0 + r, bv, bi)) { bv = v; bi = q0 + r; }
+            if (f == 0 && qpb_better(v, qoff + q0 + r, bv, bi)) { bv = v; bi = qoff + q0 + r; }
         }
         qpb_argmin_arrive(a, bv, bi);
     }
 }
+
+#ifndef QPB_GROUP
+extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
+    __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * 4 * LDS_ROW];
+    qpb_row_body(a, qpb_xcd_block(), 0, qpb_lds);
+}
+#endif
+#endif  // QPB_ROW_COMMON_ONLY

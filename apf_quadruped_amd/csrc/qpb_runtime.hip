@@ -517,6 +517,118 @@ int qpb_solve_best(qpb_plan *plan, long B, const double *P, const double *A, con
     return solve_impl(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, best, stream);
 }
 
+/* ---- plan groups: one launch for a mixed-pattern batch (qpb_group_*) ---- */
+
+struct qpb_group {
+    std::vector<long> p;                         // per member: equality count (A, b, y needed when > 0)
+    std::string kname, src;
+    std::shared_ptr<std::vector<char>> code;
+};
+
+namespace {
+struct GroupArgs {                               // = qpb_group_args of the generated kernel
+    qpb::KernelArgs m[qpb::QPB_GROUP_MAX];
+    long bend[qpb::QPB_GROUP_MAX];
+    long qoff[qpb::QPB_GROUP_MAX];
+};
+}  // namespace
+
+int qpb_group_create(qpb_group **out, qpb_plan *const *plans, int nplans) {
+    if (!out) return fail(QPB_EINVAL, "NULL output");
+    *out = nullptr;
+    if (!plans || nplans < 1 || nplans > qpb::QPB_GROUP_MAX)
+        return fail(QPB_EINVAL, "a group holds 1.." + std::to_string(qpb::QPB_GROUP_MAX) + " plans");
+    std::vector<const qpb::Plan *> pls;
+    auto g = std::make_unique<qpb_group>();
+    for (int i = 0; i < nplans; i++) {
+        const qpb_plan *pl = plans[i];
+        if (!pl) return fail(QPB_EINVAL, "NULL plan in group");
+        if (!pl->wave_ok || pl->wave_qpw != 4 || pl->gen.exact)
+            return fail(QPB_EINVAL, "plan " + std::to_string(i) +
+                                        " has no row-form kernel (groups need n, p <= 16, m <= 32, z/y rows leaves, fast mode)");
+        pls.push_back(&pl->pl);
+        g->p.push_back(pl->pl.p);
+    }
+    g->src = qpb::generate_row_group_kernel(pls, &g->kname);
+    *out = g.release();
+    return QPB_OK;
+}
+
+void qpb_group_destroy(qpb_group *g) { delete g; }
+
+long qpb_group_source(const qpb_group *g, char *buf, long cap) {
+    if (!g) return fail(QPB_EINVAL, "NULL group");
+    if (buf && cap > 0) {
+        long k = std::min<long>(cap - 1, (long)g->src.size());
+        std::memcpy(buf, g->src.data(), k);
+        buf[k] = 0;
+    }
+    return (long)g->src.size();
+}
+
+int qpb_group_compile(qpb_group *g) {
+    if (!g) return fail(QPB_EINVAL, "NULL group");
+    return qpb::compile_kernel(g->kname, [g] { return g->src; }, false, &g->code);
+}
+
+int qpb_group_solve(qpb_group *g, const qpb_io *io, const qpb_settings *st, double *best, void *stream) {
+    if (!g || !io) return fail(QPB_EINVAL, "NULL group or io");
+    const int nm = (int)g->p.size();
+    qpb_settings def;
+    qpb_default_settings(&def);
+    if (!st) st = &def;
+    GroupArgs ga;
+    std::memset(&ga, 0, sizeof ga);
+    long blocks = 0, qs = 0;
+    for (int i = 0; i < nm; i++) {
+        const qpb_io &b = io[i];
+        if (b.B < 0) return fail(QPB_EINVAL, "need B >= 0");
+        if (b.B > 0) {
+            if (!b.P || !b.G || !b.c || !b.h || !b.x || !b.z || !b.s || !b.flag || !b.iters || !b.fval)
+                return fail(QPB_EINVAL, "NULL data pointer (member " + std::to_string(i) + ")");
+            if (g->p[i] > 0 && (!b.A || !b.b || !b.y))
+                return fail(QPB_EINVAL, "p > 0 needs A, b and y (member " + std::to_string(i) + ")");
+        }
+        qpb::KernelArgs &a = ga.m[i];
+        a.P = b.P; a.A = b.A; a.G = b.G; a.c = b.c; a.h = b.h; a.b = b.b;
+        a.x = b.x; a.y = b.y; a.z = b.z; a.s = b.s;
+        a.flag = b.flag; a.iters = b.iters; a.fval = b.fval; a.stats = b.stats;
+        a.B = b.B;
+        a.tol = st->reltol / std::sqrt(3.0);
+        a.abstol = st->abstol;
+        a.sigma_d = st->sigma_d;
+        a.maxit = st->maxit;
+        ga.qoff[i] = qs;
+        qs += b.B;
+        blocks += (b.B + 3) / 4;                 // row form: 4 QPs per one-wave block
+        ga.bend[i] = blocks;
+    }
+    if (blocks == 0) {
+        if (best) {   // empty batch: {+inf, -1}, as qpb_argmin
+            const double none[2] = {INFINITY, -1.0};
+            if (hipMemcpyAsync(best, none, sizeof none, hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess)
+                return fail(QPB_EHIP, "group: best copy failed");
+        }
+        return QPB_OK;
+    }
+    const unsigned grid = (unsigned)((blocks + 7) & ~7L);    // XCD-aware block order (qpb_xcd_block)
+    if (best) {
+        unsigned long long *part;
+        unsigned *ctr;
+        int rc = qpb::argmin_scratch(stream, grid, &part, &ctr);
+        if (rc) return rc;
+        for (int i = 0; i < nm; i++) { ga.m[i].best = best; ga.m[i].part = part; ga.m[i].ctr = ctr; }
+    }
+    int rc = qpb_group_compile(g);
+    hipFunction_t fn;
+    if (!rc) rc = qpb::load_function(g->kname, g->code, &fn);
+    if (rc) return rc;
+    void *params[] = {&ga};
+    hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, 64, 1, 1, 0, (hipStream_t)stream, params, nullptr);
+    if (e != hipSuccess) return fail(QPB_EHIP, std::string("group launch: ") + hipGetErrorString(e));
+    return QPB_OK;
+}
+
 int qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *stream) {
     if (B < 0 || !out2 || (B > 0 && (!fval || !flag))) return fail(QPB_EINVAL, "bad argmin arguments");
     // partials live in a per-device scratch buffer (grown on demand, never freed)

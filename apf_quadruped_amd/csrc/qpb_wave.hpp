@@ -27,4 +27,8 @@ std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out);
 // with every z / y row a leaf, the x block in natural order, n, p <= 16, m <= 32.
 bool row_eligible(const Plan &pl);
 std::string generate_row_kernel(const Plan &pl, std::string *name_out);
+// One kernel for up to QPB_GROUP_MAX row-form plans (qpb_group_*): logical
+// blocks [bend[i-1], bend[i]) run member i.
+constexpr int QPB_GROUP_MAX = 16;
+std::string generate_row_group_kernel(const std::vector<const Plan *> &pls, std::string *name_out);
 }  // namespace qpb

@@ -130,10 +130,15 @@ def contact_force_qp(seed: int, qp_ids, stance=(0, 1, 2, 3), mu: float = MU,
         f = np.stack([(0.8 * u[..., 0] - 0.4) * mu * 2 * fz * 0.5,
                       (0.8 * u[..., 1] - 0.4) * mu * 2 * fz * 0.5, fz], -1)
         W = np.einsum("bfij,bfi->bj", Jc.reshape(B, 4, 3, 6), f)
+    return _contact_qp(Jc, W, stance, mu)
+
+
+def _contact_qp(Jc, W, stance, mu):
+    B = len(W)
     P = 50.0 * np.einsum("bij,bkj->bik", Jc, Jc) + np.eye(12)[None]
     c = -50.0 * np.einsum("bij,bj->bi", Jc, W)
     A = np.ascontiguousarray(np.transpose(Jc, (0, 2, 1)))
-    b = W.copy()
+    b = np.array(W, dtype=np.float64, copy=True)
     cfr = friction_block(mu)
     m = 5 * len(stance)
     G = np.zeros((B, m, 12))
@@ -141,6 +146,19 @@ def contact_force_qp(seed: int, qp_ids, stance=(0, 1, 2, 3), mu: float = MU,
         G[:, 5 * k:5 * k + 5, 3 * foot:3 * foot + 3] = cfr
     h = np.zeros((B, m))
     return dict(n=12, m=m, p=6, P=P, c=c, A=A, b=b, G=G, h=h)
+
+
+def contact_qp_from_terms(r: np.ndarray, W: np.ndarray, stance=(0, 1, 2, 3), mu: float = MU):
+    """Dense contact-force QPs from given robot terms: foot positions relative to
+    the CoM r [B,4,3] (BR, BL, FL, FR) and wrench W [B,6] (e.g. from recorded
+    traces, traces.py) -- the host restatement of qpb_assemble_contact."""
+    r = np.asarray(r, dtype=np.float64).reshape(-1, 4, 3)
+    Jc = np.zeros((len(r), 12, 6))
+    sk = _skew(r)
+    for i in stance:
+        Jc[:, 3 * i:3 * i + 3, 0:3] = np.eye(3)
+        Jc[:, 3 * i:3 * i + 3, 3:6] = -sk[:, i]
+    return _contact_qp(Jc, np.asarray(W, dtype=np.float64), stance, mu)
 
 
 def mpc_qp(seed: int, qp_ids, horizon: int = 10, mu: float = MU):

@@ -216,12 +216,14 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
 
 def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
     """configs[2]: 4 x 1024 QPs, one sparsity pattern per gait phase (stance4,
-    trot BL+FR, trot BR+FL, crawl), bucketed into one plan each and launched
-    on one stream each (qpb_solve_best: solve + argmin); a step = all four
-    complete."""
+    trot BL+FR, trot BR+FL, crawl), bucketed into one plan each.  A step is ONE
+    launch of the plans' group kernel (qpb_group_solve: every pattern's QPs in
+    their own blocks + the argmin over all 4 096 in the same launch).  For
+    comparison, `per_plan_streams` times the same work as four qpb_solve_best
+    launches on four streams (joined by events)."""
     import torch
     from apf_quadruped_amd import plans, workloads as W
-    from apf_quadruped_amd.batch import Plan
+    from apf_quadruped_amd.batch import Plan, PlanGroup
     legs = []
     for k, name in enumerate(("stance4", "trot_blfr", "trot_brfl", "crawl_blflfr")):
         stance = W.STANCE_SETS[name]
@@ -237,8 +239,13 @@ def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
         legs.append(dict(name=name, plan=plan, out=out, stream=st, vals=vals,
                          solve=plan.launcher(vals, out, per_pattern, reltol=tol, abstol=tol, stream=st, best=best)))
     main = torch.cuda.current_stream(dev)
+    group = PlanGroup([L["plan"] for L in legs])
+    group.compile()
+    gbest = torch.zeros(2, dtype=torch.float64, device=dev)
+    gsolve = group.launcher([L["vals"] for L in legs], [L["out"] for L in legs], [per_pattern] * len(legs),
+                            reltol=tol, abstol=tol, stream=main, best=gbest)
 
-    def step():
+    def streams_step():
         ev = torch.cuda.Event()
         ev.record(main)
         for L in legs:
@@ -249,19 +256,75 @@ def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
             e.record(L["stream"])
             main.wait_event(e)
 
+    def timed(step):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    el_streams = timed(streams_step)
+    el = timed(gsolve)
+    # kernel duration of the group launch (events on its stream, outside the timed loop)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+    for a, b in evs:
+        a.record(main)
+        gsolve()
+        b.record(main)
+    torch.cuda.synchronize()
+    kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    B = per_pattern * len(legs)
+    return {"batch": B, "patterns": [L["name"] for L in legs], "value": B * steps / el,
+            "ms_per_step": el * 1e3 / steps, "kernel": group.kernel_name(), "kernel_ms": kms,
+            "member_kernels": [L["plan"].kernel_name(per_pattern) for L in legs],
+            "kkt_N": [L["plan"].info.N for L in legs],
+            "per_plan_streams": {"value": B * steps / el_streams, "ms_per_step": el_streams * 1e3 / steps},
+            "optimal_frac": float(np.mean([(L["out"]["flag"] == 0).float().mean().item() for L in legs]))}
+
+
+def trace_leg(tol, dev, steps=20, warmup=3):
+    """Recorded Gazebo traces (traces.py): every logged step of
+    the reference's DogBot runs with >= 2 feet on the ground, as contact-force QPs
+    assembled on the device from the recorded foot positions / CoM wrench
+    (qpb_assemble_contact, outside the timed loop) and solved as ONE group launch
+    (one member per stance set) + argmin.  Real gaits include infeasible
+    two-foot phases: those QPs run to maxit (100 iterations), as in qpSWIFT."""
+    import torch
+    from apf_quadruped_amd import traces, workloads as W
+    from apf_quadruped_amd.batch import PlanGroup, to_tiled
+    batches = traces.stance_batches()
+    plans_ = traces.stance_plans(batches)
+    vals, outs, Bs = [], [], []
+    for (mask, r, Wr), plan in zip(batches, plans_):
+        B = len(r)
+        feet = torch.from_numpy(to_tiled(r.reshape(B, 12))).to(dev)
+        wrench = torch.from_numpy(to_tiled(Wr)).to(dev)
+        vals.append(plan.assemble_contact(feet, wrench, stance=mask, mu=W.MU, B=B))
+        outs.append(plan.alloc_outputs(B, device=dev))
+        Bs.append(B)
+    grp = PlanGroup(plans_)
+    grp.compile()
+    best = torch.zeros(2, dtype=torch.float64, device=dev)
+    go = grp.launcher(vals, outs, Bs, reltol=tol, abstol=tol, best=best)
     for _ in range(warmup):
-        step()
+        go()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        go()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    B = per_pattern * len(legs)
-    return {"batch": B, "patterns": [L["name"] for L in legs], "value": B * steps / el,
-            "ms_per_step": el * 1e3 / steps, "kernels": [L["plan"].kernel_name(per_pattern) for L in legs],
-            "kkt_N": [L["plan"].info.N for L in legs],
-            "optimal_frac": float(np.mean([(L["out"]["flag"] == 0).float().mean().item() for L in legs]))}
+    flags = torch.cat([o["flag"][:B] for o, B in zip(outs, Bs)])
+    iters = torch.cat([o["iters"][:B] for o, B in zip(outs, Bs)]).float()
+    Bt = sum(Bs)
+    return {"workload": f"recorded Gazebo traces: {Bt} logged steps of 5 DogBot runs, {len(Bs)} stance sets, one group launch",
+            "batch": Bt, "value": Bt * steps / el, "unit": "QP solves/s", "ms_per_step": el * 1e3 / steps,
+            "kernel": grp.kernel_name(), "stance_sets": [int(b[0]) for b in batches],
+            "optimal_frac": float((flags == 0).float().mean().item()), "mean_iters": float(iters.mean().item()),
+            "max_iters": int(iters.max().item())}
 
 
 def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
@@ -361,7 +424,7 @@ def main():
         del outl
 
     # configs[2]: 4 096 QPs across the 4 gait contact patterns (mixed KKT sparsity):
-    # one plan per pattern, the four launches on four HIP streams
+    # one plan per pattern, all four in one group launch
     mixed = None
     if rank == 0 and world == 1 and args.mixed:
         mixed = mixed_patterns_leg(args.tol, dev)
@@ -382,6 +445,7 @@ def main():
                       lambda ids: W.controller_qp(plans.SEED + 30, ids), 1024, args.tol, dev,
                       cpu=None if args.no_cpu else (512, 16)),
             apf_leg(args.tol, dev),
+            trace_leg(args.tol, dev),
         ]
 
     if rank == 0:

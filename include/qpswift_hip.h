@@ -145,6 +145,31 @@ int  qpb_assemble_contact(const qpb_plan *plan, long B, const double *feet, cons
                           int stance, double mu, double *P, double *A, double *G,
                           double *c, double *h, double *b, void *stream);
 
+/* ---- plan groups: one launch for a batch of mixed sparsity patterns ----
+ * The APF planner's candidates differ in their stance sets (gait phases), i.e.
+ * in their KKT patterns (configs[2]).  A group fuses up to 16 row-form plans
+ * (qpb_plan_info.wave_qpw == 4: n, p <= 16, m <= 32, e.g. every contact-force
+ * pattern) into ONE kernel: member i's QPs run in their own blocks with exactly
+ * the code of qpb_solve on that plan (bit-identical results), and with best
+ * != NULL the argmin over the whole concatenated batch (member 0's QPs first,
+ * then member 1's, ...) is reduced inside the same launch.  Replaces one
+ * QP_SETUP_dense + QP_SOLVE per candidate (qpSWIFT.c:260-456, 473-644) for a
+ * mixed batch.  The plans may be destroyed after qpb_group_create. */
+typedef struct qpb_group qpb_group;
+typedef struct qpb_io {          /* one member's batch: DEVICE pointers, tiled SoA as qpb_solve */
+    long B;
+    const double *P, *A, *G, *c, *h, *b;
+    double *x, *y, *z, *s;
+    int *flag, *iters;
+    double *fval, *stats;        /* stats may be NULL */
+} qpb_io;
+int  qpb_group_create(qpb_group **group, qpb_plan *const *plans, int nplans);
+void qpb_group_destroy(qpb_group *group);
+long qpb_group_source(const qpb_group *group, char *buf, long cap);
+int  qpb_group_compile(qpb_group *group);
+/* io[nplans]; best: DEVICE {fval, global index} or NULL.  Asynchronous on stream. */
+int  qpb_group_solve(qpb_group *group, const qpb_io *io, const qpb_settings *st, double *best, void *stream);
+
 const char *qpb_last_error(void);
 const char *qpb_version(void);
 
