@@ -40,8 +40,22 @@ struct qpb_args {
     unsigned *ctr;            // arrival counter (zero between launches)
 };
 
+// Experiment knobs.  Each of ZF128 / AADPP alone was measured correct (and ~1 %
+// faster, scripts/gpu_rowbisect.sh), but the build with all three knobs on
+// faulted on the GPU (illegal address, cause not found), so both stay off.
+#ifndef QPB_R_ZF128
+#define QPB_R_ZF128 0     // zero-fill the staging area with 16-byte LDS stores
+#endif
+#ifndef QPB_R_AADPP
+#define QPB_R_AADPP 0     // 1e7 A'A of H0 by DPP broadcasts (1) or LDS reads (0)
+#endif
+#ifndef QPB_R_LATEFAC
+#define QPB_R_LATEFAC 1   // factor after the exit test (0: before it, overlapping the reductions)
+#endif
 #ifndef QPB_R_TIMING
-#define QPB_R_TIMING 0    // 2: per-QP start / end (realtime, cycles), iterations, hardware ids into stats
+#define QPB_R_TIMING 0    // 2: per-QP start / end (realtime, cycles), iterations, hardware ids into stats;
+                          // 3: cycles per phase (H0 + setup solve, residuals, factor, predictor,
+                          //    corrector + tail, staging) into stats
 #endif
 
 static __device__ __forceinline__ double qpb_rcp(double v) {
@@ -223,6 +237,13 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     const int lane = threadIdx.x & 63, row = lane >> 4, c = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long q0 = (lb * WPB + wv) * 4;
+#if QPB_R_TIMING == 3
+    double tph[6] = {0, 0, 0, 0, 0, 0};
+    long tcy = (long)__builtin_readcyclecounter();
+#define QPB_TM(k) { const long t2_ = (long)__builtin_readcyclecounter(); tph[k] += (double)(t2_ - tcy); tcy = t2_; }
+#else
+#define QPB_TM(k)
+#endif
     if (q0 >= a.B) {                           // wave-uniform
         if (a.best) qpb_argmin_arrive(a, __builtin_huge_val(), -1);
         return;
@@ -282,7 +303,12 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #else
     const double by = 0.0;
 #endif
+#if QPB_R_ZF128
+    for (int k = 2 * c; k < OFF_T; k += 32)
+        *reinterpret_cast<double2 *>(Ls + k) = double2{0.0, 0.0};   // 16-byte stores (OFF_T, LDS_ROW even)
+#else
     for (int k = c; k < OFF_T; k += 16) Ls[k] = 0.0;
+#endif
     qpb_wsync();
 #pragma unroll
     for (int u = 0; u < NPL; u++) {
@@ -296,6 +322,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     for (int u = 0; u < NAL; u++)
         if (iA[u] >= 0) Ls[OFF_A + iA[u]] = vA[u];
     qpb_wsync();
+    QPB_TM(5);    // staging: global loads + LDS scatter
     const double *Pd = Ls, *Ad = Ls + OFF_A, *Gd = Ls + OFF_G;
     double *Tx = Ls + OFF_T, *PR = Ls + OFF_PR, *H0s = Ls + OFF_H0;
     // Pd[j*NX+i] = P(i,j) (both triangles); Ad[j*NY+l] = A(l,j); Gd[j*NZ+r] = G(r,j)
@@ -321,11 +348,22 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #pragma unroll
         for (int j = 0; j < NX; j++) {
             nP[j] = -Pd[j * NX + ix];
-            double v = ix <= j ? Pd[j * NX + ix] : Pd[ix * NX + j];
+            H0[j] = ix <= j ? Pd[j * NX + ix] : Pd[ix * NX + j];
+#if !QPB_R_AADPP
 #pragma unroll
-            for (int l = 0; l < NY; l++) v = __builtin_fma(Ad[ix * NY + l], -RDY * Ad[j * NY + l], v);
-            H0[j] = v;
+            for (int l = 0; l < NY; l++) H0[j] = __builtin_fma(Ad[ix * NY + l], -RDY * Ad[j * NY + l], H0[j]);
+#endif
         }
+#if QPB_R_AADPP
+        // += 1e7 A(l,j) A(l,c): row lane j's 1e7 A(l,j) by DPP broadcast (no LDS
+        // reads); per H0[j] the same fma chain over l as the factor's reference order
+#pragma unroll
+        for (int l = 0; l < NY; l++) {
+            const double qs = RDY * nAc[l];      // 1e7 A(l,c)
+            qpb_fence(qs);
+            qpb_for<0, NX>([&](auto jc) { qpb_fx<decltype(jc)::value>(H0[decltype(jc)::value], qs, -nAc[l]); });
+        }
+#endif
         if (isx) {
 #pragma unroll
             for (int j = 0; j < NX; j++) { PR[c * NX + j] = nP[j]; H0s[c * NX + j] = H0[j]; }
@@ -333,6 +371,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         qpb_wsync();
     }
 
+    QPB_TM(0);
     double H[NX], rDd = 0.0;
     // factor with z diagonal kd: H = H0 + G' diag(w) G, w = -1/regularise(kd),
     // then the LDL' of H (rows of -L in H, 1/D in rDd), -L transposed into Lt
@@ -430,6 +469,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         }
         // updatekktmatrix (Auxilary.c:211-215): z diagonal -s/z (-I at setup, s = z = 1)
         const double rzi0 = qpb_rcp(z0), rzi1 = qpb_rcp(z1);
+        const double rsi0 = __builtin_amdgcn_rcp(s0), rsi1 = __builtin_amdgcn_rcp(s1);   // step length
         const double kd0 = isz0 ? -s0 * rzi0 : -1.0, kd1 = isz1 ? -s1 * rzi1 : -1.0;
         const double w0 = -qpb_rcp_reg(kd0), w1 = -qpb_rcp_reg(kd1);
         // residuals (Auxilary.c:745-786)
@@ -459,9 +499,14 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                          (isz0 ? s0 * z0 : 0.0) + (isz1 ? s1 * z1 : 0.0)};
         qpb_rsum<4>(red);
         const double sz = red[3];
+        const double rsz = qpb_rcp(sz);            // formrho's 1 / s'z, off the predictor's chain
+        QPB_TM(1);
+#if !QPB_R_LATEFAC
         // the factor does not depend on the residuals: formed before the exit
         // test (wasted on a row's last iteration), overlapping the reductions
         factor(w0, w1);
+        QPB_TM(2);
+#endif
         bool pc = true;
         double mu = 0.0;
         if (it >= 0) {
@@ -482,13 +527,17 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             mu = mu_it;
             pc = sigma > a.sigma_d;
         }
+#if QPB_R_LATEFAC
+        // factor after the exit test: the wave's last pass skips it
+        factor(w0, w1);
+        QPB_TM(2);
+#endif
         if (!pc) sigma = a.sigma_d;
         double cc0 = sigma * mu, cc1 = sigma * mu;
         double dx, dy, dz0, dz1, dsl0, dsl1;
         auto step_length = [&]() {
             // alpha = min over d < 0 of v/(-d) == 1 / max(-d/v); 1 if none (Auxilary.c:359-393)
-            double bm[2] = {__builtin_fmax(isz0 ? -dsl0 * __builtin_amdgcn_rcp(s0) : 0.0,
-                                           isz1 ? -dsl1 * __builtin_amdgcn_rcp(s1) : 0.0),
+            double bm[2] = {__builtin_fmax(isz0 ? -dsl0 * rsi0 : 0.0, isz1 ? -dsl1 * rsi1 : 0.0),
                             __builtin_fmax(isz0 ? -dz0 * rzi0 : 0.0, isz1 ? -dz1 * rzi1 : 0.0)};
             bm[0] = __builtin_fmax(bm[0], 0.0);
             bm[1] = __builtin_fmax(bm[1], 0.0);
@@ -514,6 +563,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             if (!isz0) { s0 = 1.0; z0 = 1.0; }
             if (!isz1) { s1 = 1.0; z1 = 1.0; }
             it = 0;
+            QPB_TM(0);
             continue;
         }
         if (qpb_any(act && pc)) {
@@ -525,7 +575,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             double rr[1] = {(isz0 ? (s0 + ap * dsl0) * (z0 + ad * dz0) : 0.0) +
                             (isz1 ? (s1 + ap * dsl1) * (z1 + ad * dz1) : 0.0)};
             qpb_rsum<1>(rr);
-            const double rho = rr[0] * qpb_rcp(sz);     // formrho
+            const double rho = rr[0] * rsz;             // formrho
             const double r1 = 1 > rho ? rho : 1;
             const double cube = r1 * r1 * r1;
             if (pc) {
@@ -534,6 +584,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 cc1 = __builtin_fma(-dsl1, dz1, sigma * mu);
             }
         }
+        QPB_TM(3);
         // corrector / centering (kktsolve_2, Auxilary.c:524-564)
         solve(w0, w1, rx, ry, __builtin_fma(-cc0, rzi0, rz0 + s0), __builtin_fma(-cc1, rzi1, rz1 + s1), dx, dy, dz0,
               dz1);
@@ -549,6 +600,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             if (isz1) { s1 = __builtin_fma(dsl1, ap, s1); z1 = __builtin_fma(dz1, ad, z1); }
         }
         it++;
+        QPB_TM(4);
     }
     double fr[1] = {fv};
     qpb_rsum<1>(fr);
@@ -570,6 +622,13 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             a.flag[q] = flag;
             a.iters[q] = (int)itq;
             a.fval[q] = fr[0];
+#if QPB_R_TIMING == 3
+            QPB_TM(4);
+            if (a.stats) {
+                double *o = a.stats + tile * 384 + ql;
+                for (int k = 0; k < 6; k++) o[64 * k] = tph[k];
+            }
+#else
             if (a.stats && QPB_R_TIMING != 2) {
                 double *o = a.stats + tile * 384 + ql;
                 o[0] = __builtin_sqrt(st_rx2); o[64] = __builtin_sqrt(st_ry2); o[128] = __builtin_sqrt(st_rz2);
@@ -585,6 +644,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 o[320] = (double)hwid + 4294967296.0 * (double)(xcc & 0xf);
             }
 #endif
+#endif  // QPB_R_TIMING == 3
         }
     }
     if (a.best) {
@@ -607,4 +667,5 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     qpb_row_body(a, qpb_xcd_block(), 0, qpb_lds);
 }
 #endif
+#undef QPB_TM
 #endif  // QPB_ROW_COMMON_ONLY
