@@ -8,8 +8,9 @@
 //     c = -50 Jc W                   (main.cpp:1573)
 //     A = Jc',  b = W                (main.cpp:1580-1587)
 //     G = blkdiag(cfr of the stance feet), h = 0   (main.cpp:1603-1625)
-// qpb_assemble_contact evaluates this for B QPs at once, one thread per QP, from
-// 18 doubles per QP (foot positions relative to the CoM and the desired wrench),
+// qpb_assemble_contact evaluates this for B QPs at once -- one lane per (QP, output
+// value), the tile's 18 input doubles per QP (foot positions relative to the CoM
+// and the desired wrench) staged in LDS --
 // writing straight into the plan's tiled SoA input arrays -- so APF / footstep
 // samples generated on the device never round-trip through the host.
 #include <hip/hip_runtime.h>
@@ -33,63 +34,71 @@ struct AsmMap {
     double mu;
 };
 
-// J(u, j) of the contact Jacobian (12 x 6) for foot positions r (4 x 3)
-__device__ __forceinline__ double qpb_jc(const double *r, int stance, int u, int j) {
+// J(u, j) of the contact Jacobian (12 x 6) of QP lane `ql`, foot positions in
+// LDS (sr[3 i + a][ql]); u, j are wave-uniform, so every branch is uniform
+__device__ __forceinline__ double qpb_jc(const double (*sr)[64], int ql, int stance, int u, int j) {
     const int i = u / 3, a = u - 3 * i;
     if (!((stance >> i) & 1)) return 0.0;
     if (j < 3) return a == j ? 1.0 : 0.0;
-    const double rx = r[3 * i], ry = r[3 * i + 1], rz = r[3 * i + 2];
     // -[r]x, row a, column j - 3
     const int k = j - 3;
-    if (a == 0) return k == 0 ? 0.0 : (k == 1 ? rz : -ry);
-    if (a == 1) return k == 0 ? -rz : (k == 1 ? 0.0 : rx);
-    return k == 0 ? ry : (k == 1 ? -rx : 0.0);
+    if (a == k) return 0.0;
+    const int o = 3 - a - k;                  // the remaining axis
+    const double v = sr[3 * i + o][ql];
+    // -[r]x = [[0, rz, -ry], [-rz, 0, rx], [ry, -rx, 0]]
+    return ((a + 1) % 3 == k) ? v : -v;
 }
 
+// One block per tile of 64 QPs and slot chunk (blockIdx.y): the tile's foot
+// positions and wrenches are staged in LDS once, then wave g of the block writes
+// output slots s = blockIdx.y * 4 + g, + 4 gridDim.y, ... of all 64 QPs -- every
+// store a coalesced 512-B row of the tiled layout.  Slots: P values, A, G, c, h, b.
 __global__ void __launch_bounds__(256) qpb_assemble_contact_k(long B, const double *__restrict__ feet,
                                                               const double *__restrict__ wrench, AsmMap mp,
                                                               double *__restrict__ P, double *__restrict__ A,
                                                               double *__restrict__ G, double *__restrict__ c,
                                                               double *__restrict__ h, double *__restrict__ b) {
-    const long q = (long)blockIdx.x * 256 + threadIdx.x;
-    if (q >= B) return;
-    const long tile = q >> 6;
-    const int ql = (int)(q & 63);
-    double r[12], W[6], J[12][6];
-#pragma unroll
-    for (int j = 0; j < 12; j++) r[j] = feet[tile * (12 * 64) + j * 64 + ql];
-#pragma unroll
-    for (int j = 0; j < 6; j++) W[j] = wrench[tile * (6 * 64) + j * 64 + ql];
-#pragma unroll
-    for (int u = 0; u < 12; u++)
-#pragma unroll
-        for (int j = 0; j < 6; j++) J[u][j] = qpb_jc(r, mp.stance, u, j);
-    for (int k = 0; k < mp.nP; k++) {
-        const int u = mp.Pr[k], v = mp.Pc[k];
-        double d = 0.0;
-        for (int j = 0; j < 6; j++) d += J[u][j] * J[v][j];
-        P[tile * ((long)mp.nP * 64) + k * 64 + ql] = 50.0 * d + (u == v ? 1.0 : 0.0);
+    __shared__ double sr[12][64], sw[6][64];
+    const long tile = blockIdx.x;
+    const int ql = threadIdx.x & 63, g = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 18 * 64; i += 256) {
+        const int j = i >> 6, l = i & 63;
+        if (j < 12) sr[j][l] = feet[tile * (12 * 64) + i];
+        else sw[j - 12][l] = wrench[tile * (6 * 64) + (i - 12 * 64)];
     }
-    for (int k = 0; k < mp.nA; k++) A[tile * ((long)mp.nA * 64) + k * 64 + ql] = J[mp.Ac[k]][mp.Ar[k]];
-    for (int k = 0; k < mp.nG; k++) {
-        const int row = mp.Gr[k], col = mp.Gc[k], blk = row / 5, t = row - 5 * blk;
-        const int j = col - 3 * mp.foot_of[blk];
-        // cfr (main.cpp:1610-1615): t1 - mu n, t2 - mu n, -t1 - mu n, -t2 - mu n, -n
-        double v = 0.0;
-        if (j == 2) v = t == 4 ? -1.0 : -mp.mu;
-        else if (j == 0) v = t == 0 ? 1.0 : (t == 2 ? -1.0 : 0.0);
-        else if (j == 1) v = t == 1 ? 1.0 : (t == 3 ? -1.0 : 0.0);
-        G[tile * ((long)mp.nG * 64) + k * 64 + ql] = v;
+    __syncthreads();
+    if (tile * 64 + ql >= B) return;
+    const int oA = mp.nP, oG = oA + mp.nA, oc = oG + mp.nG, oh = oc + 12, ob = oh + mp.m, S = ob + 6;
+    for (int s = blockIdx.y * 4 + g; s < S; s += gridDim.y * 4) {
+        if (s < oA) {
+            const int u = mp.Pr[s], v = mp.Pc[s];
+            double d = 0.0;
+            for (int j = 0; j < 6; j++) d += qpb_jc(sr, ql, mp.stance, u, j) * qpb_jc(sr, ql, mp.stance, v, j);
+            P[tile * ((long)mp.nP * 64) + s * 64 + ql] = 50.0 * d + (u == v ? 1.0 : 0.0);
+        } else if (s < oG) {
+            const int k = s - oA;
+            A[tile * ((long)mp.nA * 64) + k * 64 + ql] = qpb_jc(sr, ql, mp.stance, mp.Ac[k], mp.Ar[k]);
+        } else if (s < oc) {
+            const int k = s - oG;
+            const int row = mp.Gr[k], col = mp.Gc[k], blk = row / 5, t = row - 5 * blk;
+            const int j = col - 3 * mp.foot_of[blk];
+            // cfr (main.cpp:1610-1615): t1 - mu n, t2 - mu n, -t1 - mu n, -t2 - mu n, -n
+            double v = 0.0;
+            if (j == 2) v = t == 4 ? -1.0 : -mp.mu;
+            else if (j == 0) v = t == 0 ? 1.0 : (t == 2 ? -1.0 : 0.0);
+            else if (j == 1) v = t == 1 ? 1.0 : (t == 3 ? -1.0 : 0.0);
+            G[tile * ((long)mp.nG * 64) + k * 64 + ql] = v;
+        } else if (s < oh) {
+            const int u = s - oc;
+            double d = 0.0;
+            for (int j = 0; j < 6; j++) d += qpb_jc(sr, ql, mp.stance, u, j) * sw[j][ql];
+            c[tile * (12 * 64) + u * 64 + ql] = -50.0 * d;
+        } else if (s < ob) {
+            h[tile * ((long)mp.m * 64) + (s - oh) * 64 + ql] = 0.0;
+        } else {
+            b[tile * (6 * 64) + (s - ob) * 64 + ql] = sw[s - ob][ql];
+        }
     }
-#pragma unroll
-    for (int u = 0; u < 12; u++) {
-        double d = 0.0;
-        for (int j = 0; j < 6; j++) d += J[u][j] * W[j];
-        c[tile * (12 * 64) + u * 64 + ql] = -50.0 * d;
-    }
-    for (int k = 0; k < mp.m; k++) h[tile * ((long)mp.m * 64) + k * 64 + ql] = 0.0;
-#pragma unroll
-    for (int j = 0; j < 6; j++) b[tile * (6 * 64) + j * 64 + ql] = W[j];
 }
 
 // Structural pattern of a generic contact-force QP for `stance` (the exact zeros
@@ -170,9 +179,10 @@ extern "C" int qpb_assemble_contact(const qpb_plan *plan, long B, const double *
         if ((stance >> i) & 1) mp.foot_of[k++] = (signed char)i;
     if (B == 0) return QPB_OK;
     if (!feet || !wrench || !P || !A || !G || !c || !h || !b) return qpb::set_error(QPB_EINVAL, "NULL data pointer");
-    const unsigned grid = (unsigned)((B + 255) / 256);
-    hipLaunchKernelGGL(qpb_assemble_contact_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, feet, wrench, mp, P,
-                       A, G, c, h, b);
+    // one block per 64-QP tile x 4 slot chunks (16 waves share a tile's ~190 slots)
+    const unsigned tiles = (unsigned)((B + 63) / 64);
+    hipLaunchKernelGGL(qpb_assemble_contact_k, dim3(tiles, 4), dim3(256), 0, (hipStream_t)stream, B, feet, wrench, mp,
+                       P, A, G, c, h, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return qpb::set_error(QPB_EHIP, (std::string("assemble: ") + hipGetErrorString(e)).c_str());
     return QPB_OK;
