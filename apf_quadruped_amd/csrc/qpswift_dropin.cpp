@@ -76,6 +76,7 @@ struct Priv {
     hipStream_t stream = nullptr;
     double *dmem = nullptr;   // tiled inputs/outputs + packed staging
     double *hmem = nullptr;   // pinned host staging: packed inputs, packed outputs
+    double *zmem = nullptr, *zdev = nullptr;   // zero-copy slab (host / device address)
     long nP = 0, nA = 0, nG = 0, nin = 0, nout = 0;
     long oP = 0, oA = 0, oG = 0, oc = 0, oh = 0, ob = 0, ox = 0, oy = 0, oz = 0, os = 0, ost = 0, ofv = 0,
          oin = 0, oout = 0, ototal = 0;
@@ -307,9 +308,27 @@ struct Workspace {
     hipStream_t stream = nullptr;
     double *dmem = nullptr;
     double *hmem = nullptr;
-    long dcap = 0, hcap = 0;   // doubles
+    double *zmem = nullptr;    // zero-copy slab: fine-grained pinned host memory the kernel reads / writes
+    double *zdev = nullptr;    //   its device-side address
+    long dcap = 0, hcap = 0, zcap = 0;   // doubles
 };
+
+// QP_SOLVE moves one QP's data either by zero copy (default for the fast kernels:
+// the tiled slab lives in pinned, device-mapped host memory, so a solve is one
+// kernel launch + one synchronisation; C1 per tick 51 -> 41 us) or staged
+// (QPSWIFT_HIP_STAGED=1, and always for the exact lane kernel, which re-reads its
+// inputs every iteration -- over the host link that costs more than the copies:
+// H2D copy, scatter kernel, solve, gather kernel, D2H copy).
+bool zero_copy_enabled() {
+    static const bool z = [] {
+        const char *e = std::getenv("QPSWIFT_HIP_STAGED");
+        return !(e && e[0] == '1');
+    }();
+    return z;
+}
 thread_local std::map<int, Workspace> t_ws;
+
+bool zero_copy(const Priv &v) { return zero_copy_enabled() && !v.plan->gen.exact; }
 
 int ensure_device(Priv &v, const QP &q) {
     int ndev = 0;
@@ -339,7 +358,7 @@ int ensure_device(Priv &v, const QP &q) {
         w.stream = nullptr;
         return qpb::set_error(QPB_EHIP, "QP_SOLVE: stream creation failed");
     }
-    if (w.dcap < v.ototal) {
+    if (!zero_copy(v) && w.dcap < v.ototal) {
         if (w.dmem) (void)hipFree(w.dmem);
         w.dcap = 0;
         if (hipMalloc((void **)&w.dmem, sizeof(double) * (size_t)v.ototal) != hipSuccess) {
@@ -349,7 +368,7 @@ int ensure_device(Priv &v, const QP &q) {
         w.dcap = v.ototal;
     }
     const long hneed = v.nin + v.nout + 1;
-    if (w.hcap < hneed) {
+    if (!zero_copy(v) && w.hcap < hneed) {
         if (w.hmem) (void)hipHostFree(w.hmem);
         w.hcap = 0;
         if (hipHostMalloc((void **)&w.hmem, sizeof(double) * (size_t)hneed, hipHostMallocDefault) != hipSuccess) {
@@ -358,10 +377,80 @@ int ensure_device(Priv &v, const QP &q) {
         }
         w.hcap = hneed;
     }
+    if (zero_copy(v) && w.zcap < v.ototal) {
+        if (w.zmem) (void)hipHostFree(w.zmem);
+        w.zcap = 0;
+        w.zdev = nullptr;
+        if (hipHostMalloc((void **)&w.zmem, sizeof(double) * (size_t)v.ototal, hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&w.zdev, w.zmem, 0) != hipSuccess) {
+            w.zmem = nullptr;
+            return qpb::set_error(QPB_ENOMEM, "QP_SOLVE: mapped pinned host allocation failed");
+        }
+        w.zcap = v.ototal;
+    }
     v.dmem = w.dmem;
     v.hmem = w.hmem;
+    v.zmem = w.zmem;
+    v.zdev = w.zdev;
     v.stream = w.stream;
     return QPB_OK;
+}
+
+// Zero-copy solve: inputs written straight into the tiled slot of QP 0 (stride
+// 64) of the mapped pinned slab, one launch reads them over the host link and
+// writes x, y, z, s, stats, flag, iterations and fval back into it.
+int solve_zero_copy(Priv &v, QP &q) {
+    const long n = q.n, m = q.m, p = q.p;
+    double *h = v.zmem, *d = v.zdev;
+    auto put = [h](long off, const double *src, long k) {
+        for (long i = 0; i < k; i++) h[off + 64 * i] = src[i];
+    };
+    put(v.oP, q.P->pr, v.nP);
+    if (p > 0) put(v.oA, q.A->pr, v.nA);
+    put(v.oG, q.G->pr, v.nG);
+    put(v.oc, q.c, n);
+    put(v.oh, q.h, m);
+    if (p > 0) put(v.ob, q.b, p);
+    qpb_settings st;
+    st.maxit = q.options->maxit;
+    st.reltol = q.options->reltol;
+    st.abstol = q.options->abstol;
+    st.sigma_d = q.sigma_d;
+    const long ofl = v.oout;               // flag, iterations: two ints in one double slot
+    int rc = qpb_solve(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
+                       p > 0 ? d + v.ob : nullptr, &st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz, d + v.os,
+                       reinterpret_cast<int *>(d + ofl), reinterpret_cast<int *>(d + ofl) + 1, d + v.ofv, d + v.ost,
+                       v.stream);
+    if (hipStreamSynchronize(v.stream) != hipSuccess && !rc) rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: kernel failed");
+    if (rc) return rc;
+    auto get = [h](double *dst, long off, long k) {
+        for (long i = 0; i < k; i++) dst[i] = h[off + 64 * i];
+    };
+    get(q.x, v.ox, n);
+    if (p > 0) get(q.y, v.oy, p);
+    get(q.z, v.oz, m);
+    get(q.s, v.os, m);
+    double r[6];
+    get(r, v.ost, 6);
+    v.st.n_rx = r[0]; v.st.n_ry = r[1]; v.st.n_rz = r[2]; v.st.n_mu = r[3];
+    v.st.alpha_p = r[4]; v.st.alpha_d = r[5];
+    v.st.fval = h[v.ofv];
+    int iv[2];
+    std::memcpy(iv, h + ofl, sizeof(iv));
+    v.st.Flag = iv[0];
+    v.st.IterationCount = iv[1];
+    return QPB_OK;
+}
+
+// host mirror of the KKT after the solve: z-block diagonal as the last
+// updatekktmatrix left it (Auxilary.c:205-233); mu from the last residuals
+void mirror_kkt(Priv &v, QP &q) {
+    q.mu = v.st.n_mu;
+    const qpb::Plan &pl = v.plan->pl;
+    const double *Av = q.p > 0 ? q.A->pr : nullptr;
+    for (size_t k = 0; k < pl.K_loop.size() && k < v.Kpr.size(); k++)
+        if (pl.K_loop[k].kind == qpb::Src::ZDiag && v.st.IterationCount > 0)
+            v.Kpr[k] = kkt_slot_value(pl.K_loop[k], q.P->pr, Av, q.G->pr, q.s, q.z);
 }
 
 int solve_on_device(Priv &v, QP &q) {
@@ -371,6 +460,12 @@ int solve_on_device(Priv &v, QP &q) {
     (void)hipGetDevice(&cur);
     if (cur != v.dev) (void)hipSetDevice(v.dev);
     const long n = q.n, m = q.m, p = q.p;
+    if (zero_copy(v)) {
+        rc = solve_zero_copy(v, q);
+        if (cur != v.dev && cur >= 0) (void)hipSetDevice(cur);
+        if (!rc) mirror_kkt(v, q);
+        return rc;
+    }
     double *hin = v.hmem, *hout = v.hmem + v.nin;
     double *w = hin;
     auto put = [&w](const double *src, long k) {
@@ -442,13 +537,7 @@ int solve_on_device(Priv &v, QP &q) {
     std::memcpy(iv, hout + v.nout, sizeof(iv));
     v.st.Flag = iv[0];
     v.st.IterationCount = iv[1];
-    q.mu = v.st.n_mu;
-    // KKT mirror: z-block diagonal as the last updatekktmatrix left it (Auxilary.c:205-233)
-    const qpb::Plan &pl = v.plan->pl;
-    const double *Av = p > 0 ? q.A->pr : nullptr;
-    for (size_t k = 0; k < pl.K_loop.size() && k < v.Kpr.size(); k++)
-        if (pl.K_loop[k].kind == qpb::Src::ZDiag && v.st.IterationCount > 0)
-            v.Kpr[k] = kkt_slot_value(pl.K_loop[k], q.P->pr, Av, q.G->pr, q.s, q.z);
+    mirror_kkt(v, q);
     return QPB_OK;
 }
 

@@ -195,17 +195,20 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # kernel duration: HIP events on the launch stream around each of a further
-    # kev launches (per-step event records inside the timed loop cost ~8 us of host
-    # time per step, more than the gap they measure, so they stay out of it)
+    # kernel duration: one HIP event pair on the launch stream around kev further
+    # back-to-back launches (GPU-bound: a launch is queued faster than the kernel
+    # runs), so the average is the kernel plus the ~1 us dispatch gap -- an upper
+    # bound that rocprof's per-dispatch durations (profiles/) bracket from below.
+    # Per-launch event pairs would add their own ~3 us; per-step events inside the
+    # timed loop cost ~8 us of host time per step, so they stay out of it.
     kev = min(steps, 50)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(kev)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
     for i in range(kev):
-        ev[i][0].record(stream)
         solves[0]()
-        ev[i][1].record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = e0.elapsed_time(e1) / kev
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -269,13 +272,13 @@ def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
     el_streams = timed(streams_step)
     el = timed(gsolve)
     # kernel duration of the group launch (events on its stream, outside the timed loop)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
-    for a, b in evs:
-        a.record(main)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(main)
+    for _ in range(20):
         gsolve()
-        b.record(main)
+    e1.record(main)
     torch.cuda.synchronize()
-    kms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kms = e0.elapsed_time(e1) / 20
     B = per_pattern * len(legs)
     return {"batch": B, "patterns": [L["name"] for L in legs], "value": B * steps / el,
             "ms_per_step": el * 1e3 / steps, "kernel": group.kernel_name(), "kernel_ms": kms,
