@@ -352,10 +352,11 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
             qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
         }
     }
-    // for a large KKT system the alternative is the tree kernel: on 30/68/18 it
-    // wins at 1 024 QPs (1.26 vs 1.34 ms) and 8 192 (7.0 vs 9.0 ms), so the wave
-    // kernel keeps only small batches (a single QP: the drop-in)
-    if (plan->wave_ok && plan->large_tree) plan->wave_max_batch = 512;
+    // for a large KKT system the alternative is the tree kernel.  On 30/68/18 the
+    // wave kernel, with its leaf-row G'diag(w)G on the matrix cores (QPB_W_MFMA),
+    // wins at every batch size: 1 024 QPs 0.95 vs 1.26 ms, 8 192 6.4 vs 7.0 ms
+    // (before MFMA the tree kernel won beyond 512)
+    if (plan->wave_ok && plan->large_tree) plan->wave_max_batch = -1;
     if (const char *e = getenv("QPB_WAVE_MAX")) plan->wave_max_batch = atol(e);
     *out = plan.release();
     return QPB_OK;

@@ -39,6 +39,10 @@ struct qpb_args {
 #ifndef QPB_W_GG           // 1: G(r,i)G(r,j) products in registers; 0: recompute from LDS
 #define QPB_W_GG (QPB_NNZG <= 48)
 #endif
+#ifndef QPB_W_MFMA         // 1: the leaf z rows' G'diag(w)G as an MFMA GEMM (v_mfma_f64_16x16x4f64)
+#define QPB_W_MFMA (!QPB_W_GG && QPB_NX <= 64 && \
+                    (16 * ((QPB_NX + 15) / 16)) * (16 * ((QPB_NX + 15) / 16)) <= QPB_ND * QPB_ND)
+#endif
 #ifndef QPB_W_REGS         // 1: this lane's slices of P, A, G in registers; 0: read LDS in place
 #define QPB_W_REGS (QPB_NX <= 16 && QPB_NZ <= 32)
 #endif
@@ -411,9 +415,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     };
     // after a wsync: H = H0 + G_L' W G_L, then the right-looking LDL' of the
     // dense block in permutation order (registers and DPP only)
+    int fstamp = 0;     // timing build: factor-internal stamps base (0 = off)
     auto factor_ldl = [&]() {
 #pragma unroll
         for (int e = 0; e < ND; e++) H[e] = H0[e];
+        if (fstamp) QPB_TS(fstamp + 0);
         if constexpr (QPB_W_GG) {      // small G: every (r, j) unrolled, products precomputed
             int e = 0;
 #pragma unroll
@@ -426,6 +432,60 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                         e++;
                     }
             }
+        } else if constexpr (QPB_W_MFMA) {
+            // C = G_L' diag(w) G_L over the x columns as a dense GEMM on the matrix
+            // cores: 16 x 16 output tiles (I <= J; C is symmetric), K = 4 z rows per
+            // v_mfma_f64_16x16x4f64.  A operand: lane l holds G(r, 16 I + (l & 15)),
+            // r = 4 s + (l >> 4); B operand: w_r G(r, 16 J + (l & 15)) (w_r = 0 for a
+            // non-leaf row, which joins the dense block instead).  D: lane l, reg t is
+            // C(16 I + (l >> 4) + 4 t, 16 J + (l & 15)).  The tiles go through the L
+            // transpose area (dead between the last solve and the next transpose),
+            // and each x row adds its row of C.
+            typedef double qpb_v4d __attribute__((ext_vector_type(4)));
+            constexpr int NT = (NX + 15) / 16, NXP = 16 * NT, NP = NT * (NT + 1) / 2;
+            qpb_v4d acc[NP];
+#pragma unroll
+            for (int p = 0; p < NP; p++) acc[p] = qpb_v4d{0.0, 0.0, 0.0, 0.0};
+            const int li = lane & 15, lk = lane >> 4;
+#pragma unroll 2
+            for (int s4 = 0; s4 < NZ; s4 += 4) {
+                const int r = s4 + lk;
+                const bool rok = r < NZ;
+                const int rr = rok ? r : NZ - 1;
+                const double wr = (rok && qpb_zleaf_d[rr]) ? Vb[VBW + rr] : 0.0;
+                double g[NT];
+#pragma unroll
+                for (int I = 0; I < NT; I++) {
+                    const int i = 16 * I + li;
+                    g[I] = (rok && i < NX) ? Gd[i * NZ + rr] : 0.0;
+                }
+                int p = 0;
+#pragma unroll
+                for (int I = 0; I < NT; I++)
+#pragma unroll
+                    for (int J = I; J < NT; J++, p++)
+                        acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(g[I], wr * g[J], acc[p], 0, 0, 0);
+            }
+            double *Sc = Tx;
+            {
+                int p = 0;
+#pragma unroll
+                for (int I = 0; I < NT; I++)
+#pragma unroll
+                    for (int J = I; J < NT; J++, p++)
+#pragma unroll
+                        for (int t = 0; t < 4; t++) {
+                            const int row = 16 * I + lk + 4 * t, col = 16 * J + li;
+                            Sc[row * NXP + col] = acc[p][t];
+                            if (I != J) Sc[col * NXP + row] = acc[p][t];
+                        }
+            }
+            qpb_wsync();
+            if (dk == 0) {
+#pragma unroll
+                for (int j = 0; j < NX; j++) H[qpb_xpos[j]] += Sc[dxi * NXP + j];
+            }
+            qpb_wsync();
         } else {                       // per column-pattern group: rows looped, columns unrolled
             qpb_for<0, QPB_NGRP>([&](auto gc) {
                 constexpr int g = decltype(gc)::value;
@@ -440,6 +500,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 }
             });
         }
+        if (fstamp) QPB_TS(fstamp + 1);
         double kdz[ND];
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
@@ -469,6 +530,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             });
             H[k] = lane > k ? nl : 0.0;       // -L(d,k) below the diagonal, 0 elsewhere
         });
+        if (fstamp) QPB_TS(fstamp + 2);
     };
     // transpose -L through LDS: lane e gets column e (0 on and above the
     // diagonal); the first wsync also orders every earlier Vb read before the
@@ -610,6 +672,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         // the exit test (wasted on the last iteration): one LDS exchange serves
         // both, and the LDL's latency-bound pivot chain is scheduled together
         // with the residual products and reductions.
+        if (QPB_W_TIMING) fstamp = it == 1 ? 360 : 0;
         factor_publish(kd);
         // residuals (Auxilary.c:745-786), objective (Auxilary.c:1133-1141)
         if (lane < NX) Vb[lane] = x;
