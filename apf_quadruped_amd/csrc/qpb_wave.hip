@@ -43,6 +43,9 @@ struct qpb_args {
 #define QPB_W_MFMA (!QPB_W_GG && QPB_NX <= 64 && \
                     (16 * ((QPB_NX + 15) / 16)) * (16 * ((QPB_NX + 15) / 16)) <= QPB_ND * QPB_ND)
 #endif
+#ifndef QPB_W_LDSB         // 1: LDL' update broadcasts through LDS (dense blocks beyond one DPP row)
+#define QPB_W_LDSB (QPB_ND > 16)
+#endif
 #ifndef QPB_W_REGS         // 1: this lane's slices of P, A, G in registers; 0: read LDS in place
 #define QPB_W_REGS (QPB_NX <= 16 && QPB_NZ <= 32)
 #endif
@@ -447,25 +450,36 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
             for (int p = 0; p < NP; p++) acc[p] = qpb_v4d{0.0, 0.0, 0.0, 0.0};
             const int li = lane & 15, lk = lane >> 4;
-#pragma unroll 2
-            for (int s4 = 0; s4 < NZ; s4 += 4) {
-                const int r = s4 + lk;
-                const bool rok = r < NZ;
-                const int rr = rok ? r : NZ - 1;
-                const double wr = (rok && qpb_zleaf_d[rr]) ? Vb[VBW + rr] : 0.0;
+            // branch-free operand loads (clamped index x 0/1 mask), so every LDS read
+            // of the GEMM can be issued ahead of the MFMA chain
+            int gi[NT];
+            double gm[NT];
+#pragma unroll
+            for (int I = 0; I < NT; I++) {
+                const int i = 16 * I + li;
+                gi[I] = (i < NX ? i : NX - 1) * NZ;
+                gm[I] = i < NX ? 1.0 : 0.0;
+            }
+            qpb_for<0, (NZ + 3) / 4>([&](auto sc) {
+                constexpr int s4 = 4 * decltype(sc)::value;
+                constexpr bool l0 = s4 < NZ && qpb_zleaf[s4 < NZ ? s4 : 0];
+                constexpr bool l1 = s4 + 1 < NZ && qpb_zleaf[s4 + 1 < NZ ? s4 + 1 : 0];
+                constexpr bool l2 = s4 + 2 < NZ && qpb_zleaf[s4 + 2 < NZ ? s4 + 2 : 0];
+                constexpr bool l3 = s4 + 3 < NZ && qpb_zleaf[s4 + 3 < NZ ? s4 + 3 : 0];
+                const double lm = lk == 0 ? (l0 ? 1.0 : 0.0) : lk == 1 ? (l1 ? 1.0 : 0.0)
+                                : lk == 2 ? (l2 ? 1.0 : 0.0) : (l3 ? 1.0 : 0.0);
+                const int rr = (s4 + 3 < NZ) ? s4 + lk : (s4 + lk < NZ ? s4 + lk : NZ - 1);
+                const double wr = lm * Vb[VBW + rr];
                 double g[NT];
 #pragma unroll
-                for (int I = 0; I < NT; I++) {
-                    const int i = 16 * I + li;
-                    g[I] = (rok && i < NX) ? Gd[i * NZ + rr] : 0.0;
-                }
+                for (int I = 0; I < NT; I++) g[I] = gm[I] * Gd[gi[I] + rr];
                 int p = 0;
 #pragma unroll
                 for (int I = 0; I < NT; I++)
 #pragma unroll
                     for (int J = I; J < NT; J++, p++)
                         acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(g[I], wr * g[J], acc[p], 0, 0, 0);
-            }
+            });
             double *Sc = Tx;
             {
                 int p = 0;
@@ -510,6 +524,15 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         // H'(k+1,k) and H'(k+1,k+1) (values before step k) with exactly the
         // operations lane k+1's own update performs, so the trailing updates
         // of step k are off the chain.
+#if QPB_W_LDSB
+        // broadcasts of the updates through LDS instead of v_readlane pairs: column
+        // k (H(j,k) of every row j) is published by its lanes as soon as step k-1
+        // has finalised it, into one of two 64-slot buffers in the L transpose area
+        // (free between the G'WG and the transpose); step k reads it as wave-uniform
+        // LDS loads, paired by the compiler
+        double *__restrict__ Bc = Tx;
+        Bc[lane] = H[0];
+#endif
         double dpiv = qpb_xb<0>(H[0]);
         if constexpr (qpb_dkind[0] == 2) dpiv += kdz[0];
         qpb_for<0, ND>([&](auto kc) {
@@ -524,10 +547,19 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             // -L(d,k): kept negated so every update (and the solves) is a plain
             // v_fmac_f64 whose broadcast operand folds into it as DPP row_newbcast
             const double nl = H[k] * -rd;
+#if QPB_W_LDSB
+            constexpr int cb = (k & 1) * 64, nb = ((k + 1) & 1) * 64;
+            qpb_for<k + 1, ND>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                H[j] = __builtin_fma(Bc[cb + j], nl, H[j]);
+                if constexpr (j == k + 1) Bc[nb + lane] = H[j];      // column k+1 is final
+            });
+#else
             qpb_for<k + 1, ND>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 H[j] = qpb_fmac_xb<j>(H[j], H[k], nl);
             });
+#endif
             H[k] = lane > k ? nl : 0.0;       // -L(d,k) below the diagonal, 0 elsewhere
         });
         if (fstamp) QPB_TS(fstamp + 2);
