@@ -40,8 +40,7 @@ struct qpb_args {
 #define QPB_W_GG (QPB_NNZG <= 48)
 #endif
 #ifndef QPB_W_MFMA         // 1: the leaf z rows' G'diag(w)G as an MFMA GEMM (v_mfma_f64_16x16x4f64)
-#define QPB_W_MFMA (!QPB_W_GG && QPB_NX <= 64 && \
-                    (16 * ((QPB_NX + 15) / 16)) * (16 * ((QPB_NX + 15) / 16)) <= QPB_ND * QPB_ND)
+#define QPB_W_MFMA (!QPB_W_GG && QPB_NX <= 64)
 #endif
 #ifndef QPB_W_LDSB         // 1: LDL' update broadcasts through LDS (dense blocks beyond one DPP row)
 #define QPB_W_LDSB (QPB_ND > 16)
@@ -65,12 +64,21 @@ struct qpb_args {
 #define NV (NX + NZ + NY)
 // vector exchange area: x | z | y  (residual gather); solve: bx | by | bz | v | out
 #define VB_SIZE (((2 * NV + NZ + NX) + 1) & ~1)
-// per-wave LDS (doubles): Pd[NX*NX] Ad[NY*NX] Gd[NZ*NX] | Tx[ND*ND] | Vb
+// per-wave LDS (doubles): Pd[NX*NX] Ad[NY*NX] Gd[NZ*NX] | T | Vb.  T holds the
+// strictly lower triangle of -L, packed by rows (row d at d(d-1)/2), for the
+// transpose; between a transpose and the next factor it is scratch for the MFMA
+// G'WG tiles (NXP^2) and the LDL' broadcast buffers (2 x 64); its last two slots
+// are a read target for masked lanes.  (Packing, instead of ND^2, keeps the
+// 30/68/18 QP at 39.6 KB: four QPs per CU.)
 #define OFF_A (NX * NX)
 #define OFF_G (OFF_A + NY * NX)
 #define OFF_C (OFF_G + NZ * NX)
 #define OFF_T ((OFF_C + 1) & ~1)
-#define OFF_V (OFF_T + ((ND * ND + 1) & ~1))
+#define QPB_TMAX(a, b) ((a) > (b) ? (a) : (b))
+#define TSZ (((QPB_TMAX(QPB_TMAX(ND * (ND - 1) / 2, QPB_W_MFMA ? 256 * ((NX + 15) / 16) * ((NX + 15) / 16) : 0), \
+                        QPB_W_LDSB ? 128 : 0) + 1) & ~1) + 2)
+#define T_SINK (TSZ - 2)
+#define OFF_V (OFF_T + TSZ)
 #define LDS_WAVE (OFF_V + VB_SIZE)
 #define ZC ((NZ + 63) / 64)          // z rows per lane (lane r holds r, r + 64, ...)
 #define ROWS_D ((ND + 15) / 16)
@@ -568,13 +576,20 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     // diagonal); the first wsync also orders every earlier Vb read before the
     // solve's stores
     auto factor_transpose = [&]() {
-        if (isd) {
+        {
+            // row `lane` of -L: entries e < lane at lane(lane-1)/2 + e (exec-masked
+            // stores: a shared sink slot would serialise the masked lanes' writes)
+            const int base = isd ? lane * (lane - 1) / 2 : 0;
 #pragma unroll
-            for (int e = 0; e < ND; e++) Tx[lane * ND + e] = H[e];
+            for (int e = 0; e < ND - 1; e++)
+                if (isd && e < lane) Tx[base + e] = H[e];
         }
         qpb_wsync();
 #pragma unroll
-        for (int k = 0; k < ND; k++) Lt[k] = Tx[k * ND + id];
+        for (int k = 0; k < ND; k++) {
+            const double v = Tx[k > id ? k * (k - 1) / 2 + id : T_SINK];
+            Lt[k] = k > id ? v : 0.0;
+        }
         qpb_wsync();
     };
 
