@@ -45,6 +45,9 @@ struct qpb_args {
 #ifndef QPB_W_LDSB         // 1: LDL' update broadcasts through LDS (dense blocks beyond one DPP row)
 #define QPB_W_LDSB (QPB_ND > 16)
 #endif
+#ifndef QPB_W_LTLDS        // 1: the backward solve reads its column of -L from LDS (no register copy)
+#define QPB_W_LTLDS (QPB_ND > 16)
+#endif
 #ifndef QPB_W_REGS         // 1: this lane's slices of P, A, G in registers; 0: read LDS in place
 #define QPB_W_REGS (QPB_NX <= 16 && QPB_NZ <= 32)
 #endif
@@ -408,7 +411,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 if (qpb_Gnz[r][j]) GG[e++] = GC(r) * Gd[j * NZ + r];
     }
 
-    double H[ND], Lt[ND], rDd = 0.0, w[ZC];
+    double H[ND], Lt[QPB_W_LTLDS ? 1 : ND], rDd = 0.0, w[ZC];
     // The factor with z diagonal kd (per z row) in three pieces, so that its
     // register-only part can be scheduled together with the residuals: leaf z
     // rows fold into the x block as G'diag(w)G, w = -1/regularise(kd); dense z
@@ -585,12 +588,14 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 if (isd && e < lane) Tx[base + e] = H[e];
         }
         qpb_wsync();
+#if !QPB_W_LTLDS
 #pragma unroll
         for (int k = 0; k < ND; k++) {
             const double v = Tx[k > id ? k * (k - 1) / 2 + id : T_SINK];
             Lt[k] = k > id ? v : 0.0;
         }
         qpb_wsync();
+#endif
     };
 
     // solve K [dx; dy; dz] = [bx; byv; bz] with the current factor
@@ -635,10 +640,25 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             t = qpb_fmac_xb_dep<k>(t, t, H[k]);
         });
         t *= rDd;
+#if QPB_W_LTLDS
+        // column `id` of -L straight from the packed transpose area (intact until
+        // the next factor): live only through this chain, not across the iteration
+        double Ltl[ND];
+#pragma unroll
+        for (int k = 0; k < ND; k++) {
+            const double v = Tx[k > id ? k * (k - 1) / 2 + id : T_SINK];
+            Ltl[k] = k > id ? v : 0.0;
+        }
+        qpb_for<0, ND>([&](auto kc) {
+            constexpr int k = ND - 1 - decltype(kc)::value;
+            t = qpb_fmac_xb_dep<k>(t, t, Ltl[k]);
+        });
+#else
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = ND - 1 - decltype(kc)::value;
             t = qpb_fmac_xb_dep<k>(t, t, Lt[k]);
         });
+#endif
         if (sstamp) QPB_TS(sstamp + 3);
         if constexpr (QPB_XID) {
             if (lane < NX) Vb[VBO + lane] = t;

@@ -259,3 +259,31 @@ def test_solve_best_fused_argmin(kernel):
             ref = argmin(out["fval"], out["flag"]).cpu().numpy()
             got = best.cpu().numpy()
             assert got[0] == ref[0] and got[1] == ref[1], (kernel, B, got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 5, 257, 1024])
+def test_controller_shape_batch_auto_dispatch(B, oracle):
+    """Controller stance QPs (30/68/18) as the bench runs them: auto dispatch (the
+    wave kernel with its MFMA G'diag(w)G at every batch size, four QPs per CU),
+    ragged and full batches; a strided sample vs the oracle run with the plan's
+    order: same flags and iteration counts, x / z / s within 1e-9 relative;
+    deterministic across launches."""
+    import torch
+    from apf_quadruped_amd import plans, workloads as W
+    from apf_quadruped_amd.batch import Plan
+    d = W.controller_qp(plans.SEED + 30, np.arange(B))
+    plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0])
+    assert plan.kernel_for(B) == "wave"
+    vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"],
+                                                                d["b"]).items()}
+    r1 = plan.unpack(plan.solve(**vals, B=B), B)
+    r2 = plan.unpack(plan.solve(**vals, B=B), B)
+    for k in ("x", "z", "s", "iters"):
+        np.testing.assert_array_equal(r1[k], r2[k])
+    Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    for q in sorted(set(range(0, B, max(1, B // 12))) | {B - 1}):
+        o = oracle.solve_dense(30, 68, 18, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm)
+        assert r1["flag"][q] == o["flag"] and r1["iters"][q] == o["iters"], q
+        for k in ("x", "z", "s"):
+            assert np.abs(r1[k][q] - o[k]).max() <= 1e-9 * max(1.0, np.abs(o[k]).max()), (q, k)
