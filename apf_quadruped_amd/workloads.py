@@ -193,12 +193,123 @@ def mpc_qp(seed: int, qp_ids, horizon: int = 10, mu: float = MU):
     return dict(n=n, m=m, p=p, P=P, c=c, A=A, b=b, G=G, h=h)
 
 
+# swing phases of the controller (SURVEY §8a shape table): the legs in stance,
+# the swing legs and the slack count (x = [ddx 6; ddq 12; f_st 3k; slack 12-3k])
+SWING_PHASES = {
+    "trot": dict(stance=(1, 3), swing=(0, 2), w_slack=1e8),         # 30/70/12, main.cpp:1730-2005
+    "crawl": dict(stance=(1, 2, 3), swing=(0,), w_slack=1e4),       # 30/69/15, main.cpp:2919-3232
+}
+
+
+def controller_swing_qp(seed: int, qp_ids, phase: str = "trot"):
+    """Controller-shape swing-phase QPs: trot (two stance legs, 30/70/12,
+    main.cpp:1730-2005) and crawl (three stance legs, 30/69/15, main.cpp:2919-3232).
+
+    x = [ddx_com (6); ddq (12); f_st (3k); slack (12 - 3k)] with k stance legs:
+      Q = 50 T_s' T_s + R, T_s = Jst(:, 0:6)' Sigma (f_st columns), R = I with
+          w_slack on the slack block (1e8 trot :1751, 1e4 crawl :2976)
+      c = -50 T_s' W_des
+      A = [M_com 0 -Jst_com' 0; Jst_com Jst_q 0 0] (3k + 6 rows; :1844-1848, :3021-3044)
+      D = friction (5 per stance foot) | tau_max [0 M_jj -Jst_q' 0] | tau_min (negated)
+          | swing task [Jsw_com Jsw_q 0 -I] | -[Jsw_com Jsw_q 0 I] | ddq_max [0 I] | ddq_min [0 -I]
+          (:1857-1992, :3048-3230)
+    Synthetic robot terms as controller_qp; Jst / Jsw rows are the contact
+    Jacobian rows [I3, -[r_i]x] of the stance / swing feet w.r.t. the CoM plus
+    leg-dominant joint blocks.  b and the swing-task bounds are consistent with a
+    random state (ddx*, ddq*, f* inside the friction pyramids, slack 0), so every
+    QP is feasible (the controller's trot right-hand side is identically zero,
+    main.cpp:1851-1854, which the synthetic state replaces)."""
+    ph = SWING_PHASES[phase]
+    st, sw = ph["stance"], ph["swing"]
+    qp_ids = np.atleast_1d(np.asarray(qp_ids, dtype=np.int64))
+    B = len(qp_ids)
+    Jc, W = contact_terms(seed, qp_ids)                    # [B, 12, 6] rows per foot coordinate
+    u = uniforms(seed ^ 0x5E1F, qp_ids, 144 + 144 + 12 + 12 + 12 + 12 + 6 + 12 + 12 + 12)
+    k = 0
+
+    def take(cnt):
+        nonlocal k
+        v = u[:, k:k + cnt]
+        k += cnt
+        return v
+    Mcom = np.zeros((B, 6, 6))
+    Mcom[:, [0, 1, 2], [0, 1, 2]] = ROBOT_MASS
+    Mcom[:, 3:, 3:] = np.diag([0.35, 0.85, 0.95])[None]
+    Lm = 0.02 * take(144).reshape(B, 12, 12) - 0.01 + 0.25 * np.eye(12)[None]
+    Mjj = np.einsum("bij,bkj->bik", Lm, Lm)
+    Jq = 0.004 * take(144).reshape(B, 12, 12) - 0.002           # foot-coordinate x joint (leg-dominant)
+    jb = 0.7 * take(12).reshape(B, 4, 3) - 0.35
+    for leg in range(4):
+        blk = np.einsum("bi,ij->bij", jb[:, leg], np.ones((3, 3))) * np.array([[1, .5, .3], [.4, 1, .6], [.2, .5, 1]])
+        Jq[:, 3 * leg:3 * leg + 3, 3 * leg:3 * leg + 3] += blk + 0.3 * np.eye(3)[None]
+    bias_j = 4.0 * take(12) - 2.0
+    q = take(12) - 0.5
+    dq = 0.4 * take(12) - 0.2
+    ddx = 2.0 * take(6) - 1.0
+    ddq = 2.0 * take(12) - 1.0
+    uf = take(12).reshape(B, 4, 3)
+    tol_sw = 0.5 + take(12)                                      # swing-task tolerances
+    rows = lambda legs: np.concatenate([np.arange(3 * i, 3 * i + 3) for i in legs])
+    Jst_c, Jst_q = Jc[:, rows(st), :], Jq[:, rows(st), :]        # [B, 3k, 6], [B, 3k, 12]
+    Jsw_c, Jsw_q = Jc[:, rows(sw), :], Jq[:, rows(sw), :]
+    ns, nw = 3 * len(st), 3 * len(sw)
+    n, p = 30, 6 + ns
+    o_f, o_s = 18, 18 + ns
+    fz = 40.0 + 60.0 * uf[:, list(st), 2]
+    f = np.stack([(0.8 * uf[:, list(st), 0] - 0.4) * MU * fz, (0.8 * uf[:, list(st), 1] - 0.4) * MU * fz, fz],
+                 -1).reshape(B, ns)
+    Ts = np.zeros((B, 6, n))
+    Ts[:, :, o_f:o_s] = np.transpose(Jst_c, (0, 2, 1))
+    R = np.eye(n)
+    R[o_s:, o_s:] *= ph["w_slack"]
+    P = 50.0 * np.einsum("bki,bkj->bij", Ts, Ts) + R[None]
+    c = -50.0 * np.einsum("bki,bk->bi", Ts, W)
+    A = np.zeros((B, p, n))
+    A[:, 0:6, 0:6] = Mcom
+    A[:, 0:6, o_f:o_s] = -np.transpose(Jst_c, (0, 2, 1))
+    A[:, 6:, 0:6] = Jst_c
+    A[:, 6:, 6:18] = Jst_q
+    xs = np.concatenate([ddx, ddq, f, np.zeros((B, n - o_s))], 1)
+    b = np.einsum("bij,bj->bi", A, xs)
+    m = 5 * len(st) + 24 + 2 * nw + 24
+    G = np.zeros((B, m, n))
+    h = np.zeros((B, m))
+    cfr = friction_block(MU)
+    for i in range(len(st)):
+        G[:, 5 * i:5 * i + 5, o_f + 3 * i:o_f + 3 * i + 3] = cfr
+    r0 = 5 * len(st)
+    JqT = np.transpose(Jst_q, (0, 2, 1))                        # [B, 12, 3k]
+    G[:, r0:r0 + 12, 6:18] = Mjj
+    G[:, r0:r0 + 12, o_f:o_s] = -JqT
+    G[:, r0 + 12:r0 + 24, 6:18] = -Mjj
+    G[:, r0 + 12:r0 + 24, o_f:o_s] = JqT
+    h[:, r0:r0 + 12] = 60.0 - bias_j
+    h[:, r0 + 12:r0 + 24] = 60.0 + bias_j
+    r1 = r0 + 24
+    sw_acc = np.einsum("bij,bj->bi", Jsw_c, ddx) + np.einsum("bij,bj->bi", Jsw_q, ddq)
+    G[:, r1:r1 + nw, 0:6] = Jsw_c
+    G[:, r1:r1 + nw, 6:18] = Jsw_q
+    G[:, r1:r1 + nw, o_s:o_s + nw] = -np.eye(nw)[None]
+    h[:, r1:r1 + nw] = sw_acc + tol_sw[:, :nw]
+    G[:, r1 + nw:r1 + 2 * nw, 0:6] = -Jsw_c
+    G[:, r1 + nw:r1 + 2 * nw, 6:18] = -Jsw_q
+    G[:, r1 + nw:r1 + 2 * nw, o_s:o_s + nw] = -np.eye(nw)[None]
+    h[:, r1 + nw:r1 + 2 * nw] = -sw_acc + tol_sw[:, :nw]
+    r2 = r1 + 2 * nw
+    dt = 0.025
+    G[:, r2:r2 + 12, 6:18] = np.eye(12)[None]
+    G[:, r2 + 12:r2 + 24, 6:18] = -np.eye(12)[None]
+    h[:, r2:r2 + 12] = (2 / dt ** 2) * (1.5 - q - dt * dq)
+    h[:, r2 + 12:r2 + 24] = -(2 / dt ** 2) * (-1.5 - q - dt * dq)
+    return dict(n=n, m=m, p=p, P=P, c=c, A=A, b=b, G=G, h=h)
+
+
 def to_colmajor(M: np.ndarray) -> np.ndarray:
     """[B, r, c] row-major -> [B, r*c] column-major (QP_SETUP_dense, ordering 30)."""
     return np.ascontiguousarray(np.transpose(M, (0, 2, 1))).reshape(M.shape[0], -1)
 
 
-def controller_qp(seed: int, qp_ids):
+def controller_qp(seed: int, qp_ids, phase: str = "stance"):
     """Controller-shape stance QP "C30" (30 vars / 68 ineq / 18 eq), following
     dogbot_controller/src/client/main.cpp:1471-1647 (SURVEY §8a shape table):
 
@@ -215,6 +326,8 @@ def controller_qp(seed: int, qp_ids):
     made consistent with a random state (ddx*, ddq*, f* inside the friction
     pyramids) so every QP is feasible.  Returns the same dict layout as
     contact_force_qp (dense row-major [B, r, c])."""
+    if phase != "stance":
+        return controller_swing_qp(seed, qp_ids, phase)
     qp_ids = np.atleast_1d(np.asarray(qp_ids, dtype=np.int64))
     B = len(qp_ids)
     Jc, W = contact_terms(seed, qp_ids)

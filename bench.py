@@ -447,6 +447,12 @@ def main():
             shape_leg("controller stance QP 30/68/18 (main.cpp:1649), batch 1024",
                       lambda ids: W.controller_qp(plans.SEED + 30, ids), 1024, args.tol, dev,
                       cpu=None if args.no_cpu else (512, 16)),
+            shape_leg("controller trot QP 30/70/12 (main.cpp:2005), batch 1024",
+                      lambda ids: W.controller_qp(plans.SEED + 31, ids, phase="trot"), 1024, args.tol, dev,
+                      cpu=None if args.no_cpu else (512, 16)),
+            shape_leg("controller crawl QP 30/69/15 (main.cpp:3232), batch 1024",
+                      lambda ids: W.controller_qp(plans.SEED + 31, ids, phase="crawl"), 1024, args.tol, dev,
+                      cpu=None if args.no_cpu else (512, 16)),
             apf_leg(args.tol, dev),
             trace_leg(args.tol, dev),
         ]

@@ -5,6 +5,7 @@ Run in the build container (needs oracle/_ref/libqpswift_ref.so, which
 
     python tests/golden/make_golden.py          # every case
     python tests/golden/make_golden.py c30      # only the controller-shape cases
+    python tests/golden/make_golden.py c30_swing  # only the swing-phase controller shapes
 
 Every case calls the reference exactly as dogbot_controller does
 (QP_SETUP_dense -> options override -> QP_SOLVE, main.cpp:1649-1656) and records
@@ -68,10 +69,23 @@ def c30_cases(ref):
     save("c30_tol1e-2", seed=SEED_BASE + 30, **dense_case(ref, d, ids, 1e-2))
 
 
+def c30_swing_cases(ref):
+    """Controller-shape swing-phase QPs: trot 30/70/12 (main.cpp:1730-2005) and
+    crawl 30/69/15 (main.cpp:2919-3232), at 1e-6 and at the controller's 1e-2."""
+    ids = np.arange(8)
+    for phase in ("trot", "crawl"):
+        d = W.controller_qp(SEED_BASE + 31, ids, phase=phase)
+        save(f"c30_{phase}_tol1e-6", seed=SEED_BASE + 31, **dense_case(ref, d, ids, 1e-6))
+        save(f"c30_{phase}_tol1e-2", seed=SEED_BASE + 31, **dense_case(ref, d, ids, 1e-2))
+
+
 def main(only=None):
     ref = Reference()
     if only == "c30":
         c30_cases(ref)
+        return
+    if only == "c30_swing":
+        c30_swing_cases(ref)
         return
     # C1: 12-var / 20-ineq / 6-eq contact-force QP (configs 1, 2, 5).
     ids = np.arange(64)
@@ -106,6 +120,7 @@ def main(only=None):
     # Sparse QP_SETUP with sigma_d > 0: the pure-centering branch (qpSWIFT.c:572-579).
     sparse_cases(ref)
     c30_cases(ref)
+    c30_swing_cases(ref)
 
 
 def to_csc(M):

@@ -153,7 +153,8 @@ def test_solve_without_gpu_fails_loudly():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "mixed_crawl_blflfr", "c30_tol1e-6", "c30_tol1e-2"])
+@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "mixed_crawl_blflfr", "c30_tol1e-6", "c30_tol1e-2",
+                                  "c30_trot_tol1e-2", "c30_crawl_tol1e-2"])
 def test_dropin_fast_default_with_reference_permutation(name):
     """Default (fast) drop-in given the reference's permutation: same pivots and
     regularisations, so x, y, z, s agree to 1e-6 even at the controller's tol 1e-2

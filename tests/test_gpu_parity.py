@@ -118,9 +118,12 @@ def test_exact_kernel_matches_oracle_with_own_ordering(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,ref_perm", [("c30_tol1e-6", False), ("c30_tol1e-6", True), ("c30_tol1e-2", True)])
+@pytest.mark.parametrize("name,ref_perm", [("c30_tol1e-6", False), ("c30_tol1e-6", True), ("c30_tol1e-2", True),
+                                           ("c30_trot_tol1e-6", False), ("c30_trot_tol1e-6", True),
+                                           ("c30_trot_tol1e-2", True), ("c30_crawl_tol1e-6", False),
+                                           ("c30_crawl_tol1e-6", True), ("c30_crawl_tol1e-2", True)])
 def test_wave_kernel_controller_shape_vs_reference(name, ref_perm):
-    """Controller-shape QPs (30/68/18, N = 116: two z rows per lane, dense block
+    """Controller-shape QPs (stance 30/68/18, trot 30/70/12, crawl 30/69/15; N = 116: two z rows per lane, dense block
     of 48-51 rows over several 16-lane rows) on the wave kernel vs the reference
     golden vectors.  Given the reference's permutation the wave kernel factors
     with the reference's pivots (and regularisations), so even the loosely
@@ -140,7 +143,8 @@ def _oracle_perm(plan):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "c1_noeq", "mixed_stance4", "mixed_trot_blfr",
-                                  "mixed_trot_brfl", "mixed_crawl_blflfr", "c1_maxit3", "c30_tol1e-6", "c30_tol1e-2"])
+                                  "mixed_trot_brfl", "mixed_crawl_blflfr", "c1_maxit3", "c30_tol1e-6", "c30_tol1e-2",
+                                  "c30_trot_tol1e-6", "c30_trot_tol1e-2", "c30_crawl_tol1e-6", "c30_crawl_tol1e-2"])
 @pytest.mark.parametrize("kernel", ["wave", "wave1"])
 def test_wave_kernel_matches_oracle_in_its_order(name, kernel, oracle):
     """Wave kernel (row form where the pattern fits, and one QP per wavefront) vs

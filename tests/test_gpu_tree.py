@@ -15,7 +15,7 @@ from conftest import golden
 from test_gpu_parity import DENSE_CASES, _dense, _solve
 
 TOL = 1e-6
-CASES = DENSE_CASES + ["c30_tol1e-6", "c30_tol1e-2", "mpc_h10"]
+CASES = DENSE_CASES + ["c30_tol1e-6", "c30_tol1e-2", "c30_trot_tol1e-6", "c30_crawl_tol1e-6", "mpc_h10"]
 
 
 def _close(got, ref, what, tol):
