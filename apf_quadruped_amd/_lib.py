@@ -88,6 +88,8 @@ def lib() -> C.CDLL:
     L.qpb_group_compile.argtypes = [vp]
     L.qpb_group_solve.restype = C.c_int
     L.qpb_group_solve.argtypes = [vp, C.POINTER(QpbIo), C.POINTER(QpbSettings), vp, vp]
+    L.qpb_winner.restype = C.c_int
+    L.qpb_winner.argtypes = [vp, vp, C.c_long, C.c_long, vp, vp]
     L.qpb_argmin.restype = C.c_int
     L.qpb_argmin.argtypes = [C.c_long, vp, vp, vp, vp]
     if hasattr(L, "QP_SETUP"):

@@ -125,6 +125,19 @@ __global__ void __launch_bounds__(1024) qpb_argmin_single(long B, const double *
     if (threadIdx.x == 0) { out[0] = bv; out[1] = (double)bi; }
 }
 
+// The winner's payload for the multi-GPU gather: {fval, index,
+// x*[0..n)} -- x of QP `index` read from the tiled outputs, NaN when the batch
+// has no optimal QP (index -1).  One wavefront; stream-ordered after the solve.
+__global__ void __launch_bounds__(64) qpb_winner_k(const double *__restrict__ best, const double *__restrict__ x,
+                                                   long n, long B, double *__restrict__ out) {
+    const double fv = best[0];
+    const long q = (long)best[1];
+    const bool ok = q >= 0 && q < B;
+    if (threadIdx.x == 0) { out[0] = fv; out[1] = best[1]; }
+    for (long j = threadIdx.x; j < n; j += 64)
+        out[2 + j] = ok ? x[(q >> 6) * n * 64 + j * 64 + (q & 63)] : __builtin_nan("");
+}
+
 // Strided segment copies dst[i * ds] = src[i * ss]; blockIdx.y selects the
 // segment.  Used by the single-QP drop-in to move packed host-order vectors in
 // and out of the tiled SoA layout with one H2D and one D2H transfer.
@@ -627,6 +640,14 @@ int qpb_group_solve(qpb_group *g, const qpb_io *io, const qpb_settings *st, doub
     void *params[] = {&ga};
     hipError_t e = hipModuleLaunchKernel(fn, grid, 1, 1, 64, 1, 1, 0, (hipStream_t)stream, params, nullptr);
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("group launch: ") + hipGetErrorString(e));
+    return QPB_OK;
+}
+
+int qpb_winner(const double *best, const double *x, long n, long B, double *out, void *stream) {
+    if (!best || !x || !out || n < 0 || B < 0) return fail(QPB_EINVAL, "bad winner arguments");
+    hipLaunchKernelGGL(qpb_winner_k, dim3(1), dim3(64), 0, (hipStream_t)stream, best, x, n, B, out);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(QPB_EHIP, std::string("winner: ") + hipGetErrorString(e));
     return QPB_OK;
 }
 

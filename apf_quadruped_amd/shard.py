@@ -2,9 +2,10 @@
 
 QPs are independent, so the batch is cut into contiguous per-rank shards and
 solved with no data-path collective.  The only exchange is config 5's argmin
-gather: each rank reduces its shard to (fval, local index) on device
-(qpb_argmin) and one all_gather of 16 B per rank -- RCCL over xGMI on the GPU,
-gloo in the CPU tests -- lets every rank pick the same global winner.
+gather: each rank reduces its shard to the payload (fval, local index, x*[n])
+on device (qpb_solve_best / qpb_argmin, then qpb_winner) and one all_gather of
+16 + 8n B per rank -- RCCL over xGMI on the GPU, gloo in the CPU tests -- gives
+every rank the same global winner and its solution.
 """
 from __future__ import annotations
 
@@ -25,13 +26,15 @@ def split_even(total: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def global_winner(gathered, offsets):
-    """Pick the global (fval, global index, rank) from per-rank (fval, local
-    index) pairs; index -1 marks a rank with no optimal QP.  Lowest fval wins,
-    ties go to the lowest global index (the same rule as qpb_argmin)."""
-    g = np.asarray(gathered, dtype=np.float64).reshape(-1, 2)
+def global_winner(gathered, offsets, width: int = 2):
+    """Pick the global (fval, global index, rank) from per-rank payloads
+    (fval, local index[, x*...]) of `width` doubles; index -1 marks a rank with
+    no optimal QP.  Lowest fval wins, ties go to the lowest global index (the
+    same rule as qpb_argmin).  The winner's x* is gathered[rank, 2:]."""
+    g = np.asarray(gathered, dtype=np.float64).reshape(-1, width)
     best = (np.inf, -1, -1)
-    for r, (fv, idx) in enumerate(g):
+    for r, row in enumerate(g):
+        fv, idx = row[0], row[1]
         if idx < 0:
             continue
         gi = int(idx) + int(offsets[r])
@@ -41,17 +44,33 @@ def global_winner(gathered, offsets):
 
 
 def all_gather_winner(best_local, world: int):
-    """all_gather of one rank's (fval, index) pair; returns [world, 2].
-    best_local: a 2-element float64 tensor on the rank's device (GPU: RCCL
+    """all_gather of one rank's payload (fval, index[, x*...]); returns
+    [world, len].  best_local: a float64 tensor on the rank's device (GPU: RCCL
     all_gather_into_tensor; CPU/gloo: list all_gather)."""
     import torch
     import torch.distributed as dist
+    w = best_local.numel()
     if world == 1:
-        return best_local.reshape(1, 2)
+        return best_local.reshape(1, w)
     if best_local.is_cuda:
-        out = torch.empty(2 * world, dtype=best_local.dtype, device=best_local.device)
+        out = torch.empty(w * world, dtype=best_local.dtype, device=best_local.device)
         dist.all_gather_into_tensor(out, best_local)
-        return out.reshape(world, 2)
+        return out.reshape(world, w)
     parts = [torch.empty_like(best_local) for _ in range(world)]
     dist.all_gather(parts, best_local)
     return torch.stack(parts)
+
+
+def winner_payload(best, x_tiled, n: int, B: int, out=None, stream=None):
+    """Device payload {fval, index, x*[n]} of a rank's winner (qpb_winner): one
+    small launch on `stream`, no host synchronisation."""
+    import ctypes as C
+    import torch
+    from ._lib import check, lib
+    if out is None:
+        out = torch.empty(2 + n, dtype=torch.float64, device=best.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(best.device)
+    check(lib().qpb_winner(C.c_void_p(best.data_ptr()), C.c_void_p(x_tiled.data_ptr()), int(n), int(B),
+                           C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream)), "qpb_winner")
+    return out

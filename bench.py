@@ -152,7 +152,7 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
     ranks, outputs, gathered winners)."""
     import torch
     import torch.distributed as dist
-    from apf_quadruped_amd.shard import shard_range
+    from apf_quadruped_amd.shard import shard_range, winner_payload
     host = make_shard(plan, seed, shard_range(rank, world, B)[0], B, chunk=65536 if gen is None else 1024, gen=gen)
     vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
     del host
@@ -160,7 +160,10 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
     # {fval, index} of the rank's winner, double-buffered: step i writes bests[i % 2]
     # while step i-1's all_gather may still read the other buffer
     bests = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]
-    gathered = [torch.empty(2 * world, dtype=torch.float64, device=dev) for _ in range(2)]
+    # the gathered payload per rank: {fval, index, x*[n]} (qpb_winner), 16 + 8n B
+    n = plan.n
+    payloads = [torch.zeros(2 + n, dtype=torch.float64, device=dev) for _ in range(2)]
+    gathered = [torch.empty((2 + n) * world, dtype=torch.float64, device=dev) for _ in range(2)]
     stream = torch.cuda.current_stream(dev)
     # one step = qpb_solve_best: the batched solve and the argmin {fval, index}
     # (inside the solve launch for the row kernel -- its last wave reduces the
@@ -175,8 +178,11 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
             works[k].wait()          # stream-side: the gather that read bests[k] is done
         solves[k]()
         if coll:
-            # 16 B per rank, RCCL; async so it overlaps the next step's solve
-            works[k] = dist.all_gather_into_tensor(gathered[k], bests[k], async_op=True)
+            # the winner's payload (one small launch, stream-ordered before the next
+            # solve overwrites x), then 16 + 8n B per rank over RCCL; async so the
+            # gather overlaps the next step's solve
+            winner_payload(bests[k], out["x"], n, B, out=payloads[k], stream=stream)
+            works[k] = dist.all_gather_into_tensor(gathered[k], payloads[k], async_op=True)
 
     for i in range(warmup):
         step(i)
@@ -491,8 +497,9 @@ def main():
         }
         if world > 1:
             from apf_quadruped_amd.shard import global_winner, shard_range
-            fv, gi, rk = global_winner(gathered.cpu().numpy(), [shard_range(r, world, B)[0] for r in range(world)])
-            line["argmin"] = {"fval": fv, "rank": rk, "index": gi}
+            g = gathered.cpu().numpy().reshape(world, -1)
+            fv, gi, rk = global_winner(g, [shard_range(r, world, B)[0] for r in range(world)], width=g.shape[1])
+            line["argmin"] = {"fval": fv, "rank": rk, "index": gi, "x": g[rk, 2:].tolist() if rk >= 0 else None}
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

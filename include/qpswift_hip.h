@@ -133,6 +133,13 @@ int  qpb_solve_best(qpb_plan *plan, long B,
  * none -> {+inf, -1}) to out2 (device, 2 doubles; the index as a double). */
 int  qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *stream);
 
+/* The multi-GPU gather's payload: out[0..1] = best {fval, index}
+ * (from qpb_solve_best / qpb_argmin), out[2..2+n) = x of that QP read from the
+ * tiled outputs x (nv = n, B QPs), NaN when index is -1.  One small launch on
+ * `stream`; all_gather the 2 + n doubles of every rank (RCCL) and every rank
+ * holds the global winner's solution.  DEVICE pointers. */
+int  qpb_winner(const double *best, const double *x, long n, long B, double *out, void *stream);
+
 /* On-device assembly of contact-force QPs (the controller's
  * stance-QP force block, main.cpp:1471-1647): for QP q, feet = foot positions
  * relative to the CoM (tiled, nv = 12: BR, BL, FL, FR, x y z each) and wrench =

@@ -291,3 +291,33 @@ def test_controller_shape_batch_auto_dispatch(B, oracle):
         assert r1["flag"][q] == o["flag"] and r1["iters"][q] == o["iters"], q
         for k in ("x", "z", "s"):
             assert np.abs(r1[k][q] - o[k]).max() <= 1e-9 * max(1.0, np.abs(o[k]).max()), (q, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 1000, 4096])
+def test_winner_payload(B):
+    """qpb_winner: the multi-GPU gather's payload {fval, index, x*[n]} built on the
+    device after qpb_solve_best equals the host argmin and that QP's x; an index
+    of -1 yields NaN for x*."""
+    import torch
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan
+    from apf_quadruped_amd.shard import winner_payload
+    d = W.contact_force_qp(0xD06B07 + 21, np.arange(B))
+    plan = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0])
+    vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"],
+                                                                d["b"]).items()}
+    out = plan.alloc_outputs(B, device="cuda")
+    best = torch.zeros(2, dtype=torch.float64, device="cuda")
+    plan.launcher(vals, out, B, best=best)()
+    pay = winner_payload(best, out["x"], 12, B)
+    torch.cuda.synchronize()
+    r = plan.unpack(out, B)
+    ok = r["flag"] == 0
+    want = int(np.flatnonzero(ok)[np.argmin(r["fval"][ok])])
+    p = pay.cpu().numpy()
+    assert int(p[1]) == want and p[0] == r["fval"][want]
+    np.testing.assert_array_equal(p[2:], r["x"][want])
+    none = torch.tensor([np.inf, -1.0], dtype=torch.float64, device="cuda")
+    p2 = winner_payload(none, out["x"], 12, B).cpu().numpy()
+    assert p2[1] == -1 and np.isnan(p2[2:]).all()

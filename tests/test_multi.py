@@ -3,8 +3,9 @@
 
 Each rank solves its own contiguous shard (here with the oracle, the CPU
 checker), reduces it to (fval, local index) with the qpb_argmin rule, and the
-ranks exchange 16 B each; the gathered winner must equal the single-process
-argmin over the whole batch."""
+ranks exchange their payload (fval, local index, x*[12]: 16 + 96 B each, as
+qpb_winner builds it on the GPU); the gathered winner and its x* must equal the
+single-process argmin over the whole batch."""
 import os
 import socket
 
@@ -34,12 +35,13 @@ def _solve_fvals(ids):
     o = Oracle()
     d = W.contact_force_qp(SEED, ids)
     Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
-    fv, fl = [], []
+    fv, fl, xs = [], [], []
     for k in range(len(ids)):
         r = o.solve_dense(12, 20, 6, Pc[k], Ac[k], Gc[k], d["c"][k], d["h"][k], d["b"][k])
         fv.append(r["fval"])
         fl.append(r["flag"])
-    return np.array(fv), np.array(fl)
+        xs.append(r["x"])
+    return np.array(fv), np.array(fl), np.array(xs)
 
 
 def _local_argmin(fv, fl):
@@ -57,11 +59,13 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = shard_range(rank, world, PER_RANK)
-    fv, fl = _solve_fvals(np.arange(lo, hi))
+    fv, fl, xs = _solve_fvals(np.arange(lo, hi))
     v, i = _local_argmin(fv, fl)
-    g = all_gather_winner(torch.tensor([v, float(i)], dtype=torch.float64), world)
+    payload = np.concatenate([[v, float(i)], xs[i] if i >= 0 else np.full(12, np.nan)])
+    g = all_gather_winner(torch.tensor(payload, dtype=torch.float64), world)
     offsets = [shard_range(r, world, PER_RANK)[0] for r in range(world)]
-    q.put((rank, global_winner(g.numpy(), offsets)))
+    wv, wi, wr = global_winner(g.numpy(), offsets, width=14)
+    q.put((rank, (wv, wi, wr, g.numpy()[wr, 2:].tolist())))
     dist.destroy_process_group()
 
 
@@ -77,10 +81,11 @@ def test_two_rank_gloo_argmin_gather():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    fv, fl = _solve_fvals(np.arange(world * PER_RANK))
+    fv, fl, xs = _solve_fvals(np.arange(world * PER_RANK))
     v, i = _local_argmin(fv, fl)
     for r in range(world):
         assert res[r][0] == v and res[r][1] == i, (r, res[r], (v, i))
+        np.testing.assert_array_equal(res[r][3], xs[i])          # every rank holds the winner's x*
 
 
 def test_shard_helpers():
