@@ -541,7 +541,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         // has finalised it, into one of two 64-slot buffers in the L transpose area
         // (free between the G'WG and the transpose); step k reads it as wave-uniform
         // LDS loads, paired by the compiler
-        double *__restrict__ Bc = Tx;
+        double *Bc = Tx;                         // aliases Tx (no __restrict__: the MFMA tiles and the transpose share it)
         Bc[lane] = H[0];
 #endif
         double dpiv = qpb_xb<0>(H[0]);
