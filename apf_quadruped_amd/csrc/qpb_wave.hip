@@ -332,7 +332,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #else
     const double by = 0.0;
 #endif
-    for (int k = lane; k < OFF_C; k += 64) Ls[k] = 0.0;
+    // the whole per-wave area starts zeroed (staging needs it; the transpose /
+    // scratch area and the exchange vectors then never hold stale bits)
+    for (int k = lane; k < LDS_WAVE; k += 64) Ls[k] = 0.0;
     qpb_wsync();
 #pragma unroll
     for (int u = 0; u < NPL; u++) {
