@@ -64,6 +64,8 @@ def lib() -> C.CDLL:
     L.qpb_plan_destroy.restype = None
     L.qpb_plan_get_info.argtypes = [vp, C.POINTER(QpbPlanInfo)]
     L.qpb_plan_get_perm.argtypes = [vp, lp]
+    L.qpb_amd_order.restype = C.c_int
+    L.qpb_amd_order.argtypes = [C.c_long, lp, lp, lp]
     L.qpb_plan_source.restype = C.c_long
     L.qpb_plan_source.argtypes = [vp, C.c_char_p, C.c_long]
     L.qpb_plan_wave_source.restype = C.c_long

@@ -21,6 +21,10 @@ from . import _lib
 from ._lib import QpbIo, QpbPlanInfo, QpbSettings, check
 
 QPB_P_FULL, QPB_P_UPPER, QPB_EXACT = 0x0, 0x1, 0x10
+# KKT ordering when no permutation is given: "own" (leaves first for small QPs,
+# else minimum degree), "amd" (the reference's AMD: what qpSWIFT computes for
+# Permut = NULL, qpSWIFT.c:424-440), "mindeg", "leaves"
+ORDER_FLAGS = {"own": 0x0, "amd": 0x20, "mindeg": 0x40, "leaves": 0x80}
 QPB_KERNEL_LANE, QPB_KERNEL_WAVE, QPB_KERNEL_NOROW, QPB_KERNEL_TREE = 0x100, 0x200, 0x400, 0x800
 # "wave" = the wave kernel in the form the plan picks (row form: four QPs per
 # wavefront, where it fits); "wave1" = one QP per wavefront regardless
@@ -89,7 +93,8 @@ class Patterns:
 class Plan:
     """One sparsity pattern (+ KKT ordering) and its generated gfx950 kernel."""
 
-    def __init__(self, n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=None, p_upper=True, exact=False, kernel="auto"):
+    def __init__(self, n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=None, p_upper=True, exact=False, kernel="auto",
+                 order="own"):
         L = _lib.lib()
         self.n, self.m, self.p = int(n), int(m), int(p)
         self.p_upper, self.exact = bool(p_upper), bool(exact)
@@ -99,8 +104,9 @@ class Plan:
         self.patterns = Patterns((Pjc, Pir), (Ajc, Air), (Gjc, Gir))
         lp = lambda a: None if a is None else a.ctypes.data_as(C.POINTER(C.c_long))
         h = C.c_void_p()
-        flags = (QPB_P_UPPER if p_upper else QPB_P_FULL) | (QPB_EXACT if exact else 0) | KERNEL_FLAGS[kernel]
-        self.kernel = kernel
+        flags = ((QPB_P_UPPER if p_upper else QPB_P_FULL) | (QPB_EXACT if exact else 0) | KERNEL_FLAGS[kernel]
+                 | ORDER_FLAGS[order])
+        self.kernel, self.order = kernel, order
         check(L.qpb_plan_create(C.byref(h), self.n, self.m, self.p, flags, lp(Pjc), lp(Pir),
                                 lp(Ajc) if self.p else None, lp(Air) if self.p else None,
                                 lp(Gjc), lp(Gir), lp(perm)), "qpb_plan_create")
@@ -121,16 +127,18 @@ class Plan:
             self._h = None
 
     @classmethod
-    def from_dense(cls, n, m, p, P, A, G, perm=None, p_upper=True, exact=False, kernel="auto"):
+    def from_dense(cls, n, m, p, P, A, G, perm=None, p_upper=True, exact=False, kernel="auto", order="own"):
         """Plan for the non-zero pattern of one dense QP (P [n,n], A [p,n], G [m,n]).
         kernel: "auto" (wave kernel for small batches when eligible), "lane", "wave"
         (its row form -- four QPs per wavefront -- where the pattern fits a 16-lane
         row), "wave1" / "auto1" (as "wave" / "auto" but one QP per wavefront),
-        "tree" (one QP per workgroup, level-scheduled sparse LDL'; any pattern)."""
+        "tree" (one QP per workgroup, level-scheduled sparse LDL'; any pattern).
+        order: KKT ordering without `perm` (ORDER_FLAGS; "amd" = the reference's)."""
         Pjc, Pir = dense_pattern(P, upper=p_upper)
         Ajc, Air = dense_pattern(A) if p else (None, None)
         Gjc, Gir = dense_pattern(G)
-        return cls(n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=perm, p_upper=p_upper, exact=exact, kernel=kernel)
+        return cls(n, m, p, Pjc, Pir, Ajc, Air, Gjc, Gir, perm=perm, p_upper=p_upper, exact=exact, kernel=kernel,
+                   order=order)
 
     # -- inspection ---------------------------------------------------------
     def source(self) -> str:

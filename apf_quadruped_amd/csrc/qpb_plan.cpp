@@ -98,7 +98,7 @@ int build_plan(Plan &pl, long n, long m, long p, int pmode,
                const long *Pjc, const long *Pir,
                const long *Ajc, const long *Air,
                const long *Gjc, const long *Gir,
-               const long *perm, std::string *err) {
+               const long *perm, std::string *err, int order) {
     if (n <= 0 || m <= 0 || p < 0) { if (err) *err = "need n > 0, m > 0, p >= 0"; return E_INVAL; }
     if (!check_csc(n, n, Pjc, Pir, err, "P") || !check_csc(m, n, Gjc, Gir, err, "G")) return E_INVAL;
     if (p > 0 && !check_csc(p, n, Ajc, Air, err, "A")) return E_INVAL;
@@ -182,20 +182,28 @@ int build_plan(Plan &pl, long n, long m, long p, int pmode,
         }
         pl.perm.assign(perm, perm + N);
         pl.ordering_kind = 0;
-    } else if (n <= 16 && p <= 16 && m <= 32) {
-        // small QPs (the contact-force shapes): z rows, y rows, then x in natural
-        // order.  Every z / y row is then a leaf (its neighbours are x rows, all
-        // later) and the x block is dense -- the elimination of the row kernel
-        // (qpb_row.hip) for every such pattern; the fill is the same as AMD's on C1
-        // (Lnz 138).  Min-degree instead puts isolated rows (the force variables of
-        // swing feet) first, which leaves the x block out of natural order.
-        for (long i = n + p; i < N; i++) pl.perm.push_back(i);
-        for (long i = n; i < n + p; i++) pl.perm.push_back(i);
-        for (long i = 0; i < n; i++) pl.perm.push_back(i);
-        pl.ordering_kind = 3;
     } else {
-        pl.perm = min_degree_order(K);
-        pl.ordering_kind = 1;
+        if (order == ORDER_OWN) order = (n <= 16 && p <= 16 && m <= 32) ? ORDER_LEAVES : ORDER_MINDEG;
+        if (order == ORDER_LEAVES) {
+            // z rows, y rows, then x in natural order.  Every z / y row is then a
+            // leaf (its neighbours are x rows, all later) and the x block is dense --
+            // the elimination of the row kernel (qpb_row.hip); on C1 the fill equals
+            // AMD's (Lnz 138).
+            for (long i = n + p; i < N; i++) pl.perm.push_back(i);
+            for (long i = n; i < n + p; i++) pl.perm.push_back(i);
+            for (long i = 0; i < n; i++) pl.perm.push_back(i);
+        } else if (order == ORDER_MINDEG) {
+            pl.perm = min_degree_order(K);
+        } else if (order == ORDER_AMD) {
+            // qpSWIFT.c:424-440: AMD with default controls; identity if it fails
+            pl.perm.assign(N, 0);
+            if (amd_order(N, K.jc.data(), K.ir.data(), pl.perm.data()) < 0)
+                for (long i = 0; i < N; i++) pl.perm[i] = i;
+        } else {
+            if (err) *err = "unknown ordering";
+            return E_INVAL;
+        }
+        pl.ordering_kind = order;
     }
     pl.pinv.assign(N, 0);
     for (long k = 0; k < N; k++) pl.pinv[pl.perm[k]] = k;

@@ -5,8 +5,9 @@
 //   * the full symmetric KKT CSC [P A' G'; A 0 0; G 0 -I] exactly as the
 //     reference assembles it (dogbot_controller/src/qpSWIFT/Auxilary.c:71-181),
 //     every slot tagged with the input value it comes from;
-//   * the KKT permutation (caller's, or our own minimum-degree ordering -- the
-//     reference runs SuiteSparse AMD every tick, qpSWIFT.c:416-440);
+//   * the KKT permutation: the caller's, the reference's own AMD ordering
+//     (qpb_amd.cpp; what qpSWIFT computes every tick when Permut = NULL,
+//     qpSWIFT.c:416-440), or one of our orderings (leaves first / min degree);
 //   * the elimination tree and column counts (ldl.c:187-240);
 //   * the exact operation schedule of the up-looking LDL' numeric factorisation
 //     (ldl.c:253-326), obtained by executing its index logic symbolically.
@@ -51,6 +52,25 @@ struct FacStep {
 
 enum PModes : int { P_FULL = 0, P_UPPER = 1 };
 
+// Ordering of the KKT rows when the caller gives no permutation.
+enum Ordering : int {
+    ORDER_CALLER = 0,   // caller's permutation (qpSWIFT's Permut argument)
+    ORDER_MINDEG = 1,   // own exact minimum degree, lowest-index ties
+    ORDER_AMD = 2,      // the reference's AMD (amd_l_order with amd_l_defaults): Permut = NULL
+    ORDER_LEAVES = 3,   // own: z rows, y rows, then x in natural order (small QPs)
+    ORDER_OWN = 4,      // request only: ORDER_LEAVES for n, p <= 16, m <= 32, else ORDER_MINDEG
+};
+
+// amd_l_order's status codes (include/qpSWIFT/amd.h): OK, OK but the columns were
+// unsorted / held duplicates (still ordered), invalid input.
+enum AmdStatus : int { AMD_STATUS_OK = 0, AMD_STATUS_JUMBLED = 1, AMD_STATUS_INVALID = -2 };
+
+// AMD ordering of the n x n pattern (ap, ai) (CSC; A + A' is ordered, the diagonal
+// ignored), written to perm[n]; the same permutation as the reference's
+// amd_l_order for the same pattern and control values (qpb_amd.cpp).
+int amd_order(long n, const long *ap, const long *ai, long *perm, double dense_ratio = 10.0,
+              bool aggressive = true);
+
 struct Plan {
     long n = 0, m = 0, p = 0, N = 0;
     int pmode = P_FULL;
@@ -63,7 +83,7 @@ struct Plan {
     std::vector<Slot> K_loop;                // after updatekktmatrix (IPM loop)
     std::vector<long> perm, pinv, parent, Lp, Li;
     long lnz = 0;
-    int ordering_kind = 0;                   // 0 caller-given, 1 own min-degree, 3 leaves first (z, y, x)
+    int ordering_kind = 0;                   // ORDER_* below: how perm was chosen
     std::vector<FacStep> fac;                // numeric schedule
     long fac_updates = 0, fac_divs = 0;      // op counts (flop accounting)
     uint64_t hash = 0;
@@ -82,12 +102,13 @@ enum Err : int {
 
 // Build a plan.  P pattern is either full (both triangles, as QP_SETUP takes it)
 // or upper-triangular (pmode = P_UPPER, symmetric semantics).  perm may be null:
-// then our own minimum-degree ordering is used.  Returns QPB_OK or an error.
+// then `order` (ORDER_OWN / ORDER_LEAVES / ORDER_MINDEG: ours, ORDER_AMD: the
+// reference's AMD) chooses it.  Returns QPB_OK or an error.
 int build_plan(Plan &pl, long n, long m, long p, int pmode,
                const long *Pjc, const long *Pir,
                const long *Ajc, const long *Air,
                const long *Gjc, const long *Gir,
-               const long *perm, std::string *err);
+               const long *perm, std::string *err, int order = ORDER_OWN);
 
 // Minimum-degree ordering of a symmetric pattern (own implementation; ties go
 // to the lowest index).  Exposed for tests.

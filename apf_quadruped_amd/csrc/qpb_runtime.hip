@@ -322,8 +322,10 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     std::unique_ptr<qpb_plan> plan(new (std::nothrow) qpb_plan());
     if (!plan) return fail(QPB_ENOMEM, "out of host memory");
     std::string err;
+    const int order = (flags & QPB_ORDER_LEAVES) ? qpb::ORDER_LEAVES : (flags & QPB_ORDER_MINDEG) ? qpb::ORDER_MINDEG
+                    : (flags & QPB_ORDER_AMD) ? qpb::ORDER_AMD : qpb::ORDER_OWN;
     int rc = qpb::build_plan(plan->pl, n, m, p, (flags & QPB_P_UPPER) ? qpb::P_UPPER : qpb::P_FULL,
-                             Pjc, Pir, Ajc, Air, Gjc, Gir, perm, &err);
+                             Pjc, Pir, Ajc, Air, Gjc, Gir, perm, &err, order);
     if (rc) return fail(rc, err);
     plan->gen = qpb::choose_options(plan->pl, (flags & QPB_EXACT) != 0);
     // experiment overrides (kernel name encodes them, so caches stay consistent)
@@ -401,6 +403,12 @@ int qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info) {
     info->large_kernel = plan->kernel_pref == 3 ? 3 : plan->kernel_pref == 2 ? 2 : plan->kernel_pref == 1 ? 1
                        : plan->large_tree ? 3 : 1;
     return QPB_OK;
+}
+
+int qpb_amd_order(long n, const long *Ap, const long *Ai, long *perm) {
+    int rc = qpb::amd_order(n, Ap, Ai, perm);
+    if (rc < 0) return fail(QPB_EINVAL, "qpb_amd_order: invalid pattern");
+    return rc;
 }
 
 int qpb_plan_get_perm(const qpb_plan *plan, long *perm) {

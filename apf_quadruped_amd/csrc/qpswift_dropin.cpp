@@ -167,7 +167,7 @@ PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const
         if (it != g_cache.end()) return it->second;
     }
     qpb_plan *raw = nullptr;
-    int rc = qpb_plan_create(&raw, n, m, p, QPB_P_FULL | (exact ? QPB_EXACT : 0), Pjc, Pir, p > 0 ? Ajc : nullptr,
+    int rc = qpb_plan_create(&raw, n, m, p, QPB_P_FULL | QPB_ORDER_AMD | (exact ? QPB_EXACT : 0), Pjc, Pir, p > 0 ? Ajc : nullptr,
                              p > 0 ? Air : nullptr, Gjc, Gir, perm);
     if (rc) {
         err = qpb_last_error();
@@ -175,8 +175,11 @@ PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const
     }
     PlanPtr plan(raw, PlanDeleter());
     // compile only the kernel a batch of one runs (the wave kernel when the plan
-    // is eligible, else the lane kernel): large lane kernels take minutes
-    rc = raw->wave_ok && raw->kernel_pref != 1 ? qpb::compile_wave(raw) : qpb::compile_plan(raw);
+    // is eligible, else the lane kernel): large lane kernels take minutes.  With
+    // no GPU QP_SOLVE fails anyway (QP_FATAL), so setup does not JIT at all.
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) rc = 0;
+    else rc = raw->wave_ok && raw->kernel_pref != 1 ? qpb::compile_wave(raw) : qpb::compile_plan(raw);
     if (rc != 0) {
         err = qpb_last_error();
         return nullptr;

@@ -50,6 +50,14 @@ typedef struct qpb_plan qpb_plan;
 #define QPB_P_FULL   0x0   /* P pattern holds both triangles (QP_SETUP semantics) */
 #define QPB_P_UPPER  0x1   /* P pattern is the upper triangle (symmetric P)        */
 #define QPB_EXACT    0x10  /* bit-faithful arithmetic: IEEE division, no FMA       */
+/* Ordering when perm == NULL.  Default (none of these): ours -- leaves first
+ * (z rows, y rows, then x in natural order) for n, p <= 16, m <= 32, which the
+ * row kernel is built for, else exact minimum degree. */
+#define QPB_ORDER_AMD    0x20  /* the reference's AMD (qpSWIFT.c:424-440, amd_l_defaults):
+                                  QP_SETUP's Permut = NULL -- the same pivots, hence the
+                                  same regularised pivots, as qpSWIFT                 */
+#define QPB_ORDER_MINDEG 0x40  /* exact minimum degree, lowest-index ties             */
+#define QPB_ORDER_LEAVES 0x80  /* z rows, y rows, then x rows in natural order        */
 #define QPB_KERNEL_LANE 0x100  /* always the lane kernel (one QP per lane)         */
 #define QPB_KERNEL_WAVE 0x200  /* always the wave kernel (wave or row form)         */
 #define QPB_KERNEL_NOROW 0x400 /* wave kernel in its one-QP-per-wavefront form even
@@ -77,8 +85,8 @@ typedef struct qpb_plan_info {
     long nnzP, nnzA, nnzG;       /* value counts per QP */
     long nnzK, lnz;              /* nnz of the KKT and of its L factor */
     long fac_updates, fac_divs;  /* LDL numeric op counts per factorisation */
-    int  ordering;               /* 0 caller permutation, 1 own minimum degree, 3 own leaves-first
-                                    (z rows, y rows, x rows; plans with n, p <= 16, m <= 32) */
+    int  ordering;               /* 0 caller permutation, 1 own minimum degree, 2 the reference's AMD,
+                                    3 own leaves-first (z rows, y rows, x rows) */
     int  exact;
     uint64_t hash;               /* pattern + permutation hash */
     int  wave_ok;                /* plan can use the wave-cooperative kernel */
@@ -94,10 +102,16 @@ int  qpb_plan_create(qpb_plan **plan, long n, long m, long p, int flags,
                      const long *Pjc, const long *Pir,
                      const long *Ajc, const long *Air,
                      const long *Gjc, const long *Gir,
-                     const long *perm /* length n+m+p, or NULL = own ordering */);
+                     const long *perm /* length n+m+p, or NULL: own / QPB_ORDER_* */);
 void qpb_plan_destroy(qpb_plan *plan);
 int  qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info);
 int  qpb_plan_get_perm(const qpb_plan *plan, long *perm /* [N] */);
+/* Host-side AMD ordering of an n x n CSC pattern (A + A' ordered, diagonal
+ * ignored; unsorted columns / duplicates allowed): replaces amd_l_order with
+ * amd_l_defaults (src/qpSWIFT/amd_order.c:21-199, include/qpSWIFT/amd.h:339-348)
+ * and writes the same permutation.  Returns 0 (OK), 1 (OK, input was unsorted or
+ * had duplicates) or QPB_EINVAL.  Needs no GPU. */
+int  qpb_amd_order(long n, const long *Ap, const long *Ai, long *perm);
 /* Generated HIP source of the plan's kernel; returns its length (copies at most
  * cap-1 bytes plus a NUL when buf is non-NULL). */
 long qpb_plan_source(const qpb_plan *plan, char *buf, long cap);

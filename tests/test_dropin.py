@@ -7,7 +7,9 @@ elimination-tree mirror that setup fills in equals what reference qpSWIFT's own
 setup produces (oracle/_ref, only where /root/reference was available to build
 it), and QP_SOLVE fails loudly (QP_FATAL) when there is no GPU.
 GPU tests: given the reference's permutation the drop-in is BIT-IDENTICAL to the
-golden vectors; with Permut = NULL (own ordering) it is within 1e-6.
+golden vectors; with Permut = NULL the drop-in orders the KKT with the AMD
+restatement (csrc/qpb_amd.cpp) -- the reference's own permutation -- so the same
+holds for the controller's real call (QP_SETUP_dense(..., NULL, ...) at tol 1e-2).
 """
 import ctypes as C
 import os
@@ -98,15 +100,19 @@ def _setup_mirror(L, qp, n, m, p):
 
 
 @pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref not built (needs /root/reference)")
-@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_rowmajor", "c1_noeq", "mixed_trot_blfr", "edge_zero_g_row"])
-def test_setup_mirror_equals_reference_setup(name):
+@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_rowmajor", "c1_noeq", "mixed_trot_blfr", "edge_zero_g_row",
+                                  "c30_tol1e-2", "c30_trot_tol1e-2", "c30_crawl_tol1e-2", "mpc_h10"])
+@pytest.mark.parametrize("null_perm", [False, True])
+def test_setup_mirror_equals_reference_setup(name, null_perm):
     """Our QP_SETUP_dense fills the KKT CSC (values as assembled), ordering, Pinv,
-    elimination tree, Lp and the transposes exactly as the reference's setup does."""
+    elimination tree, Lp and the transposes exactly as the reference's setup does
+    -- given the permutation, and with Permut = NULL (both run AMD: ours is the
+    restatement in csrc/qpb_amd.cpp, theirs SuiteSparse's amd_l_order)."""
     g = golden(name)
     args = _golden_dense_args(g, 0)
     n, m, p = args[:3]
     keep = [None if a is None else np.ascontiguousarray(a, dtype=np.float64) for a in args[3:]]
-    perm = np.ascontiguousarray(g["perm"][0], dtype=np.int64)
+    perm = None if null_perm else np.ascontiguousarray(g["perm"][0], dtype=np.int64)
     ordering = int(g["ordering"])
     R = abi.bind_qpswift(C.CDLL(REF_SO))
     L = _lib.lib()
@@ -121,13 +127,13 @@ def test_setup_mirror_equals_reference_setup(name):
         assert np.array_equal(np.asarray(ref[key]), np.asarray(ours[key])), key
 
 
-def test_setup_own_ordering_fills_perm_and_amd_result():
+def test_setup_null_permut_fills_reference_perm_and_amd_result():
     g = golden("c1_tol1e-6")
     qp, keep = dropin.setup_dense(*_golden_dense_args(g, 0))
     q = qp.contents
     N = 38
     perm = _arr(q.kkt.contents.P, N)
-    assert sorted(perm.tolist()) == list(range(N))
+    assert np.array_equal(perm, g["perm"][0])        # the reference's AMD ordering
     assert q.stats.contents.AMD_RESULT == 0 and q.stats.contents.Flag == abi.QP_FATAL
     assert int(q.kkt.contents.Lp[N]) > 0
     _lib.lib().QP_CLEANUP_dense(qp)
@@ -180,12 +186,15 @@ def exact_mode(monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", DENSE)
-def test_dropin_dense_bit_identical_to_reference(name, exact_mode):
+@pytest.mark.parametrize("null_perm", [False, True])
+def test_dropin_dense_bit_identical_to_reference(name, null_perm, exact_mode):
+    """Exact mode, given the reference's permutation or with Permut = NULL (AMD
+    restatement): bit-identical x, y, z, s, flag, iterations and fval."""
     g = golden(name)
     tol, maxit = float(g["tol"]), int(g["maxit"])
     for q in range(0, g["x"].shape[0], 7):
-        r = dropin.solve_dense(*_golden_dense_args(g, q), perm=g["perm"][q], ordering=int(g["ordering"]),
-                               reltol=tol, abstol=tol, maxit=maxit)
+        r = dropin.solve_dense(*_golden_dense_args(g, q), perm=None if null_perm else g["perm"][q],
+                               ordering=int(g["ordering"]), reltol=tol, abstol=tol, maxit=maxit)
         assert r["flag"] == int(g["flag"][q]), r["error"]
         assert r["iters"] == int(g["iters"][q])
         for k in ("x", "z", "s"):
@@ -194,7 +203,7 @@ def test_dropin_dense_bit_identical_to_reference(name, exact_mode):
             assert np.array_equal(r["y"], g["y"][q]), (name, q, "y")
         if maxit > 0:   # with maxit = 0 the reference never writes stats->fval (qpSWIFT.c:511)
             assert r["fval"] == float(g["fval"][q])
-        assert r["amd_result"] == -3
+        assert r["amd_result"] == (0 if null_perm else -3)
 
 
 @pytest.mark.gpu
@@ -213,19 +222,30 @@ def test_dropin_csc_bit_identical_to_reference(name, exact_mode):
             assert np.array_equal(r[k], g[k][q]), (name, q, k)
 
 
+CONTROLLER_CALLS = ["c1_tol1e-6", "c1_tol1e-2", "mixed_trot_brfl", "c30_tol1e-2", "c30_tol1e-6", "c30_trot_tol1e-2",
+                    "c30_trot_tol1e-6", "c30_crawl_tol1e-2", "c30_crawl_tol1e-6"]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["c1_tol1e-6", "c1_tol1e-2", "mixed_trot_brfl"])
-def test_dropin_controller_call_own_ordering(name):
-    """Permut = NULL as main.cpp:1649 passes it, default (fast) kernels: own
-    ordering, within 1e-6."""
+@pytest.mark.parametrize("name", CONTROLLER_CALLS)
+def test_dropin_controller_call_null_permut(name):
+    """The controller's real call: QP_SETUP_dense(n, m, p, ..., Permut = NULL,
+    COLUMN_MAJOR_ORDERING) -> reltol = abstol = tol -> QP_SOLVE (main.cpp:1649-1656,
+    2005-2011, 3232-3237), default (fast) kernels.  The drop-in orders the KKT with
+    the AMD restatement, i.e. the reference's permutation, so the regularised
+    pivots are the reference's and x, y, z, s agree to 1e-6 (north-star tolerance)
+    at the controller's tol 1e-2 as well, with the same flag and iteration count."""
     g = golden(name)
-    tol = float(g["tol"])
-    for q in range(0, g["x"].shape[0], 5):
-        r = dropin.solve_dense(*_golden_dense_args(g, q), ordering=int(g["ordering"]), reltol=tol, abstol=tol)
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    for q in range(g["x"].shape[0]):
+        r = dropin.solve_dense(*_golden_dense_args(g, q), ordering=int(g["ordering"]), reltol=tol, abstol=tol,
+                               maxit=maxit)
         assert r["flag"] == int(g["flag"][q]), r["error"]
-        scale = max(1.0, float(np.abs(g["x"][q]).max()))
-        assert np.abs(r["x"] - g["x"][q]).max() <= 1e-6 * scale
-        assert np.abs(r["z"] - g["z"][q]).max() <= 1e-6 * max(1.0, float(np.abs(g["z"][q]).max()))
+        assert r["iters"] == int(g["iters"][q]), (name, q)
+        assert r["amd_result"] == 0
+        for k in ("x", "z", "s") + (("y",) if int(g["p"]) else ()):
+            scale = max(1.0, float(np.abs(g[k][q]).max()))
+            assert np.abs(r[k] - g[k][q]).max() <= 1e-6 * scale, (name, q, k)
 
 
 @pytest.mark.gpu
