@@ -1,7 +1,10 @@
 // qpb_runtime.hip -- C ABI of the batched solver: plans, the code-object cache
 // (hiprtc JIT for gfx950 + on-disk cache), launches, and the argmin reduction.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <spawn.h>
+#include <sys/wait.h>
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -16,6 +19,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/qpswift_hip.h"
@@ -24,6 +28,8 @@
 #include "qpb_runtime.hpp"
 #include "qpb_tree.hpp"
 #include "qpb_wave.hpp"
+
+extern char **environ;
 
 namespace {
 
@@ -161,27 +167,131 @@ qpb_plan::~qpb_plan() {
 
 namespace qpb {
 
-// Compile (hiprtc, gfx950) or fetch from the memory / disk cache.
-int compile_kernel(const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
-                   std::shared_ptr<std::vector<char>> *out) {
-    if (*out) return QPB_OK;
-    std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_code.find(kname);
-    if (it != g_code.end()) { *out = it->second; return QPB_OK; }
-    const std::string dir = cache_dir();
-    const std::string path = dir + "/" + kname + ".hsaco";
-    auto code = std::make_shared<std::vector<char>>();
-    if (!getenv("QPB_NO_DISK_CACHE") && read_file(path, *code)) {
-        g_code[kname] = code;
-        *out = code;
-        return QPB_OK;
+// ---- the kernel compiler ------------------------------------------------------
+// Generated kernels are compiled for gfx950 by ONE pinned compiler: ROCm's clang
+// (ROCM_PATH or /opt/rocm, lib/llvm/bin/clang++; QPB_CLANG overrides), run as a
+// child process.  In-process hiprtc would use whichever libamd_comgr the process
+// loaded first -- torch ships its own ROCm 7.0 comgr, a C++ controller gets
+// /opt/rocm's -- so the same source could become different code objects in a test
+// and in the product.  hiprtc stays as the fallback when no clang is installed.
+// The code-object cache file name carries the compiler's identity and options:
+// <kernel name>.<hash(compiler version, options)>.hsaco.
+
+struct Compiler {
+    std::string clang;   // path, empty -> hiprtc
+    std::string ident;   // version line(s) of the compiler actually used
+};
+
+// run argv, stdout+stderr into *out; returns the exit status (-1: not started)
+static int run_child(const std::vector<std::string> &argv, std::string *out) {
+    char tmpl[] = "/tmp/qpb_logXXXXXX";
+    std::string dir = getenv("TMPDIR") && *getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp";
+    std::string logp = dir + "/qpb_logXXXXXX";
+    std::vector<char> lp(logp.begin(), logp.end());
+    lp.push_back(0);
+    int fd = mkstemp(lp.data());
+    if (fd < 0) { fd = mkstemp(tmpl); if (fd < 0) return -1; lp.assign(tmpl, tmpl + sizeof(tmpl)); }
+    posix_spawn_file_actions_t fa;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_adddup2(&fa, fd, 1);
+    posix_spawn_file_actions_adddup2(&fa, fd, 2);
+    posix_spawn_file_actions_addopen(&fa, 0, "/dev/null", O_RDONLY, 0);
+    std::vector<char *> av;
+    for (auto &a : argv) av.push_back(const_cast<char *>(a.c_str()));
+    av.push_back(nullptr);
+    pid_t pid = 0;
+    int rc = posix_spawn(&pid, av[0], &fa, nullptr, av.data(), environ);
+    posix_spawn_file_actions_destroy(&fa);
+    int status = -1;
+    if (rc == 0) {
+        while (waitpid(pid, &status, 0) < 0 && errno == EINTR) {}
+        status = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
     }
-    std::string src = gen_src();
+    close(fd);
+    if (out) {
+        std::vector<char> buf;
+        read_file(lp.data(), buf);
+        out->assign(buf.begin(), buf.end());
+    }
+    unlink(lp.data());
+    return rc == 0 ? status : -1;
+}
+
+static const Compiler &compiler() {
+    static Compiler c = [] {
+        Compiler r;
+        std::string path;
+        if (const char *e = getenv("QPB_CLANG")) path = e;
+        else {
+            const char *rp = getenv("ROCM_PATH");
+            path = std::string(rp && *rp ? rp : "/opt/rocm") + "/lib/llvm/bin/clang++";
+        }
+        std::string ver;
+        if (path != "hiprtc" && access(path.c_str(), X_OK) == 0 && run_child({path, "--version"}, &ver) == 0) {
+            r.clang = path;
+            r.ident = ver.substr(0, ver.find("\nInstalledDir"));
+        } else {
+            int maj = 0, min = 0;
+            hiprtcVersion(&maj, &min);
+            r.ident = "hiprtc " + std::to_string(maj) + "." + std::to_string(min);
+            // the comgr hiprtc resolved in THIS process (torch's or ROCm's)
+            using getv_t = void (*)(size_t *, size_t *);
+            if (auto gv = (getv_t)dlsym(RTLD_DEFAULT, "amd_comgr_get_version")) {
+                size_t a = 0, b = 0;
+                gv(&a, &b);
+                r.ident += " comgr " + std::to_string(a) + "." + std::to_string(b);
+            }
+            Dl_info di;
+            if (auto sym = dlsym(RTLD_DEFAULT, "amd_comgr_get_version"))
+                if (dladdr(sym, &di) && di.dli_fname) r.ident += std::string(" ") + di.dli_fname;
+        }
+        return r;
+    }();
+    return c;
+}
+
+static std::vector<std::string> compile_options(bool exact) {
+    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    if (exact) o.push_back("-ffp-contract=off");
+    return o;
+}
+
+static int compile_with_clang(const std::string &clang, const std::string &kname, const std::string &src,
+                              bool exact, std::vector<char> &code) {
+    std::string dir = getenv("TMPDIR") && *getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp";
+    const std::string base = dir + "/qpb_" + kname + "_" + std::to_string((long)getpid()) + "_" +
+                             std::to_string((unsigned long)std::hash<std::thread::id>()(std::this_thread::get_id()));
+    const std::string sp = base + ".hip", op = base + ".co";
+    {
+        std::ofstream f(sp, std::ios::binary);
+        if (!f) return fail(QPB_ECOMPILE, "cannot write " + sp);
+        f << src;
+    }
+    std::vector<std::string> argv = {clang, "-x", "hip", "--cuda-device-only", "--no-gpu-bundle-output",
+                                     "-I" + clang.substr(0, clang.rfind("/lib/llvm/bin/")) + "/include",
+                                     "-include", "hip/hip_runtime.h"};
+    for (auto &o : compile_options(exact)) argv.push_back(o);
+    argv.push_back("-o");
+    argv.push_back(op);
+    argv.push_back(sp);
+    std::string log;
+    const int st = run_child(argv, &log);
+    unlink(sp.c_str());
+    if (st != 0 || !read_file(op, code)) {
+        unlink(op.c_str());
+        return fail(QPB_ECOMPILE, "clang (" + clang + ") exit " + std::to_string(st) + ": " + log.substr(0, 4000));
+    }
+    unlink(op.c_str());
+    return QPB_OK;
+}
+
+static int compile_with_hiprtc(const std::string &kname, const std::string &src, bool exact, std::vector<char> &code) {
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), (kname + ".hip").c_str(), 0, nullptr, nullptr) != HIPRTC_SUCCESS)
         return fail(QPB_ECOMPILE, "hiprtcCreateProgram failed");
-    std::vector<const char *> opts = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    if (exact) opts.push_back("-ffp-contract=off");
+    const auto opt = compile_options(exact);
+    std::vector<const char *> opts;
+    for (auto &o : opt) opts.push_back(o.c_str());
     hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     if (rc != HIPRTC_SUCCESS) {
         size_t ls = 0;
@@ -193,9 +303,38 @@ int compile_kernel(const std::string &kname, const std::function<std::string()> 
     }
     size_t cs = 0;
     hiprtcGetCodeSize(prog, &cs);
-    code->resize(cs);
-    hiprtcGetCode(prog, code->data());
+    code.resize(cs);
+    hiprtcGetCode(prog, code.data());
     hiprtcDestroyProgram(&prog);
+    return QPB_OK;
+}
+
+std::string compiler_ident() { return compiler().ident; }
+
+// Compile or fetch from the memory / disk cache (keyed by compiler identity).
+int compile_kernel(const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
+                   std::shared_ptr<std::vector<char>> *out) {
+    if (*out) return QPB_OK;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_code.find(kname);
+    if (it != g_code.end()) { *out = it->second; return QPB_OK; }
+    const Compiler &cc = compiler();
+    std::string id = cc.ident;
+    for (auto &o : compile_options(exact)) id += " " + o;
+    char tag[17];
+    snprintf(tag, sizeof tag, "%016llx", (unsigned long long)fnv1a(id));
+    const std::string dir = cache_dir();
+    const std::string path = dir + "/" + kname + "." + tag + ".hsaco";
+    auto code = std::make_shared<std::vector<char>>();
+    if (!getenv("QPB_NO_DISK_CACHE") && read_file(path, *code)) {
+        g_code[kname] = code;
+        *out = code;
+        return QPB_OK;
+    }
+    const std::string src = gen_src();
+    const int rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
+                                    : compile_with_clang(cc.clang, kname, src, exact, *code);
+    if (rc) return rc;
     mkdir(dir.c_str(), 0755);
     write_file(path, *code);
     g_code[kname] = code;
@@ -305,7 +444,12 @@ int strided_copy(const CopySegs &t, void *stream) {
 extern "C" {
 
 const char *qpb_last_error(void) { return g_err.c_str(); }
-const char *qpb_version(void) { return "qpswift-hip 0.1 (gfx950)"; }
+const char *qpb_version(void) { return "qpswift-hip 0.2 (gfx950)"; }
+
+const char *qpb_compiler(void) {
+    static std::string id = qpb::compiler_ident();
+    return id.c_str();
+}
 
 void qpb_default_settings(qpb_settings *st) {
     st->maxit = 100;

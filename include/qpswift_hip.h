@@ -193,6 +193,11 @@ int  qpb_group_solve(qpb_group *group, const qpb_io *io, const qpb_settings *st,
 
 const char *qpb_last_error(void);
 const char *qpb_version(void);
+/* Identity (version text) of the compiler that builds the generated kernels:
+ * ROCm's clang run as a child process (pinned, whatever HIP libraries the host
+ * process loaded), or hiprtc + the comgr it resolved when clang is absent.  The
+ * code-object cache is keyed by it. */
+const char *qpb_compiler(void);
 
 #ifdef __cplusplus
 }
