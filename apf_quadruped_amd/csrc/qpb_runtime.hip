@@ -253,6 +253,14 @@ static const Compiler &compiler() {
 static std::vector<std::string> compile_options(bool exact) {
     std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
     if (exact) o.push_back("-ffp-contract=off");
+    // experiments only (diagnostics): extra compiler options, e.g. "-O1"; part of
+    // the cache key.  A process keeps one code object per kernel name, so run
+    // each variant in its own process.
+    if (const char *e = getenv("QPB_CLANG_FLAGS")) {
+        std::istringstream in(e);
+        std::string t;
+        while (in >> t) o.push_back(t);
+    }
     return o;
 }
 
