@@ -65,6 +65,12 @@ def lib() -> C.CDLL:
     L.qpb_plan_destroy.restype = None
     L.qpb_plan_get_info.argtypes = [vp, C.POINTER(QpbPlanInfo)]
     L.qpb_plan_get_perm.argtypes = [vp, lp]
+    L.qpb_comm_get_unique_id.argtypes = [vp]
+    L.qpb_comm_init.argtypes = [C.POINTER(vp), C.c_int, vp, C.c_int]
+    L.qpb_comm_destroy.argtypes = [vp]
+    L.qpb_comm_destroy.restype = None
+    L.qpb_argmin_allgather.argtypes = [vp, vp, C.c_long, C.c_long, C.c_long, vp, vp, vp]
+    L.qpb_argmin_reduce.argtypes = [vp, C.c_long, C.c_long, vp, vp]
     L.qpb_amd_order.restype = C.c_int
     L.qpb_amd_order.argtypes = [C.c_long, lp, lp, lp]
     L.qpb_plan_source.restype = C.c_long

@@ -183,7 +183,11 @@ int build_plan(Plan &pl, long n, long m, long p, int pmode,
         pl.perm.assign(perm, perm + N);
         pl.ordering_kind = 0;
     } else {
-        if (order == ORDER_OWN) order = (n <= 16 && p <= 16 && m <= 32) ? ORDER_LEAVES : ORDER_MINDEG;
+        // own ordering: leaves first wherever the x block fits the wave kernel's
+        // dense block (one row per lane): the row kernel for the contact-force
+        // shapes, a 30-row dense block instead of AMD's 45-51 for the controller
+        // shapes; minimum degree beyond (MPC horizon: the tree kernel)
+        if (order == ORDER_OWN) order = (n <= 64 && p <= 64 && m <= 256) ? ORDER_LEAVES : ORDER_MINDEG;
         if (order == ORDER_LEAVES) {
             // z rows, y rows, then x in natural order.  Every z / y row is then a
             // leaf (its neighbours are x rows, all later) and the x block is dense --

@@ -251,7 +251,16 @@ static const Compiler &compiler() {
 }
 
 static std::vector<std::string> compile_options(bool exact) {
-    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    // -amdgpu-enable-pre-ra-optimizations=0: works around a ROCm 7.2 backend
+    // miscompile.  An -opt-bisect-limit search on the
+    // leaves-first trot wave kernel (scripts/diag_wave72.py) found this pass --
+    // which only merges the two S_MOV_B32 halves of 64-bit SGPR constants into
+    // S_MOV_B64_IMM_PSEUDO -- as the first transformation after which the
+    // kernel computes wrong iterates; with it off the results match the oracle
+    // to 1e-10, and -sgpr-regalloc=fast breaks even the stance kernel, i.e. the
+    // fault follows SGPR register allocation, not the source.
+    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-mllvm",
+                                  "-amdgpu-enable-pre-ra-optimizations=0"};
     if (exact) o.push_back("-ffp-contract=off");
     // experiments only (diagnostics): extra compiler options, e.g. "-O1"; part of
     // the cache key.  A process keeps one code object per kernel name, so run
@@ -813,20 +822,16 @@ int qpb_winner(const double *best, const double *x, long n, long B, double *out,
 
 int qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *stream) {
     if (B < 0 || !out2 || (B > 0 && (!fval || !flag))) return fail(QPB_EINVAL, "bad argmin arguments");
-    // partials live in a per-device scratch buffer (grown on demand, never freed)
-    static thread_local std::map<int, std::pair<void *, long>> scratch;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return fail(QPB_EHIP, "hipGetDevice failed");
+    // partials live in the per-(device, stream) scratch of the fused argmin:
+    // launches on one stream are ordered, launches on different streams never
+    // share partials
     const long nb = std::max(1L, std::min(1024L, (B + 4095) / 4096));
     const long chunk = (B + nb - 1) / nb;
-    auto &buf = scratch[dev];
-    if (buf.second < nb) {
-        if (buf.first) (void)hipFree(buf.first);
-        if (hipMalloc(&buf.first, (size_t)nb * 16) != hipSuccess) { buf = {nullptr, 0}; return fail(QPB_ENOMEM, "argmin scratch"); }
-        buf.second = nb;
-    }
-    double *pv = (double *)buf.first;
-    long *pi = (long *)((char *)buf.first + nb * 8);
+    unsigned long long *part = nullptr;
+    unsigned *ctr = nullptr;
+    if (int rc = qpb::argmin_scratch(stream, nb, &part, &ctr)) return rc;
+    double *pv = (double *)part;
+    long *pi = (long *)((char *)part + nb * 8);
     if (nb == 1) {   // one block covers the batch: a single launch writes the result
         hipLaunchKernelGGL(qpb_argmin_single, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, fval, flag, out2);
     } else {

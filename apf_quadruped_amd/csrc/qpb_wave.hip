@@ -51,6 +51,9 @@ struct qpb_args {
 #ifndef QPB_W_REGS         // 1: this lane's slices of P, A, G in registers; 0: read LDS in place
 #define QPB_W_REGS (QPB_NX <= 16 && QPB_NZ <= 32)
 #endif
+#ifndef QPB_W_LDSB_SYNC     // 1: a wave fence between publishing column k+1 and reading it (diagnostic)
+#define QPB_W_LDSB_SYNC 0
+#endif
 #ifndef QPB_W_TIMING
 #define QPB_W_TIMING 0    // 1: phase timestamps (s_memtime) of QP 0 of each tile into stats (debug)
 #endif
@@ -567,6 +570,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 H[j] = __builtin_fma(Bc[cb + j], nl, H[j]);
                 if constexpr (j == k + 1) Bc[nb + lane] = H[j];      // column k+1 is final
             });
+            if constexpr (QPB_W_LDSB_SYNC) qpb_wsync();
 #else
             qpb_for<k + 1, ND>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;

@@ -314,6 +314,20 @@ struct Workspace {
     double *zmem = nullptr;    // zero-copy slab: fine-grained pinned host memory the kernel reads / writes
     double *zdev = nullptr;    //   its device-side address
     long dcap = 0, hcap = 0, zcap = 0;   // doubles
+    Workspace() = default;
+    Workspace(const Workspace &) = delete;
+    Workspace &operator=(const Workspace &) = delete;
+    // released when the solving thread exits (a controller on pooled or
+    // short-lived threads must not leak one stream + slabs per thread)
+    ~Workspace() {
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        if (dmem) (void)hipFree(dmem);
+        if (hmem) (void)hipHostFree(hmem);
+        if (zmem) (void)hipHostFree(zmem);
+    }
 };
 
 // QP_SOLVE moves one QP's data either by zero copy (default for the fast kernels:
@@ -384,10 +398,15 @@ int ensure_device(Priv &v, const QP &q) {
         if (w.zmem) (void)hipHostFree(w.zmem);
         w.zcap = 0;
         w.zdev = nullptr;
-        if (hipHostMalloc((void **)&w.zmem, sizeof(double) * (size_t)v.ototal, hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer((void **)&w.zdev, w.zmem, 0) != hipSuccess) {
+        if (hipHostMalloc((void **)&w.zmem, sizeof(double) * (size_t)v.ototal, hipHostMallocCoherent) != hipSuccess) {
             w.zmem = nullptr;
             return qpb::set_error(QPB_ENOMEM, "QP_SOLVE: mapped pinned host allocation failed");
+        }
+        if (hipHostGetDevicePointer((void **)&w.zdev, w.zmem, 0) != hipSuccess) {
+            (void)hipHostFree(w.zmem);
+            w.zmem = nullptr;
+            w.zdev = nullptr;
+            return qpb::set_error(QPB_EHIP, "QP_SOLVE: mapped pinned host memory has no device address");
         }
         w.zcap = v.ototal;
     }

@@ -2,10 +2,12 @@
 
 QPs are independent, so the batch is cut into contiguous per-rank shards and
 solved with no data-path collective.  The only exchange is config 5's argmin
-gather: each rank reduces its shard to the payload (fval, local index, x*[n])
-on device (qpb_solve_best / qpb_argmin, then qpb_winner) and one all_gather of
-16 + 8n B per rank -- RCCL over xGMI on the GPU, gloo in the CPU tests -- gives
-every rank the same global winner and its solution.
+gather: each rank reduces its shard to the payload (fval, global index, x*[n])
+on device and one all_gather of 16 + 8n B per rank gives every rank the same
+global winner and its solution.  On the GPUs that is qpb_argmin_allgather (C ABI:
+payload kernel, ncclAllGather over RCCL / xGMI, device-side reduce, all on one
+stream; ArgminGather below); the CPU tests run the same logic over gloo
+(all_gather_winner + global_winner).
 """
 from __future__ import annotations
 
@@ -74,3 +76,42 @@ def winner_payload(best, x_tiled, n: int, B: int, out=None, stream=None):
     check(lib().qpb_winner(C.c_void_p(best.data_ptr()), C.c_void_p(x_tiled.data_ptr()), int(n), int(B),
                            C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream)), "qpb_winner")
     return out
+
+
+class ArgminGather:
+    """The multi-GPU argmin gather through the library's C ABI (RCCL over xGMI).
+
+    Rank 0 creates an RCCL unique id (qpb_comm_get_unique_id); every rank gets
+    it through torch.distributed's object broadcast (bootstrap only -- the data
+    path never goes through torch) and joins the communicator on its current
+    device (qpb_comm_init).  `gather(best, x, n, B, base, out, stream)` is one
+    stream-ordered qpb_argmin_allgather: out = {fval, global index, x*[n]} of the
+    global winner on every rank."""
+
+    def __init__(self, rank: int, world: int):
+        import ctypes as C
+        import torch.distributed as dist
+        from ._lib import check, lib
+        self._C, self._check, self._lib = C, check, lib
+        idb = C.create_string_buffer(128)
+        if rank == 0:
+            check(lib().qpb_comm_get_unique_id(idb), "qpb_comm_get_unique_id")
+        obj = [idb.raw if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(obj, src=0)
+        idb = C.create_string_buffer(obj[0], 128)
+        h = C.c_void_p()
+        check(lib().qpb_comm_init(C.byref(h), int(world), idb, int(rank)), "qpb_comm_init")
+        self.comm, self.rank, self.world = h, rank, world
+
+    def gather(self, best, x, n: int, B: int, base: int, out, stream):
+        C = self._C
+        self._check(self._lib().qpb_argmin_allgather(
+            C.c_void_p(best.data_ptr()), C.c_void_p(x.data_ptr()), int(n), int(B), int(base), self.comm,
+            C.c_void_p(out.data_ptr()), C.c_void_p(stream.cuda_stream)), "qpb_argmin_allgather")
+        return out
+
+    def close(self):
+        if self.comm is not None and self.comm.value:
+            self._lib().qpb_comm_destroy(self.comm)
+        self.comm = None

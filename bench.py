@@ -6,7 +6,8 @@ Workload = BASELINE.json configs[1]: a batch of 1 024 identical-sparsity C1
 contact-force QPs (12 vars / 20 ineq / 6 eq) per GPU.  One step =
 one batched IPM solve (kkt_initialize + QP_SOLVE) of this rank's
 resident batch followed by the device-side argmin; for N > 1 the per-rank
-winners are exchanged with one RCCL all_gather (config 5's argmin gather).
+winners are exchanged with one RCCL all_gather (config 5's argmin gather:
+qpb_argmin_allgather, the library's C ABI, on a second stream).
 Shards are independent (weak scaling): rank r owns QP ids [r*B, (r+1)*B);
 config 5 (65 536 QPs over 8 GPUs) is `--gpus 8 --batch 8192`.
 
@@ -83,12 +84,39 @@ def flops_per_qp(info, iters):
     return (fac + solve + 2 * info.nnzG) + iters * per_it + resid
 
 
+def host_cpus():
+    """The host cores this process can run on: the affinity set, capped by the
+    cgroup CPU quota when one is set (a GPU box shares its host: os.cpu_count()
+    shows the whole machine, the quota is this job's share), plus the CPU model."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return dict(threads=use, affinity_cpus=aff, nproc=os.cpu_count(), cgroup_quota_cpus=quota, model=model)
+
+
 def cpu_baseline(seed, sample, passes, tol, gen=None, label="C1"):
-    """Reference qpSWIFT (oracle/_ref) on the host cores; port (oracle) if absent.
+    """Reference qpSWIFT on ALL host cores this process may use (host_cpus):
+    oracle/_ref (the reference's own C sources compiled by `make -C oracle ref`
+    in the build container) when present, else the oracle restatement ("port").
     gen(ids) -> dense QP dict (default: C1 contact-force QPs)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from apf_quadruped_amd import workloads as W
-    threads = max(1, min(16, os.cpu_count() or 1))
+    hc = host_cpus()
+    threads = hc["threads"]
     d = gen(np.arange(sample)) if gen is not None else W.contact_force_qp(seed, np.arange(sample))
     n, m, p = int(d["n"]), int(d["m"]), int(d["p"])
     P, A, G = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
@@ -119,6 +147,9 @@ def cpu_baseline(seed, sample, passes, tol, gen=None, label="C1"):
     return dict(value=sample * passes / dt, unit="QP solves/s", cores=threads, kind=kind,
                 sample=f"{sample} {label} QPs x {passes} passes, setup+solve per QP (QP_SETUP_dense + QP_SOLVE "
                        f"+ QP_CLEANUP_dense, AMD ordering), tol {tol:g}, {threads} threads, {dt:.2f} s wall",
+                build=("oracle/Makefile `ref`: reference qpSWIFT C sources, gcc -O2" if kind == "reference"
+                       else "oracle/qpswift_oracle.c restatement, gcc -O2"),
+                host={k: hc[k] for k in ("affinity_cpus", "nproc", "cgroup_quota_cpus", "model")},
                 mean_iters=float(iters.mean()), optimal_frac=float((flags == 0).mean()))
 
 
@@ -152,37 +183,52 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
     ranks, outputs, gathered winners)."""
     import torch
     import torch.distributed as dist
-    from apf_quadruped_amd.shard import shard_range, winner_payload
-    host = make_shard(plan, seed, shard_range(rank, world, B)[0], B, chunk=65536 if gen is None else 1024, gen=gen)
+    from apf_quadruped_amd.shard import ArgminGather, shard_range
+    base = shard_range(rank, world, B)[0]
+    host = make_shard(plan, seed, base, B, chunk=65536 if gen is None else 1024, gen=gen)
     vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
     del host
-    out = plan.alloc_outputs(B, device=dev)
-    # {fval, index} of the rank's winner, double-buffered: step i writes bests[i % 2]
-    # while step i-1's all_gather may still read the other buffer
-    bests = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(2)]
-    # the gathered payload per rank: {fval, index, x*[n]} (qpb_winner), 16 + 8n B
+    coll = gather and world > 1
+    nbuf = 2 if coll else 1
+    # outputs and the rank's {fval, index} are double-buffered when the gather runs:
+    # step i solves into set i % 2 while step i-1's gather may still read the other
+    outs = [plan.alloc_outputs(B, device=dev) for _ in range(nbuf)]
+    bests = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(nbuf)]
     n = plan.n
-    payloads = [torch.zeros(2 + n, dtype=torch.float64, device=dev) for _ in range(2)]
-    gathered = [torch.empty((2 + n) * world, dtype=torch.float64, device=dev) for _ in range(2)]
     stream = torch.cuda.current_stream(dev)
     # one step = qpb_solve_best: the batched solve and the argmin {fval, index}
     # (inside the solve launch for the row kernel -- its last wave reduces the
     # per-wave partials -- else a separate single-block launch on the same stream)
-    solves = [plan.launcher(vals, out, B, reltol=tol, abstol=tol, stream=stream, best=b) for b in bests]
-    coll = gather and world > 1
-    works = [None, None]
+    solves = [plan.launcher(vals, outs[k], B, reltol=tol, abstol=tol, stream=stream, best=bests[k])
+              for k in range(nbuf)]
+    if coll:
+        # the argmin gather (SURVEY §8e) through the C ABI: qpb_argmin_allgather =
+        # payload kernel + ncclAllGather of 16 + 8n B per rank (RCCL, xGMI) + device
+        # reduce, on its own stream so it overlaps the next step's solve
+        try:
+            ag = ArgminGather(rank, world)
+        except Exception as e:       # keep the scaling run alive: same RCCL, through torch
+            print(f"[rank {rank}] qpb_comm_init failed ({e}); torch all_gather fallback", file=sys.stderr)
+            ag = _TorchGather(world)
+        gs = torch.cuda.Stream(dev)
+        winners = [torch.zeros(2 + n, dtype=torch.float64, device=dev) for _ in range(nbuf)]
+        solved = [torch.cuda.Event() for _ in range(nbuf)]
+        gathered_ev = [None] * nbuf
 
     def step(i):
-        k = i & 1
-        if works[k] is not None:
-            works[k].wait()          # stream-side: the gather that read bests[k] is done
+        k = i % nbuf
+        if not coll:
+            solves[k]()
+            return
+        if gathered_ev[k] is not None:
+            stream.wait_event(gathered_ev[k])     # step i-2's gather has read outs[k]
         solves[k]()
-        if coll:
-            # the winner's payload (one small launch, stream-ordered before the next
-            # solve overwrites x), then 16 + 8n B per rank over RCCL; async so the
-            # gather overlaps the next step's solve
-            winner_payload(bests[k], out["x"], n, B, out=payloads[k], stream=stream)
-            works[k] = dist.all_gather_into_tensor(gathered[k], payloads[k], async_op=True)
+        solved[k].record(stream)
+        gs.wait_event(solved[k])
+        ag.gather(bests[k], outs[k]["x"], n, B, base, winners[k], gs)
+        if gathered_ev[k] is None:
+            gathered_ev[k] = torch.cuda.Event()
+        gathered_ev[k].record(gs)
 
     for i in range(warmup):
         step(i)
@@ -193,9 +239,6 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
     t0 = time.perf_counter()
     for i in range(steps):
         step(i)
-    for w in works:
-        if w is not None:
-            w.wait()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -219,8 +262,41 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
-    last = (steps - 1) & 1
-    return elapsed, kern_ms, out, (gathered[last] if coll else bests[last].reshape(1, 2))
+    last = (steps - 1) % nbuf
+    if coll:
+        result = winners[last].clone()
+        ag.close()
+    else:
+        result = bests[last].clone()
+    return elapsed, kern_ms, outs[last], result
+
+
+class _TorchGather:
+    """Fallback for ArgminGather when the library's RCCL communicator cannot be
+    made: payload (qpb_winner, global index) + torch's all_gather_into_tensor (also
+    RCCL) + qpb_argmin_reduce, on the same stream."""
+
+    def __init__(self, world):
+        self.world = world
+        self.comm = None
+
+    def gather(self, best, x, n, B, base, out, stream):
+        import ctypes as C
+        import torch
+        import torch.distributed as dist
+        from apf_quadruped_amd import _lib
+        from apf_quadruped_amd.shard import winner_payload
+        with torch.cuda.stream(stream):
+            pay = winner_payload(best, x, n, B, stream=stream)
+            pay[1] = torch.where(pay[1] >= 0, pay[1] + base, pay[1])
+            g = torch.empty((2 + n) * self.world, dtype=torch.float64, device=pay.device)
+            dist.all_gather_into_tensor(g, pay)
+            _lib.check(_lib.lib().qpb_argmin_reduce(C.c_void_p(g.data_ptr()), self.world, n, C.c_void_p(out.data_ptr()),
+                                                    C.c_void_p(stream.cuda_stream)), "qpb_argmin_reduce")
+        return out
+
+    def close(self):
+        pass
 
 
 def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
@@ -496,10 +572,11 @@ def main():
             "cpu_baseline": cpu,
         }
         if world > 1:
-            from apf_quadruped_amd.shard import global_winner, shard_range
-            g = gathered.cpu().numpy().reshape(world, -1)
-            fv, gi, rk = global_winner(g, [shard_range(r, world, B)[0] for r in range(world)], width=g.shape[1])
-            line["argmin"] = {"fval": fv, "rank": rk, "index": gi, "x": g[rk, 2:].tolist() if rk >= 0 else None}
+            g = gathered.cpu().numpy()          # {fval, global index, x*} from qpb_argmin_allgather
+            gi = int(g[1])
+            line["argmin"] = {"fval": float(g[0]), "index": gi, "rank": gi // B if gi >= 0 else -1,
+                              "x": g[2:].tolist() if gi >= 0 else None,
+                              "collective": "qpb_argmin_allgather (RCCL ncclAllGather, 16 + 8n B per rank)"}
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -25,11 +25,24 @@
  *   permutation, pivots and regularisations and agree with qpSWIFT to rounding.
  *   QPSWIFT_HIP_EXACT=1 in the environment selects the bit-faithful kernel (the
  *   reference's operation order, IEEE division, no FMA): bit-identical to
- *   qpSWIFT when given the same permutation.  With Permut == NULL the ordering
- *   is this library's own minimum-degree ordering instead of SuiteSparse AMD;
- *   results then differ from qpSWIFT's by the reordering (measured <= 1e-11
- *   relative at tol 1e-6; up to ~4e-6 relative on 30-variable QPs at the
- *   controller's tol 1e-2).
+ *   qpSWIFT when given the same permutation.  With Permut == NULL the KKT is
+ *   ordered by this library's restatement of SuiteSparse AMD (amd_l_order with
+ *   amd_l_defaults, src/qpSWIFT/qpSWIFT.c:424-440), which yields qpSWIFT's own
+ *   permutation (bit-for-bit, tests/test_amd.py); stats->AMD_RESULT is then 0,
+ *   and -3 when Permut is given, as in the reference.
+ *
+ * Fields that differ from the reference:
+ *   stats->kkt_time, stats->ldl_numeric  always 0: the factorisation and the
+ *       triangular solves are fused with the rest of each iteration into one
+ *       device launch, so they have no separate host-side timing; tsetup and
+ *       tsolve hold the host wall time of QP_SETUP* / QP_SOLVE.
+ *   options->sigma  every QP_SOLVE starts from SIGMA (100) -- the value the
+ *       reference's setup stores (qpSWIFT.c:74, 275) -- and the final sigma is
+ *       not written back (the reference leaves its last sigma there).
+ *   options->verbose  accepted and ignored (no printing).
+ *   QP_SOLVE on the same QP object again re-runs the initial point and the loop
+ *       from the current input values (the reference continues from its last
+ *       iterate; for a converged QP both return the same x at once).
  */
 #ifndef QPSWIFT_HIP_DROPIN_H
 #define QPSWIFT_HIP_DROPIN_H
@@ -114,7 +127,7 @@ typedef struct stats {
     qp_int resolve_kkt;
 } stats;
 
-/* settings (Auxilary.h:89-100); verbose is accepted and ignored */
+/* settings (Auxilary.h:89-100); sigma and verbose: see the header comment */
 typedef struct settings {
     qp_int maxit;
     qp_real reltol;

@@ -51,8 +51,12 @@ typedef struct qpb_plan qpb_plan;
 #define QPB_P_UPPER  0x1   /* P pattern is the upper triangle (symmetric P)        */
 #define QPB_EXACT    0x10  /* bit-faithful arithmetic: IEEE division, no FMA       */
 /* Ordering when perm == NULL.  Default (none of these): ours -- leaves first
- * (z rows, y rows, then x in natural order) for n, p <= 16, m <= 32, which the
- * row kernel is built for, else exact minimum degree. */
+ * (z rows, y rows, then x in natural order) for n, p <= 64, m <= 256 (the row
+ * kernel's elimination for the contact-force shapes; a dense block of n rows for
+ * the wave kernel), else exact minimum degree.  Either agrees with qpSWIFT to
+ * 1e-6 at its default tolerance; loosely converged iterates (the controller's
+ * tol 1e-2) depend on which pivots get regularised, i.e. on the ordering --
+ * QPB_ORDER_AMD reproduces qpSWIFT's. */
 #define QPB_ORDER_AMD    0x20  /* the reference's AMD (qpSWIFT.c:424-440, amd_l_defaults):
                                   QP_SETUP's Permut = NULL -- the same pivots, hence the
                                   same regularised pivots, as qpSWIFT                 */
@@ -165,6 +169,29 @@ int  qpb_winner(const double *best, const double *x, long n, long B, double *out
 int  qpb_assemble_contact(const qpb_plan *plan, long B, const double *feet, const double *wrench,
                           int stance, double mu, double *P, double *A, double *G,
                           double *c, double *h, double *b, void *stream);
+
+/* ---- the multi-GPU argmin gather: RCCL over xGMI ----
+ * One process per GPU, each solving its own shard (no data-path collective).
+ * A communicator is an ncclComm_t: the caller's own, or one made here from a
+ * unique id (QPB_COMM_ID_BYTES) that rank 0 creates and every rank receives out
+ * of band.  RCCL is loaded on first use (librccl.so.1). */
+#define QPB_COMM_ID_BYTES 128
+int  qpb_comm_get_unique_id(void *id /* QPB_COMM_ID_BYTES */);
+int  qpb_comm_init(void **comm, int nranks, const void *id, int rank);   /* on the current HIP device */
+void qpb_comm_destroy(void *comm);
+/* Every rank calls this after qpb_solve_best on its shard: best = that shard's
+ * {fval, index} (DEVICE), x = its tiled x (nv = n, B QPs), base = global index of
+ * its QP 0.  Builds the rank's payload {fval, base + index, x*[n]} on the device,
+ * all-gathers the 16 + 8n bytes of every rank (ncclAllGather) and reduces them on
+ * the device: out (DEVICE, 2 + n doubles) = {fval, global index, x*} of the
+ * global winner (lowest fval among optimal QPs, ties -> lowest global index; none
+ * -> {+inf, -1, NaN...}).  Stream-ordered on `stream`; replaces the per-candidate
+ * selection the controller would otherwise do on the host. */
+int  qpb_argmin_allgather(const double *best, const double *x, long n, long B, long base, void *comm,
+                          double *out, void *stream);
+/* Step 3 alone: out = winner over `world` gathered payloads of width 2 + n
+ * (DEVICE pointers). */
+int  qpb_argmin_reduce(const double *gathered, long world, long n, double *out, void *stream);
 
 /* ---- plan groups: one launch for a batch of mixed sparsity patterns ----
  * The APF planner's candidates differ in their stance sets (gait phases), i.e.
