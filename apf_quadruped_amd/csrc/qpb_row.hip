@@ -92,18 +92,29 @@ template <int CTRL> static __device__ __forceinline__ double qpb_dpp(double v) {
 }
 
 // acc += (src of row lane J) * m as one v_fmac_f64 with a DPP row_newbcast
-// source.  A DPP source must not have been written by the two preceding VALU
-// instructions:
-//  - qpb_fxs: src is a static slice written in the prologue (never a hazard);
-//  - qpb_fx:  src is dynamic; the phase starts with qpb_fence(src, ...), and
-//             both are volatile so they keep their order;
+// source (the compiler does not fold a 64-bit DPP move into an FMA).  A DPP
+// source must not have been written by the two preceding VALU instructions, and
+// the compiler's hazard recognizer cannot see into inline asm -- nor can the
+// source code rule out a VALU copy the register allocator places right before
+// the asm (e.g. out of an AGPR).  So every DPP asm carries its own two wait
+// states (QPB_DPP_NOP, default on; 0 only for A/B measurements):
+//  - qpb_fxs: static sources (prologue slices) and the factor's columns;
+//  - qpb_fx:  dynamic sources, volatile so a phase keeps its order;
 //  - qpb_fxd: the chained triangular solves (src is the accumulator itself).
+#ifndef QPB_DPP_NOP
+#define QPB_DPP_NOP 1
+#endif
+#if QPB_DPP_NOP
+#define QPB_DPP_PRE "s_nop 1\n\t"
+#else
+#define QPB_DPP_PRE ""
+#endif
 template <int J> static __device__ __forceinline__ void qpb_fxs(double &acc, double src, double m) {
-    asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+    asm(QPB_DPP_PRE "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
         : "+v"(acc) : "v"(src), "v"(m), "i"(J));
 }
 template <int J> static __device__ __forceinline__ void qpb_fx(double &acc, double src, double m) {
-    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+    asm volatile(QPB_DPP_PRE "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
                  : "+v"(acc) : "v"(src), "v"(m), "i"(J));
 }
 template <int J> static __device__ __forceinline__ void qpb_fxd(double &t, double m) {

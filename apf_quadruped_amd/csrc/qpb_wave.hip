@@ -118,12 +118,22 @@ template <int J> static __device__ __forceinline__ double qpb_xb(double v) {
 
 // acc + (v of dense lane J) * m as ONE v_fmac_f64 with a DPP row_newbcast
 // source (the compiler does not fold a 64-bit DPP move into a VOP2 FMA).  The
-// caller guarantees that v was not written by the two preceding VALU
-// instructions (the DPP read hazard): every use below reads a value produced
-// several dependent instructions earlier.
+// DPP read hazard (v written by one of the two preceding VALU instructions) is
+// invisible to the compiler's hazard recognizer inside inline asm, and a VALU
+// copy placed by the register allocator right before the asm cannot be ruled
+// out from the source, so the asm carries its own two wait states
+// (QPB_DPP_NOP, default on; 0 only for A/B measurements).
+#ifndef QPB_DPP_NOP
+#define QPB_DPP_NOP 1
+#endif
+#if QPB_DPP_NOP
+#define QPB_DPP_PRE "s_nop 1\n\t"
+#else
+#define QPB_DPP_PRE ""
+#endif
 template <int J> static __device__ __forceinline__ double qpb_fmac_xb(double acc, double v, double m) {
     if constexpr (ND <= 16) {
-        asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        asm(QPB_DPP_PRE "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
             : "+v"(acc) : "v"(v), "v"(m), "i"(J));
         return acc;
     } else {

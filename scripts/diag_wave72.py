@@ -31,6 +31,8 @@ VARIANTS = {
     "no_dce_in_ra": {"QPB_CLANG_FLAGS": "-mllvm -amdgpu-dce-in-ra=0"},
     "sgpr_ra_fast": {"QPB_CLANG_FLAGS": "-mllvm -sgpr-regalloc=fast"},
     "no_prealloc_spill": {"QPB_CLANG_FLAGS": "-mllvm -amdgpu-prealloc-sgpr-spill-vgprs=0"},
+    # the row kernel's parked fault (illegal address with all three knobs on)
+    "row_knobs": {"QPB_WAVE_OPTS": "QPB_R_ZF128=1 QPB_R_AADPP=1 QPB_R_LATEFAC=1", "QPB_DIAG_PHASES": "c1row"},
     "maxit0": {"QPB_DIAG_MAXIT": "0"},
     "maxit1": {"QPB_DIAG_MAXIT": "1"},
     "maxit2": {"QPB_DIAG_MAXIT": "2"},
@@ -48,17 +50,26 @@ def child(variant, phases=("trot", "stance", "crawl")):
     o = Oracle()
     res = {"variant": variant, "compiler": _lib.lib().qpb_compiler().decode().split("\n")[0]}
     B = 64
-    for phase, seed in (("trot", plans.SEED + 31), ("stance", plans.SEED + 30), ("crawl", plans.SEED + 31)):
+    if os.environ.get("QPB_DIAG_PHASES"):
+        phases = tuple(os.environ["QPB_DIAG_PHASES"].split(","))
+    for phase, seed in (("trot", plans.SEED + 31), ("stance", plans.SEED + 30), ("crawl", plans.SEED + 31),
+                        ("c1row", plans.SEED + 1)):
         if phase not in phases:
             continue
-        d = (W.controller_qp(seed, np.arange(B)) if phase == "stance"
-             else W.controller_qp(seed, np.arange(B), phase=phase))
-        n, m, p = 30, d["m"], d["p"]
-        pl = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0], kernel="wave1", order="leaves")
+        if phase == "c1row":                 # C1 contact-force QPs on the row kernel, B = 1024
+            B = 1024
+            d = W.contact_force_qp(seed, np.arange(B))
+            n, m, p = 12, 20, 6
+            pl = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0], kernel="wave")
+        else:
+            d = (W.controller_qp(seed, np.arange(B)) if phase == "stance"
+                 else W.controller_qp(seed, np.arange(B), phase=phase))
+            n, m, p = 30, d["m"], d["p"]
+            pl = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0], kernel="wave1", order="leaves")
         maxit = int(os.environ.get("QPB_DIAG_MAXIT", "100"))
         out = pl.unpack(pl.solve(**pl.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]), B=B, maxit=maxit), B)
         worst, nbad = 0.0, 0
-        for q in range(0, B, 8):
+        for q in range(0, B, B // 8):
             ref = o.solve_dense(n, m, p, W.to_colmajor(d["P"])[q], W.to_colmajor(d["A"])[q],
                                 W.to_colmajor(d["G"])[q], d["c"][q], d["h"][q], d["b"][q], perm=pl.perm, maxit=maxit)
             dx = float(np.abs(out["x"][q] - ref["x"]).max())

@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ticks", type=int, default=200)
-    ap.add_argument("--shape", default="c1", choices=["c1", "c30"])
+    ap.add_argument("--shape", default="c1", choices=["c1", "c30", "c30_trot", "c30_crawl"])
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--tol", type=float, default=1e-2)        # the controller's (main.cpp:1651)
     a = ap.parse_args()
@@ -30,8 +30,10 @@ def main():
         os.environ["QPSWIFT_HIP_EXACT"] = "1"
     else:
         os.environ.pop("QPSWIFT_HIP_EXACT", None)
-    gen = (lambda ids: W.contact_force_qp(plans.SEED + 1, ids)) if a.shape == "c1" else \
-        (lambda ids: W.controller_qp(plans.SEED + 30, ids))
+    gen = {"c1": lambda ids: W.contact_force_qp(plans.SEED + 1, ids),
+           "c30": lambda ids: W.controller_qp(plans.SEED + 30, ids),
+           "c30_trot": lambda ids: W.controller_qp(plans.SEED + 31, ids, phase="trot"),
+           "c30_crawl": lambda ids: W.controller_qp(plans.SEED + 31, ids, phase="crawl")}[a.shape]
     d = gen(np.arange(a.ticks))
     n, m, p = d["n"], d["m"], d["p"]
     P, A, G = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])

@@ -8,7 +8,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o b -- python3 bench.py --no-cpu --steps 20 --warmup 2 > gpurun_out/pmc_fetch.log 2>&1; rc=$?; echo "fetch rc=$rc"; fatal $rc fetch
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o b -- python3 bench.py --no-cpu --steps 20 --warmup 2 > gpurun_out/pmc_write.log 2>&1; rc=$?; echo "write rc=$rc"; fatal $rc write
 : > gpurun_out/dropin_latency.jsonl
-for sh in c1 c30; do for md in fast exact; do
-  [ "$sh" = c30 ] && [ "$md" = exact ] && continue
+for sh in c1 c30 c30_trot c30_crawl; do for md in fast exact; do
+  [ "$sh" != c1 ] && [ "$md" = exact ] && continue
   timeout -k 10 120 python -u scripts/dropin_latency.py --shape $sh --mode $md >> gpurun_out/dropin_latency.jsonl 2>gpurun_out/dl.err; rc=$?; echo "dropin $sh $md rc=$rc"; fatal $rc dropin
 done; done
