@@ -96,18 +96,26 @@ template <int CTRL> static __device__ __forceinline__ double qpb_dpp(double v) {
 // source must not have been written by the two preceding VALU instructions, and
 // the compiler's hazard recognizer cannot see into inline asm -- nor can the
 // source code rule out a VALU copy the register allocator places right before
-// the asm (e.g. out of an AGPR).  So every DPP asm carries its own two wait
-// states (QPB_DPP_NOP, default on; 0 only for A/B measurements):
+// the asm (e.g. out of an AGPR).  So the runtime audits every compiled code
+// object (qpb_runtime.hip, dpp_audit: no write of a DPP instruction's VGPR
+// operands within 2 wait states, no VALU exec write within 5, across branches)
+// and, should it find one, rebuilds the kernel with QPB_DPP_NOP = 2: wait states
+// inside every DPP asm (25 % slower, never needed so far).
 //  - qpb_fxs: static sources (prologue slices) and the factor's columns;
 //  - qpb_fx:  dynamic sources, volatile so a phase keeps its order;
 //  - qpb_fxd: the chained triangular solves (src is the accumulator itself).
 #ifndef QPB_DPP_NOP
-#define QPB_DPP_NOP 1
+#define QPB_DPP_NOP 0
 #endif
-#if QPB_DPP_NOP
+#if QPB_DPP_NOP >= 2
+#define QPB_DPP_PRE "s_nop 4\n\t"
+#define QPB_DPP_DEP "s_nop 4\n\t"
+#elif QPB_DPP_NOP
 #define QPB_DPP_PRE "s_nop 1\n\t"
+#define QPB_DPP_DEP "s_nop 1\n\t"
 #else
 #define QPB_DPP_PRE ""
+#define QPB_DPP_DEP "s_nop 1\n\t"
 #endif
 template <int J> static __device__ __forceinline__ void qpb_fxs(double &acc, double src, double m) {
     asm(QPB_DPP_PRE "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
@@ -118,7 +126,7 @@ template <int J> static __device__ __forceinline__ void qpb_fx(double &acc, doub
                  : "+v"(acc) : "v"(src), "v"(m), "i"(J));
 }
 template <int J> static __device__ __forceinline__ void qpb_fxd(double &t, double m) {
-    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+    asm volatile(QPB_DPP_DEP "v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
                  : "+v"(t) : "v"(m), "i"(J));
 }
 static __device__ __forceinline__ void qpb_fence(double a) { asm volatile("s_nop 1" ::"v"(a)); }

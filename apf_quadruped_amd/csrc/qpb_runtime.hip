@@ -9,6 +9,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -328,6 +329,162 @@ static int compile_with_hiprtc(const std::string &kname, const std::string &src,
 
 std::string compiler_ident() { return compiler().ident; }
 
+// ---- DPP hazard audit of a compiled code object ----------------------------
+// The row / wave kernels issue v_fmac_f64_dpp from inline asm, where the
+// compiler's hazard recognizer cannot insert the wait states a DPP instruction
+// needs: 2 after a write of its DPP-permuted source VGPR (src0; the cross-lane
+// read happens early in the pipeline), 5 after a VALU write of EXEC.  (The
+// compiler applies the 2-state rule to every VGPR operand of its own DPP code;
+// the production row kernel has writes of src1 right before its DPP FMAs and is
+// equal to the oracle to 1e-9, so src1 / the accumulator are not checked.)  The
+// audit disassembles the code object (llvm-objdump) and checks every DPP
+// instruction against every path into it, branches included.  Returns 1 clean,
+// 0 hazard found (report says where), -1 could not audit.
+struct AsmInsn {
+    uint64_t addr = 0;
+    std::string mn;
+    std::vector<std::pair<int, int>> vregs;   // every v register operand, [lo, hi]
+    bool vdef0 = false;                       // first operand is a VGPR the instruction writes
+    bool exec_valu_def = false;               // v_cmpx*: VALU write of EXEC
+    bool dpp = false, uncond = false;
+    int ws = 1;                               // wait states the instruction itself provides
+    long long target = -1;                    // branch target address
+};
+
+static bool parse_vreg(const std::string &t, std::pair<int, int> &r) {
+    size_t i = 0;
+    while (i < t.size() && (t[i] == ' ' || t[i] == '-' || t[i] == '|')) i++;
+    if (i + 1 >= t.size() || t[i] != 'v') return false;
+    if (t[i + 1] == '[') {
+        int a = 0, b = 0;
+        if (sscanf(t.c_str() + i + 2, "%d:%d]", &a, &b) != 2) return false;
+        r = {a, b};
+        return true;
+    }
+    if (!isdigit((unsigned char)t[i + 1])) return false;
+    int a = atoi(t.c_str() + i + 1);
+    r = {a, a};
+    return true;
+}
+
+int dpp_audit(const std::vector<char> &code, std::string *report) {
+    const Compiler &cc = compiler();
+    std::string objdump;
+    if (!cc.clang.empty()) objdump = cc.clang.substr(0, cc.clang.rfind('/')) + "/llvm-objdump";
+    else {
+        const char *rp = getenv("ROCM_PATH");
+        objdump = std::string(rp && *rp ? rp : "/opt/rocm") + "/lib/llvm/bin/llvm-objdump";
+    }
+    if (access(objdump.c_str(), X_OK) != 0) { *report = "no llvm-objdump"; return -1; }
+    std::string dir = getenv("TMPDIR") && *getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp";
+    const std::string path = dir + "/qpb_audit_" + std::to_string((long)getpid()) + "_" +
+                             std::to_string((unsigned long)std::hash<std::thread::id>()(std::this_thread::get_id())) + ".co";
+    write_file(path, code);
+    std::string dis;
+    const int st = run_child({objdump, "-d", "--mcpu=gfx950", path}, &dis);
+    unlink(path.c_str());
+    if (st != 0) { *report = "llvm-objdump failed"; return -1; }
+    std::vector<AsmInsn> ins;
+    std::map<uint64_t, size_t> at;
+    uint64_t fbase = 0;
+    std::istringstream in(dis);
+    std::string line;
+    while (std::getline(in, line)) {
+        if (!line.empty() && isxdigit((unsigned char)line[0]) && line.find(">:") != std::string::npos) {
+            fbase = strtoull(line.c_str(), nullptr, 16);          // "0000000000001d00 <name>:"
+            continue;
+        }
+        if (line.empty() || line[0] != '\t') continue;
+        const size_t cm = line.find("// ");
+        if (cm == std::string::npos) continue;
+        AsmInsn a;
+        a.addr = strtoull(line.c_str() + cm + 3, nullptr, 16);
+        std::string text = line.substr(1, cm - 1);
+        std::istringstream ts(text);
+        ts >> a.mn;
+        std::string rest;
+        std::getline(ts, rest);
+        std::vector<std::string> ops;
+        {
+            std::string cur;
+            for (char ch : rest) {
+                if (ch == ',') { ops.push_back(cur); cur.clear(); }
+                else cur += ch;
+            }
+            if (!cur.empty()) {     // the last operand may carry modifiers after a space
+                std::istringstream ls(cur);
+                std::string first;
+                ls >> first;
+                ops.push_back(first);
+            }
+        }
+        for (auto &o : ops) {
+            std::pair<int, int> r;
+            if (parse_vreg(o, r)) a.vregs.push_back(r);
+        }
+        const std::string &m = a.mn;
+        a.dpp = m.find("_dpp") != std::string::npos;
+        const bool no_vdst = m.rfind("s_", 0) == 0 || m.find("store") != std::string::npos ||
+                             m.rfind("ds_write", 0) == 0 || m.rfind("v_cmp", 0) == 0 ||
+                             m.rfind("v_readlane", 0) == 0 || m.rfind("v_readfirstlane", 0) == 0;
+        std::pair<int, int> r0;
+        a.vdef0 = !no_vdst && !ops.empty() && parse_vreg(ops[0], r0);
+        a.exec_valu_def = m.rfind("v_cmpx", 0) == 0;
+        if (m == "s_nop") a.ws = 1 + (int)strtol(rest.c_str(), nullptr, 0);
+        a.uncond = m == "s_branch" || m == "s_endpgm" || m.rfind("s_setpc", 0) == 0;
+        if (m == "s_branch" || m.rfind("s_cbranch", 0) == 0) {
+            const size_t lt = line.find('<', cm);
+            if (lt != std::string::npos) {
+                const size_t plus = line.find("+0x", lt);
+                a.target = (long long)(fbase + (plus != std::string::npos ? strtoull(line.c_str() + plus + 3, nullptr, 16) : 0));
+            }
+        }
+        at[a.addr] = ins.size();
+        ins.push_back(std::move(a));
+    }
+    if (ins.empty()) { *report = "empty disassembly"; return -1; }
+    std::map<uint64_t, std::vector<size_t>> preds_by_target;
+    for (size_t i = 0; i < ins.size(); i++)
+        if (ins[i].target >= 0) preds_by_target[(uint64_t)ins[i].target].push_back(i);
+    auto overlap = [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
+        return a.first <= b.second && b.first <= a.second;
+    };
+    int hazards = 0;
+    std::ostringstream rep;
+    for (size_t d = 0; d < ins.size(); d++) {
+        if (!ins[d].dpp) continue;
+        // backward DFS over predecessors; ws = wait states between the visited
+        // instruction and the DPP instruction
+        std::vector<std::pair<size_t, int>> stack;
+        auto push_preds = [&](size_t i, int ws) {
+            if (i > 0 && !ins[i - 1].uncond) stack.push_back({i - 1, ws});
+            auto it = preds_by_target.find(ins[i].addr);
+            if (it != preds_by_target.end())
+                for (size_t p : it->second) stack.push_back({p, ws});
+        };
+        push_preds(d, 0);
+        int guard = 0;
+        while (!stack.empty() && guard++ < 4096) {
+            auto [p, ws] = stack.back();
+            stack.pop_back();
+            const AsmInsn &P = ins[p];
+            bool bad = false;
+            if (ws < 2 && P.vdef0 && ins[d].vregs.size() >= 2 && overlap(P.vregs[0], ins[d].vregs[1])) bad = true;
+            if (ws < 5 && P.exec_valu_def) bad = true;
+            if (bad) {
+                if (hazards++ < 8)
+                    rep << std::hex << "0x" << ins[d].addr << " " << ins[d].mn << " after 0x" << P.addr << " " << P.mn
+                        << std::dec << " (" << ws << " wait states); ";
+                break;
+            }
+            if (ws + P.ws < 5) push_preds(p, ws + P.ws);
+        }
+    }
+    *report = hazards ? std::to_string(hazards) + " DPP hazard(s): " + rep.str() : "clean";
+    return hazards ? 0 : 1;
+}
+
+
 // Compile or fetch from the memory / disk cache (keyed by compiler identity).
 int compile_kernel(const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
                    std::shared_ptr<std::vector<char>> *out) {
@@ -348,12 +505,27 @@ int compile_kernel(const std::string &kname, const std::function<std::string()> 
         *out = code;
         return QPB_OK;
     }
-    const std::string src = gen_src();
-    const int rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
-                                    : compile_with_clang(cc.clang, kname, src, exact, *code);
+    std::string src = gen_src();
+    int rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
+                              : compile_with_clang(cc.clang, kname, src, exact, *code);
     if (rc) return rc;
+    std::string audit = "no DPP asm";
+    if (src.find("v_fmac_f64_dpp") != std::string::npos) {
+        // DPP from inline asm: verify the wait states in the code object; on a
+        // hazard (or no way to check) rebuild with wait states inside every
+        // DPP asm (QPB_DPP_NOP = 2), which is hazard-free by construction
+        const int ok = dpp_audit(*code, &audit);
+        if (ok != 1) {
+            src = "#define QPB_DPP_NOP 2\n" + src;
+            rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
+                                  : compile_with_clang(cc.clang, kname, src, exact, *code);
+            if (rc) return rc;
+            audit += " -> rebuilt with QPB_DPP_NOP=2";
+        }
+    }
     mkdir(dir.c_str(), 0755);
     write_file(path, *code);
+    write_file(path + ".audit", std::vector<char>(audit.begin(), audit.end()));
     g_code[kname] = code;
     *out = code;
     return QPB_OK;
@@ -462,6 +634,19 @@ extern "C" {
 
 const char *qpb_last_error(void) { return g_err.c_str(); }
 const char *qpb_version(void) { return "qpswift-hip 0.2 (gfx950)"; }
+
+int qpb_audit_dpp(const void *code, long size, char *report, long cap) {
+    if (!code || size <= 0) return fail(QPB_EINVAL, "empty code object");
+    std::vector<char> c((const char *)code, (const char *)code + size);
+    std::string rep;
+    const int r = qpb::dpp_audit(c, &rep);
+    if (report && cap > 0) {
+        const long k = std::min<long>(cap - 1, (long)rep.size());
+        std::memcpy(report, rep.data(), (size_t)k);
+        report[k] = 0;
+    }
+    return r;
+}
 
 const char *qpb_compiler(void) {
     static std::string id = qpb::compiler_ident();

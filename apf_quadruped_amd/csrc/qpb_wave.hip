@@ -121,15 +121,21 @@ template <int J> static __device__ __forceinline__ double qpb_xb(double v) {
 // DPP read hazard (v written by one of the two preceding VALU instructions) is
 // invisible to the compiler's hazard recognizer inside inline asm, and a VALU
 // copy placed by the register allocator right before the asm cannot be ruled
-// out from the source, so the asm carries its own two wait states
-// (QPB_DPP_NOP, default on; 0 only for A/B measurements).
+// out from the source: the runtime audits every compiled code object
+// (qpb_runtime.hip, dpp_audit) and rebuilds with QPB_DPP_NOP = 2 (wait states
+// inside every DPP asm) should it find a hazard.
 #ifndef QPB_DPP_NOP
-#define QPB_DPP_NOP 1
+#define QPB_DPP_NOP 0
 #endif
-#if QPB_DPP_NOP
+#if QPB_DPP_NOP >= 2
+#define QPB_DPP_PRE "s_nop 4\n\t"
+#define QPB_DPP_DEP "s_nop 4\n\t"
+#elif QPB_DPP_NOP
 #define QPB_DPP_PRE "s_nop 1\n\t"
+#define QPB_DPP_DEP "s_nop 1\n\t"
 #else
 #define QPB_DPP_PRE ""
+#define QPB_DPP_DEP "s_nop 1\n\t"
 #endif
 template <int J> static __device__ __forceinline__ double qpb_fmac_xb(double acc, double v, double m) {
     if constexpr (ND <= 16) {
@@ -145,7 +151,7 @@ template <int J> static __device__ __forceinline__ double qpb_fmac_xb(double acc
 // two wait states the DPP read needs are inserted explicitly
 template <int J> static __device__ __forceinline__ double qpb_fmac_xb_dep(double acc, double v, double m) {
     if constexpr (ND <= 16) {
-        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        asm(QPB_DPP_DEP "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
             : "+v"(acc) : "v"(v), "v"(m), "i"(J));
         return acc;
     } else {

@@ -225,6 +225,11 @@ const char *qpb_version(void);
  * process loaded), or hiprtc + the comgr it resolved when clang is absent.  The
  * code-object cache is keyed by it. */
 const char *qpb_compiler(void);
+/* DPP hazard audit of a gfx950 code object (the check every generated kernel
+ * with inline-asm DPP passes before it is cached): 1 clean, 0 a write of a DPP
+ * instruction's VGPR operand within 2 wait states or a VALU EXEC write within 5
+ * (report says where), -1 cannot audit (no llvm-objdump). */
+int qpb_audit_dpp(const void *code, long size, char *report, long cap);
 
 #ifdef __cplusplus
 }
