@@ -450,6 +450,22 @@ def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
             "optimal_frac": float((out["flag"] == 0).float().mean().item())}
 
 
+def limiter_for(B):
+    """What the SQ counters say bounds the row kernel at this batch
+    (profiles/r02_sq_row.json, scripts/gpu_sq.sh + scripts/sq_summary.py)."""
+    f = os.path.join(ROOT, "profiles", "r02_sq_row.json")
+    if not os.path.exists(f):
+        return None
+    r = json.load(open(f)).get(f"B={B}")
+    if not r:
+        return None
+    fr = r["frac_of_wave_cycles"]
+    return {"kind": "VALU issue + LDS/memory latency at one wave per SIMD (neither HBM nor FP64 peak)",
+            "valu_active_frac": fr["valu_active"], "waitcnt_frac": fr["wait_any (s_waitcnt: LDS / memory)"],
+            "waves_per_simd": r["waves_per_simd_avg"], "fp64_lane_fma_per_qp": r["per_qp"]["fma_f64_lane_ops"],
+            "source": "profiles/r02_sq_row.json"}
+
+
 def traffic_for(kname, B):
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
@@ -503,7 +519,8 @@ def main():
         large = {"batch": BL, "value": BL * 10 / el, "ms_per_step": el * 1e3 / 10, "kernel": kl,
                  "kernel_ms": km, "kernel_qps": BL / (km * 1e-3),
                  "roofline": {"bound": "hbm", "achieved": achl, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": achl / HBM_PEAK_GBS, "traffic": traffic_for(kl, BL)},
+                              "frac": achl / HBM_PEAK_GBS, "traffic": traffic_for(kl, BL),
+                              "limiter": limiter_for(BL) if kl.startswith("qpb_row") else None},
                  "fp64_tflops": flops_per_qp(plan.info, itl) * BL / (km * 1e-3) / 1e12,
                  "mean_iters": itl, "optimal_frac": float((outl["flag"] == 0).float().mean().item())}
         del outl
@@ -561,7 +578,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(kname, B),
                          "algorithmic_bytes_per_launch": bpq * B, "bytes_per_qp": bpq,
-                         "kernel_ms": kern_ms, "kernel": kname},
+                         "kernel_ms": kern_ms, "kernel": kname,
+                         "limiter": limiter_for(B) if kname.startswith("qpb_row") else None},
             "fp64": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
                      "frac": fp64_tf / FP64_PEAK_TFLOPS, "flops_per_qp": fpq},
             "mean_iters": mean_it,
