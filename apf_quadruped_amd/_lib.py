@@ -26,6 +26,15 @@ class QpbIo(C.Structure):
                                                               "flag", "iters", "fval", "stats")]
 
 
+class QpbApfState(C.Structure):
+    """qpb_apf_state (include/qpswift_hip.h): one tick's state for qpb_apf_wrench."""
+    _fields_ = [("ee", (C.c_double * 2) * 4), ("com", C.c_double * 6), ("com_vel", C.c_double * 6),
+                ("acc_des", C.c_double * 6), ("des_orient", C.c_double * 2), ("rob_foot", C.c_double * 4),
+                ("versor", (C.c_double * 2) * 4), ("lat_versor", C.c_double * 2), ("R_wb", C.c_double * 9),
+                ("Mcom", C.c_double * 36), ("mass", C.c_double), ("rep_field", C.c_int), ("min_exit", C.c_int),
+                ("fake_crawl", C.c_int)]
+
+
 class QpbPlanInfo(C.Structure):
     _fields_ = [("n", C.c_long), ("m", C.c_long), ("p", C.c_long), ("N", C.c_long),
                 ("nnzP", C.c_long), ("nnzA", C.c_long), ("nnzG", C.c_long),
@@ -72,6 +81,8 @@ def lib() -> C.CDLL:
     L.qpb_comm_destroy.restype = None
     L.qpb_argmin_allgather.argtypes = [vp, vp, C.c_long, C.c_long, C.c_long, vp, vp, vp]
     L.qpb_argmin_reduce.argtypes = [vp, C.c_long, C.c_long, vp, vp]
+    L.qpb_assemble_controller.argtypes = [vp, C.c_long, vp, C.c_int, vp, C.c_double] + [vp] * 8
+    L.qpb_apf_wrench.argtypes = [C.c_long, C.POINTER(QpbApfState), vp, vp, vp, vp]
     L.qpb_amd_order.restype = C.c_int
     L.qpb_amd_order.argtypes = [C.c_long, lp, lp, lp]
     L.qpb_plan_source.restype = C.c_long

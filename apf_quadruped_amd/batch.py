@@ -18,7 +18,8 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import QpbIo, QpbPlanInfo, QpbSettings, check
+from ._lib import QpbApfState, QpbIo, QpbPlanInfo, QpbSettings, check
+check_ = check
 
 QPB_P_FULL, QPB_P_UPPER, QPB_EXACT = 0x0, 0x1, 0x10
 # KKT ordering when no permutation is given: "own" (leaves first for small QPs,
@@ -248,6 +249,34 @@ class Plan:
               "qpb_assemble_contact")
         return out
 
+    def assemble_controller(self, terms, B=None, shared=False, wdes=None, mu=0.5, out=None, check=None,
+                            stream=None):
+        """On-device assembly of the controller's stance QP 30/68/18
+        (qpb_assemble_controller): terms = float64 device tensor of robot terms
+        (tiled, nv = workloads.ROBOT_NV; or one shared copy with shared=True),
+        wdes = optional tiled [nv = 6] per-QP desired wrench (e.g. from apf_wrench),
+        check = optional int32 device tensor [B] (1: the QP has the plan's pattern).
+        Returns the dict of the plan's tiled inputs P, A, G, c, h, b."""
+        import torch
+        if B is None:
+            B = wdes.numel() // 6 if (shared and wdes is not None) else terms.numel() // 480
+        B = int(B)
+        T = ntiles(B) * TILE
+        dev = terms.device
+        if out is None:
+            f = dict(dtype=torch.float64, device=dev)
+            out = dict(P=torch.empty(self.info.nnzP * T, **f), A=torch.empty(self.info.nnzA * T, **f),
+                       G=torch.empty(self.info.nnzG * T, **f), c=torch.empty(self.n * T, **f),
+                       h=torch.empty(self.m * T, **f), b=torch.empty(self.p * T, **f))
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda a: None if a is None else C.c_void_p(a.data_ptr())
+        check_(_lib.lib().qpb_assemble_controller(self._h, B, ptr(terms), int(bool(shared)), ptr(wdes), float(mu),
+                                                  ptr(out["P"]), ptr(out["A"]), ptr(out["G"]), ptr(out["c"]),
+                                                  ptr(out["h"]), ptr(out["b"]), ptr(check),
+                                                  C.c_void_p(stream.cuda_stream)), "qpb_assemble_controller")
+        return out
+
     def unpack(self, out, B):
         """Device tiled outputs -> dict of host numpy arrays [B, n] etc."""
         r = dict(x=from_tiled(out["x"], B, self.n).cpu().numpy(),
@@ -454,3 +483,45 @@ def bucket_by_pattern(P, A, G):
     for u in range(len(uniq)):
         keys[u] = np.nonzero(inv.reshape(-1) == u)[0]
     return keys
+
+
+def apf_state(**kw) -> QpbApfState:
+    """qpb_apf_state from keyword arrays (ee [4,2], com [6], com_vel [6], acc_des [6],
+    des_orient [2], rob_foot [4], versor [4,2], lat_versor [2], R_wb [3,3], Mcom [6,6],
+    mass, rep_field, min_exit, fake_crawl)."""
+    st = QpbApfState()
+    for name, _ in QpbApfState._fields_:
+        if name not in kw:
+            continue
+        v = kw[name]
+        if name in ("mass",):
+            st.mass = float(v)
+        elif name in ("rep_field", "min_exit", "fake_crawl"):
+            setattr(st, name, int(bool(v)))
+        else:
+            flat = np.asarray(v, np.float64).reshape(-1)
+            arr = getattr(st, name)
+            if name in ("ee", "versor"):
+                for i in range(4):
+                    for j in range(2):
+                        arr[i][j] = flat[2 * i + j]
+            else:
+                for i, x in enumerate(flat):
+                    arr[i] = x
+    return st
+
+
+def apf_wrench(state: QpbApfState, targets, K=None, wrench=None, com_des=None, stream=None):
+    """qpb_apf_wrench: APF-sampled targets (tiled nv = 2 float64 device tensor) ->
+    desired CoM wrench (tiled nv = 6) [and CoMPosDes] per candidate."""
+    import torch
+    K = int(targets.numel() // 2 if K is None else K)
+    T = ntiles(K) * TILE
+    if wrench is None:
+        wrench = torch.empty(6 * T, dtype=torch.float64, device=targets.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(targets.device)
+    p = lambda a: None if a is None else C.c_void_p(a.data_ptr())
+    check(_lib.lib().qpb_apf_wrench(K, C.byref(state), p(targets), p(wrench), p(com_des),
+                                    C.c_void_p(stream.cuda_stream)), "qpb_apf_wrench")
+    return wrench

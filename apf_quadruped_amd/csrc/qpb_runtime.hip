@@ -157,6 +157,13 @@ __global__ void __launch_bounds__(256) qpb_strided_copy(qpb::CopySegs t) {
 }  // namespace
 
 qpb_plan::~qpb_plan() {
+    for (auto &kv : ctl_dev) {
+        int cur = 0;
+        if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
+            (void)hipFree(kv.second);
+            (void)hipSetDevice(cur);
+        }
+    }
     for (auto &kv : tree_dev) {
         int cur = 0;
         if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {

@@ -28,6 +28,8 @@ struct qpb_plan {
     std::shared_ptr<std::vector<char>> tree_code;
     std::vector<char> tree_tables;              // plan tables of the tree kernel (host copy)
     std::map<int, void *> tree_dev;             // device -> uploaded tables
+    std::vector<int> ctl_table;                 // controller-QP assembly entries (qpb_assemble_controller)
+    std::map<int, void *> ctl_dev;              // device -> uploaded entries
     ~qpb_plan();
 };
 

@@ -309,25 +309,32 @@ def to_colmajor(M: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(np.transpose(M, (0, 2, 1))).reshape(M.shape[0], -1)
 
 
-def controller_qp(seed: int, qp_ids, phase: str = "stance"):
-    """Controller-shape stance QP "C30" (30 vars / 68 ineq / 18 eq), following
-    dogbot_controller/src/client/main.cpp:1471-1647 (SURVEY §8a shape table):
+# Per-QP robot terms of the controller's stance QP, in the layout of
+# qpb_assemble_controller (include/qpswift_hip.h): the quantities main.cpp:1471-1647
+# reads from iDynTree / the planner each tick.
+ROBOT_TERMS = (("Jst", 12 * 18),     # JacCOM_lin: foot rows BR BL FL FR x [CoM 6 | joints 12], row-major
+               ("Mcom", 36),         # MassMatrixCOM(0:6, 0:6), row-major
+               ("Mjj", 144),         # MassMatrixCOM(6:18, 6:18), row-major
+               ("bias", 18),         # BiasCOM
+               ("jdqd", 12),         # JdqdCOM_lin
+               ("wdes", 6),          # Wcom_des (main.cpp:1571)
+               ("q", 12), ("dq", 12), ("qmin", 12), ("qmax", 12))
+ROBOT_NV = sum(k for _, k in ROBOT_TERMS)
 
-    x = [ddx_com (6); ddq (12); f (12)], Sigma_st selects f (main.cpp:496-497)
-      Q = 50 T_s' T_s + I, T_s = Jc' Sigma_st          (main.cpp:1476-1480)
-      c = -50 T_s' W_des                                (main.cpp:1573)
-      A = [M_com 0 -Jc'; Jc J_j 0], b = [-bias_com; -Jdqd] (main.cpp:1579-1588)
-      D rows: friction 0-19 on f, tau_max 20-31 = [0 M_jj -J_j'],
-              tau_min 32-43 = -(same), ddq_max 44-55 = [0 I 0], ddq_min 56-67 = [0 -I 0]
-      C: 0, 60 - bias_j, 60 + bias_j, ddq_max, -ddq_min  (main.cpp:1627-1647, deltat 0.025)
-    Synthetic robot terms (no rigid-body model here): M_com = blkdiag(m I3, I_c),
-    dense SPD M_jj, leg-dominant dense J_j, bias ~ U(-2, 2), q ~ U(-0.5, 0.5),
-    dq ~ U(-0.2, 0.2), joint limits +-1.5 rad.  The equality right-hand side is
-    made consistent with a random state (ddx*, ddq*, f* inside the friction
-    pyramids) so every QP is feasible.  Returns the same dict layout as
-    contact_force_qp (dense row-major [B, r, c])."""
-    if phase != "stance":
-        return controller_swing_qp(seed, qp_ids, phase)
+
+def pack_terms(t: dict) -> np.ndarray:
+    """terms dict -> [B, ROBOT_NV] rows in the ROBOT_TERMS layout."""
+    B = t["Jst"].shape[0]
+    return np.concatenate([np.asarray(t[k], np.float64).reshape(B, -1) for k, _ in ROBOT_TERMS], 1)
+
+
+def controller_terms(seed: int, qp_ids):
+    """The synthetic robot state behind controller_qp (stance): contact Jacobian
+    [Jc | J_j], M_com = blkdiag(m I3, I_c), dense SPD M_jj, biases, joint state and
+    limits, desired wrench.  BiasCOM(0:6) and JdqdCOM_lin are chosen so that the
+    equality right-hand side b = -[BiasCOM(0:6); Jdqd] (main.cpp:1584-1587) is
+    consistent with a random state (ddx*, ddq*, f* inside the friction pyramids),
+    so every QP is feasible."""
     qp_ids = np.atleast_1d(np.asarray(qp_ids, dtype=np.int64))
     B = len(qp_ids)
     Jc, W = contact_terms(seed, qp_ids)
@@ -363,21 +370,45 @@ def controller_qp(seed: int, qp_ids, phase: str = "stance"):
     uf = take(12).reshape(B, 4, 3)
     fz = 40.0 + 60.0 * uf[..., 2]
     f = np.stack([(0.8 * uf[..., 0] - 0.4) * MU * fz, (0.8 * uf[..., 1] - 0.4) * MU * fz, fz], -1).reshape(B, 12)
+    Jst = np.concatenate([Jc, Jj], 2)
+    A = _controller_A(Jst, Mcom)
+    b = np.einsum("bij,bj->bi", A, np.concatenate([ddx, ddq, f], 1))  # consistent with (ddx*, ddq*, f*)
+    bias = np.concatenate([-b[:, 0:6], bias_j], 1)
+    return dict(Jst=Jst, Mcom=Mcom, Mjj=Mjj, bias=bias, jdqd=-b[:, 6:18], wdes=W, q=q, dq=dq,
+                qmin=np.full((B, 12), -1.5), qmax=np.full((B, 12), 1.5))
 
+
+def _controller_A(Jst, Mcom):
+    """eigenA (main.cpp:1579-1582): [M_com 0 -Jstcom'; Jstcom Jstj 0]."""
+    B = Jst.shape[0]
+    A = np.zeros((B, 18, 30))
+    A[:, 0:6, 0:6] = Mcom
+    A[:, 0:6, 18:30] = -np.transpose(Jst[:, :, 0:6], (0, 2, 1))
+    A[:, 6:18, 0:18] = Jst
+    return A
+
+
+def controller_qp_from_terms(t: dict, mu: float = MU):
+    """The controller's stance QP 30/68/18 from its robot terms, restating
+    main.cpp:1471-1647 (the numpy reference of qpb_assemble_controller):
+      Q = 50 T_s' T_s + I, T_s = Jstcom' Sigma_st;  c = -T_s' (50 I)' W
+      A = [M_com 0 -Jstcom'; Jstcom Jstj 0], b = [-BiasCOM(0:6); -Jdqd]
+      D = friction | [0 M_jj -Jstj'] | -(same) | [0 I 0] | [0 -I 0]
+      C = 0 | tau_max - bias_j | -(tau_min - bias_j) | ddq_max | -ddq_min, tau = 60,
+          ddq_lim = (2 / dt^2)(q_lim - q - dt dq), dt = 0.025."""
+    Jst, Mcom, Mjj = (np.asarray(t[k], np.float64) for k in ("Jst", "Mcom", "Mjj"))
+    B = Jst.shape[0]
     n, m, p = 30, 68, 18
+    Jc, Jj = Jst[:, :, 0:6], Jst[:, :, 6:18]
     Ts = np.zeros((B, 6, n))
     Ts[:, :, 18:30] = np.transpose(Jc, (0, 2, 1))
     P = 50.0 * np.einsum("bki,bkj->bij", Ts, Ts) + np.eye(n)[None]
-    c = -50.0 * np.einsum("bki,bk->bi", Ts, W)
-    A = np.zeros((B, p, n))
-    A[:, 0:6, 0:6] = Mcom
-    A[:, 0:6, 18:30] = -np.transpose(Jc, (0, 2, 1))
-    A[:, 6:18, 0:6] = Jc
-    A[:, 6:18, 6:18] = Jj
-    xs = np.concatenate([ddx, ddq, f], 1)
-    b = np.einsum("bij,bj->bi", A, xs)                              # consistent with (ddx*, ddq*, f*)
+    c = -50.0 * np.einsum("bki,bk->bi", Ts, np.asarray(t["wdes"], np.float64))
+    A = _controller_A(Jst, Mcom)
+    bias = np.asarray(t["bias"], np.float64)
+    b = np.concatenate([-bias[:, 0:6], -np.asarray(t["jdqd"], np.float64)], 1)
     G = np.zeros((B, m, n))
-    cfr = friction_block(MU)
+    cfr = friction_block(mu)
     for i in range(4):
         G[:, 5 * i:5 * i + 5, 18 + 3 * i:18 + 3 * i + 3] = cfr
     JjT = np.transpose(Jj, (0, 2, 1))
@@ -388,12 +419,27 @@ def controller_qp(seed: int, qp_ids, phase: str = "stance"):
     G[:, 44:56, 6:18] = np.eye(12)[None]
     G[:, 56:68, 6:18] = -np.eye(12)[None]
     dt = 0.025
-    qmax, qmin = 1.5, -1.5
-    ddq_max = (2 / dt ** 2) * (qmax - q - dt * dq)
-    ddq_min = (2 / dt ** 2) * (qmin - q - dt * dq)
+    q, dq = np.asarray(t["q"], np.float64), np.asarray(t["dq"], np.float64)
+    ddq_max = (2 / dt ** 2) * (np.asarray(t["qmax"], np.float64) - q - dt * dq)
+    ddq_min = (2 / dt ** 2) * (np.asarray(t["qmin"], np.float64) - q - dt * dq)
     h = np.zeros((B, m))
+    bias_j = bias[:, 6:18]
     h[:, 20:32] = 60.0 - bias_j
     h[:, 32:44] = -(-60.0 - bias_j)
     h[:, 44:56] = ddq_max
     h[:, 56:68] = -ddq_min
     return dict(n=n, m=m, p=p, P=P, c=c, A=A, b=b, G=G, h=h)
+
+
+def controller_qp(seed: int, qp_ids, phase: str = "stance"):
+    """Controller-shape stance QP "C30" (30 vars / 68 ineq / 18 eq), following
+    dogbot_controller/src/client/main.cpp:1471-1647 (SURVEY §8a shape table):
+    controller_qp_from_terms of the synthetic robot state controller_terms (no
+    rigid-body model here: M_com = blkdiag(m I3, I_c), dense SPD M_jj,
+    leg-dominant dense J_j, bias ~ U(-2, 2), q ~ U(-0.5, 0.5), dq ~ U(-0.2, 0.2),
+    joint limits +-1.5 rad, an equality right-hand side consistent with a random
+    feasible state).  Swing phases: controller_swing_qp.  Returns dense row-major
+    [B, r, c] arrays like contact_force_qp."""
+    if phase != "stance":
+        return controller_swing_qp(seed, qp_ids, phase)
+    return controller_qp_from_terms(controller_terms(seed, qp_ids))

@@ -170,6 +170,46 @@ int  qpb_assemble_contact(const qpb_plan *plan, long B, const double *feet, cons
                           int stance, double mu, double *P, double *A, double *G,
                           double *c, double *h, double *b, void *stream);
 
+/* On-device assembly of the controller's own stance QP 30/68/18 (SURVEY §8f row 3,
+ * main.cpp:1471-1647) from the robot terms the controller reads each tick, for B
+ * QPs into the plan's tiled inputs.  Robot terms, QPB_ROBOT_NV doubles per QP, in
+ * this order: Jst[12][18] (JacCOM_lin, foot rows BR BL FL FR x [CoM 6 | joints 12],
+ * row-major), Mcom[6][6] (MassMatrixCOM(0:6,0:6)), Mjj[12][12] (MassMatrixCOM(6:18,
+ * 6:18)), bias[18] (BiasCOM), jdqd[12] (JdqdCOM_lin), wdes[6] (Wcom_des), q[12],
+ * dq[12], qmin[12], qmax[12].  terms_shared = 1: one copy for every QP (one robot,
+ * many candidate targets: then pass the per-candidate wrench in wdes, tiled nv = 6);
+ * 0: tiled, nv = QPB_ROBOT_NV.  wdes NULL: the terms' own.  check (DEVICE, [B] ints,
+ * or NULL): 1 when every entry of the QP outside the plan's pattern is exactly 0,
+ * as the plan assumes (QP_SETUP_dense drops exact zeros), else 0.  The plan must be
+ * 30/68/18 (QPB_ESHAPE otherwise). */
+#define QPB_ROBOT_NV 480
+int  qpb_assemble_controller(const qpb_plan *plan, long B, const double *terms, int terms_shared,
+                             const double *wdes, double mu, double *P, double *A, double *G,
+                             double *c, double *h, double *b, int *check, void *stream);
+
+/* APF-sampled targets (main.cpp:1263-1422) -> the desired CoM wrench each candidate
+ * QP tracks (main.cpp:1484-1571).  State of one tick (host struct, shared by all
+ * candidates); targets: tiled nv = 2, the candidate target point (x, y) of the
+ * attractive field; outputs tiled: wrench nv = 6 (Wcom_des), com_des nv = 6
+ * (CoMPosDes, or NULL).  The TOWR spline between target and tick is out of scope:
+ * CoMPosD = CoMPosDes, CoMVelD = 0. */
+typedef struct qpb_apf_state {
+    double ee[4][2];          /* foot positions (x, y): BR, BL, FL, FR (ee*pos)                */
+    double com[6];            /* CoM pose: x y z roll pitch yaw                                 */
+    double com_vel[6];        /* CoM twist                                                      */
+    double acc_des[6];        /* CoMAccD                                                        */
+    double des_orient[2];     /* des_com_pos[3], des_com_pos[4]                                 */
+    double rob_foot[4];       /* robustness indices rob_foot_br, _bl, _fl, _fr                  */
+    double versor[4][2];      /* repulsive-field directions br, bl, fl, fr (main.cpp:454-457)   */
+    double lat_versor[2];
+    double R_wb[9];           /* _world_H_base rotation, row-major                              */
+    double Mcom[36];          /* MassMatrixCOM(0:6,0:6), row-major                              */
+    double mass;              /* robot_mass                                                     */
+    int rep_field, min_exit, fake_crawl;
+} qpb_apf_state;
+int  qpb_apf_wrench(long K, const qpb_apf_state *st, const double *targets, double *wrench,
+                    double *com_des, void *stream);
+
 /* ---- the multi-GPU argmin gather: RCCL over xGMI ----
  * One process per GPU, each solving its own shard (no data-path collective).
  * A communicator is an ncclComm_t: the caller's own, or one made here from a

@@ -1,0 +1,80 @@
+"""Numpy restatement of the controller's artificial-potential-field step
+(dogbot_controller/src/client/main.cpp:1263-1422, compute_Kpa :2803-2843,
+saturate_* :2756-2800) and of the desired CoM wrench the stance QP tracks
+(:1484-1571) -- the checker of qpb_apf_wrench (test infrastructure).  With the
+TOWR spline out of scope, CoMPosD is the APF target CoMPosDes and CoMVelD = 0."""
+import numpy as np
+
+FOOT_OFF = np.array([[+0.186571, -0.289186], [-0.186571, -0.289186], [-0.186571, +0.289186],
+                     [+0.186571, +0.289186]])      # BR BL FL FR (main.cpp:1171-1174)
+
+
+def _sat(v, lim):
+    return np.where(np.abs(v) > lim, np.copysign(lim, v), v)
+
+
+def _fr(v):
+    return 0.0 if abs(v) < 0.07 else abs(v)
+
+
+def apf_wrench(s: dict, targets: np.ndarray):
+    """s: the fields of qpb_apf_state (numpy); targets [K, 2] -> wrench [K, 6], com_des [K, 6]."""
+    K = targets.shape[0]
+    rf = np.asarray(s["rob_foot"], float)
+    comb = _fr(rf[0] - rf[1]) + _fr(rf[3] - rf[2]) + _fr(abs(rf[0] - rf[3])) + _fr(abs(rf[1] - rf[2]))
+    cx = np.zeros(K)
+    cy = np.zeros(K)
+    for i in range(4):
+        ex = _sat(s["ee"][i][0] - (targets[:, 0] + FOOT_OFF[i, 0]), 2.0)
+        ey = _sat(s["ee"][i][1] - (targets[:, 1] + FOOT_OFF[i, 1]), 2.0)
+        if s["fake_crawl"]:
+            kx_in, ky_in = 0.01, 0.01
+        else:
+            kx_in, ky_in = 0.3, 0.4
+        kx = np.where(np.abs(ex) < 0.4, kx_in, 0.1 if s["min_exit"] else kx_in)
+        ky = np.where(np.abs(ey) < 0.4, ky_in, 0.2 if s["min_exit"] else ky_in)
+        fax, fay = -kx * ex, -ky * ey
+        if s["min_exit"]:
+            frx = 9 * rf[i] * s["versor"][i][0] + 2.2 * comb * s["lat_versor"][0]
+            fry = 9 * rf[i] * s["versor"][i][1] + 2.2 * comb * s["lat_versor"][1]
+        else:
+            frx, fry = 5 * rf[i] * s["versor"][i][0], 5 * rf[i] * s["versor"][i][1]
+        dx, dy = s["ee"][i][0] + 0.5 * fax, s["ee"][i][1] + 0.5 * fay
+        if s["rep_field"]:
+            dx, dy = dx + 0.5 * frx, dy + 0.5 * fry
+        cx, cy = cx + dx, cy + dy
+    cx, cy = cx / 4, cy / 4
+    com = np.asarray(s["com"], float)
+    stx, sty = com[0] - cx, com[1] - cy
+    px = np.where(np.abs(stx) > 0.06, com[0] - np.copysign(0.06, stx), cx)
+    py = np.where(np.abs(sty) > 0.06, com[1] - np.copysign(0.06, sty), cy)
+    pd = np.stack([px, py, np.full(K, 0.38), np.full(K, s["des_orient"][0]), np.full(K, s["des_orient"][1]),
+                   np.zeros(K)], 1)
+    dxv = pd - com[None]
+    R = np.asarray(s["R_wb"], float).reshape(3, 3)
+    dxv[:, 3:6] = dxv[:, 3:6] @ R.T
+    M = np.asarray(s["Mcom"], float).reshape(6, 6)
+    g = np.zeros(6)
+    g[2] = s["mass"] * 9.81
+    W = 3000.0 * dxv + 50.0 * (0.0 - np.asarray(s["com_vel"], float))[None] + g[None] + (M @ np.asarray(s["acc_des"], float))[None]
+    return W, pd
+
+
+def sample_state(seed: int = 7, rep_field=True, min_exit=False, fake_crawl=False):
+    """A plausible tick: nominal stance feet around the CoM with jitter, small CoM
+    motion, robustness indices, the controller's nominal versors (main.cpp:440-458)."""
+    rng = np.random.default_rng(seed)
+    com = np.array([0.1, -0.05, 0.39, 0.01, -0.02, 0.03]) + rng.uniform(-0.01, 0.01, 6)
+    ee = com[None, :2] + FOOT_OFF + rng.uniform(-0.03, 0.03, (4, 2))
+    vec = np.array([[0.186571, -0.289186], [-0.186571, -0.289186], [-0.186571, 0.289186], [0.186571, 0.289186]])
+    versor = vec / np.linalg.norm(vec, axis=1, keepdims=True)
+    Ic = np.diag([0.35, 0.85, 0.95])
+    M = np.zeros((6, 6))
+    M[:3, :3] = 21.261 * np.eye(3)
+    M[3:, 3:] = Ic
+    th = 0.03
+    R = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]])
+    return dict(ee=ee, com=com, com_vel=rng.uniform(-0.1, 0.1, 6), acc_des=rng.uniform(-0.5, 0.5, 6),
+                des_orient=np.array([0.0, 0.0]), rob_foot=rng.uniform(0.0, 0.5, 4), versor=versor,
+                lat_versor=np.array([1.0, 0.0]), R_wb=R, Mcom=M, mass=21.261, rep_field=rep_field,
+                min_exit=min_exit, fake_crawl=fake_crawl)
