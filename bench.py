@@ -466,6 +466,54 @@ def limiter_for(B):
             "source": "profiles/r02_sq_row.json"}
 
 
+def controller_apf_leg(dev, K=8192, steps=20, warmup=3):
+    """The controller's own call, batched: one tick of one robot,
+    K APF-sampled candidate targets (main.cpp:1263-1422).  A step = the candidates'
+    desired wrenches (qpb_apf_wrench) + their 30/68/18 stance QPs assembled from the
+    robot terms (qpb_assemble_controller, shared terms, main.cpp:1471-1647) + one
+    solve with the fused argmin (qpb_solve_best) at the controller's tol 1e-2, with
+    the reference's AMD ordering (QPB_ORDER_AMD: the pivots of qpSWIFT's Permut =
+    NULL, so the answers are the reference's to 1e-6)."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import apf_ref                      # a plausible tick state (synthetic)
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan, apf_state, apf_wrench, to_tiled
+    d = W.controller_qp(0xD06B07 + 30, np.arange(1))
+    plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], order="amd")
+    plan.compile()
+    st = apf_state(**apf_ref.sample_state())
+    rng = np.random.default_rng(11)
+    targets = torch.from_numpy(to_tiled(np.asarray(st.com[:2])[None] + rng.uniform(-0.6, 0.6, (K, 2)))).to(dev)
+    terms = torch.from_numpy(W.pack_terms(W.controller_terms(0xD06B07 + 43, np.arange(1)))[0].copy()).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    wd = apf_wrench(st, targets, K=K, stream=stream)
+    vals = plan.assemble_controller(terms, B=K, shared=True, wdes=wd, stream=stream)
+    out = plan.alloc_outputs(K, device=dev)
+    best = torch.zeros(2, dtype=torch.float64, device=dev)
+    solve = plan.launcher(vals, out, K, reltol=1e-2, abstol=1e-2, stream=stream, best=best)
+
+    def step():
+        apf_wrench(st, targets, K=K, wrench=wd, stream=stream)
+        plan.assemble_controller(terms, B=K, shared=True, wdes=wd, out=vals, stream=stream)
+        solve()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"workload": f"controller call batched: {K} APF-sampled candidates of one tick, wrench + 30/68/18 "
+                        "assembly on the device + solve (AMD order, tol 1e-2) + argmin",
+            "batch": K, "value": K * steps / el, "unit": "QP solves/s", "ms_per_step": el * 1e3 / steps,
+            "kernel": plan.kernel_name(K), "input_bytes_per_candidate": 16,
+            "optimal_frac": float((out["flag"] == 0).float().mean().item()),
+            "mean_iters": float(out["iters"].float().mean().item()), "best": best.cpu().tolist()}
+
+
 def traffic_for(kname, B):
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
@@ -553,6 +601,7 @@ def main():
                       lambda ids: W.controller_qp(plans.SEED + 31, ids, phase="crawl"), 1024, args.tol, dev,
                       cpu=None if args.no_cpu else (512, 16)),
             apf_leg(args.tol, dev),
+            controller_apf_leg(dev),
             trace_leg(args.tol, dev),
         ]
 
