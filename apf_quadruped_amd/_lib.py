@@ -89,6 +89,8 @@ def lib() -> C.CDLL:
     L.qpb_plan_source.argtypes = [vp, C.c_char_p, C.c_long]
     L.qpb_plan_wave_source.restype = C.c_long
     L.qpb_plan_wave_source.argtypes = [vp, C.c_char_p, C.c_long]
+    L.qpb_plan_kernel_name.restype = C.c_long
+    L.qpb_plan_kernel_name.argtypes = [vp, C.c_long, C.c_char_p, C.c_long]
     L.qpb_plan_tree_source.restype = C.c_long
     L.qpb_plan_tree_source.argtypes = [vp, C.c_char_p, C.c_long]
     L.qpb_plan_tree_tables.restype = C.c_long

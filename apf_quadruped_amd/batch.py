@@ -365,12 +365,10 @@ class Plan:
 
     def kernel_name(self, B: int) -> str:
         """Name of the kernel qpb_solve launches for a batch of B."""
-        k = self.kernel_for(B)
-        src = self.wave_source() if k == "wave" else self.tree_source() if k == "tree" else self.source()
-        for line in src.splitlines():
-            if line.startswith("#define QPB_KERNEL_NAME "):
-                return line.split()[-1]
-        return src.split("(qpb_args")[0].split()[-1]
+        L = _lib.lib()
+        buf = C.create_string_buffer(128)
+        check(0 if L.qpb_plan_kernel_name(self._h, int(B), buf, 128) >= 0 else -1, "qpb_plan_kernel_name")
+        return buf.value.decode()
 
 
 class PlanGroup:

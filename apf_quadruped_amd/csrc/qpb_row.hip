@@ -52,6 +52,9 @@ struct qpb_args {
 #ifndef QPB_R_LATEFAC
 #define QPB_R_LATEFAC 1   // factor after the exit test (0: before it, overlapping the reductions)
 #endif
+#ifndef QPB_R_ALIAS
+#define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
+#endif
 #ifndef QPB_R_TIMING
 #define QPB_R_TIMING 0    // 2: per-QP start / end (realtime, cycles), iterations, hardware ids into stats;
                           // 3: cycles per phase (H0 + setup solve, residuals, factor, predictor,
@@ -242,13 +245,20 @@ static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, doub
 #define ZH (NZ > 16)
 // per-row LDS (doubles): staging Pd[NX*NX] Ad[NY1*NX] Gd[NZ*NX] | Tx[NX*NX]
 // (columns of -L, one contiguous run per lane) | PR[NX*NX] (-P rows) | H0s[NX*NX]
+// With QPB_R_ALIAS the loop's three areas overlay the staging area: the staged
+// matrices are read only while the static slices are formed, before PR / H0s are
+// written (program order within the wave: LDS operations of one wave stay in order),
+// and Tx is first written by the first factor.  Per row 3 NX^2 (or the staging
+// area, whichever is larger) instead of both: 7.1 -> 3.6 KB for the 12/20/6 QP.
 #define EVEN(v) (((v) + 1) & ~1)
 #define OFF_A (NX * NX)
 #define OFF_G (OFF_A + NY1 * NX)
-#define OFF_T EVEN(OFF_G + NZ * NX)
+#define STG_END EVEN(OFF_G + NZ * NX)
+#define OFF_T (QPB_R_ALIAS ? 0 : STG_END)
 #define OFF_PR EVEN(OFF_T + NX * NX)
 #define OFF_H0 EVEN(OFF_PR + NX * NX)
-#define LDS_ROW EVEN(OFF_H0 + NX * NX)
+#define LOOP_END EVEN(OFF_H0 + NX * NX)
+#define LDS_ROW (LOOP_END > STG_END ? LOOP_END : STG_END)
 
 // one logical block `lb` of the plan's batch (QPs 4 (lb WPB + wave) ..); qoff
 // offsets the indices the fused argmin reports (the plan's first QP in a group)
@@ -323,10 +333,10 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     const double by = 0.0;
 #endif
 #if QPB_R_ZF128
-    for (int k = 2 * c; k < OFF_T; k += 32)
-        *reinterpret_cast<double2 *>(Ls + k) = double2{0.0, 0.0};   // 16-byte stores (OFF_T, LDS_ROW even)
+    for (int k = 2 * c; k < STG_END; k += 32)
+        *reinterpret_cast<double2 *>(Ls + k) = double2{0.0, 0.0};   // 16-byte stores (STG_END, LDS_ROW even)
 #else
-    for (int k = c; k < OFF_T; k += 16) Ls[k] = 0.0;
+    for (int k = c; k < STG_END; k += 16) Ls[k] = 0.0;
 #endif
     qpb_wsync();
 #pragma unroll
@@ -680,8 +690,11 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     }
 }
 
+#ifndef QPB_R_WPE
+#define QPB_R_WPE 1       // waves per SIMD the register allocation must allow (2: <= 256 VGPRs + AGPRs)
+#endif
 #ifndef QPB_GROUP
-extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
+extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_R_WPE) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * 4 * LDS_ROW];
     qpb_row_body(a, qpb_xcd_block(), 0, qpb_lds);
 }

@@ -553,6 +553,12 @@ int compile_wave(qpb_plan *plan) {
     return compile_kernel(plan->wave_kname, [plan] { return wave_source_of(plan); }, false, &plan->wave_code);
 }
 
+int compile_row2(qpb_plan *plan) {
+    if (plan->row_occ_batch < 0) return fail(QPB_EINVAL, "plan has no two-wave row kernel");
+    return compile_kernel(plan->row2_kname, [plan] { return generate_row_kernel(plan->pl, nullptr, 2); }, false,
+                          &plan->row2_code);
+}
+
 // the tree kernel's plan tables on the current device (uploaded on first use;
 // a regular hipMalloc buffer, so they are cached in L2 like any input)
 int tree_tables_on_device(qpb_plan *plan, const void **out) {
@@ -715,6 +721,12 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
             plan->wave_wg = 64;
             plan->wave_max_batch = -1;   // the row form beats the lane kernel at every batch size
             qpb::generate_row_kernel(plan->pl, &plan->wave_kname);
+            // beyond one wave per SIMD (4 QPs x 1 024 SIMDs) the two-wave allocation:
+            // 2^20 C1 QPs 5.79 -> 3.98 ms; below it the one-wave kernel's latency wins
+            // (1 024 QPs 32.7 vs 34.6 us: the two-wave form spills 11 registers)
+            plan->row_occ_batch = 4096;
+            if (const char *e = getenv("QPB_ROW_OCC_BATCH")) plan->row_occ_batch = atol(e);
+            if (plan->row_occ_batch >= 0) qpb::generate_row_kernel(plan->pl, &plan->row2_kname, 2);
         } else {
             plan->wave_wg = qpb::wave_wg_for(plan->pl);
             qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
@@ -805,12 +817,28 @@ long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap) {
     return (long)s.size();
 }
 
+long qpb_plan_kernel_name(const qpb_plan *plan, long B, char *buf, long cap) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
+                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
+    const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
+    const std::string &s = wave ? (plan->row_occ_batch >= 0 && B > plan->row_occ_batch ? plan->row2_kname : plan->wave_kname)
+                         : tree ? plan->tree_kname : plan->kname;
+    if (buf && cap > 0) {
+        long k = std::min<long>(cap - 1, (long)s.size());
+        std::memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return (long)s.size();
+}
+
 int qpb_plan_compile(qpb_plan *plan) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     const int k = plan->kernel_pref;
     int rc = QPB_OK;
     if (k == 1 || (k == 0 && !plan->large_tree)) rc = qpb::compile_plan(plan);
     if (!rc && plan->wave_ok && (k == 0 || k == 2)) rc = qpb::compile_wave(plan);
+    if (!rc && plan->wave_ok && (k == 0 || k == 2) && plan->row_occ_batch >= 0) rc = qpb::compile_row2(plan);
     if (!rc && plan->tree_ok && (k == 3 || (k == 0 && plan->large_tree))) rc = qpb::compile_tree(plan);
     return rc;
 }
@@ -834,8 +862,11 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
                                         (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
     const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
     hipFunction_t fn;
-    int rc = wave ? qpb::compile_wave(plan) : tree ? qpb::compile_tree(plan) : qpb::compile_plan(plan);
-    if (!rc) rc = wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
+    const bool row2 = wave && plan->row_occ_batch >= 0 && B > plan->row_occ_batch;
+    int rc = row2 ? qpb::compile_row2(plan) : wave ? qpb::compile_wave(plan) : tree ? qpb::compile_tree(plan)
+                                                                          : qpb::compile_plan(plan);
+    if (!rc) rc = row2 ? qpb::load_function(plan->row2_kname, plan->row2_code, &fn)
+                : wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
                 : tree ? qpb::load_function(plan->tree_kname, plan->tree_code, &fn)
                        : qpb::load_function(plan->kname, plan->code, &fn);
     if (rc) return rc;

@@ -21,6 +21,11 @@ struct qpb_plan {
     int kernel_pref = 0;                        // 0 auto, 1 lane only, 2 wave only
     std::string wave_kname;
     std::shared_ptr<std::vector<char>> wave_code;
+    // row form for large batches: the same kernel allocated for two waves per SIMD
+    // (<= 256 registers), used from row_occ_batch QPs on (-1: never)
+    std::string row2_kname;
+    std::shared_ptr<std::vector<char>> row2_code;
+    long row_occ_batch = -1;
     bool tree_ok = false;                       // tree kernel (one QP per workgroup, any pattern)
     bool large_tree = false;                    // auto: tree (not lane) kernel beyond the wave kernel's range
     int tree_wg = 256;
@@ -47,6 +52,7 @@ struct CopySegs {
 int strided_copy(const CopySegs &t, void *stream);
 int compile_plan(qpb_plan *plan);
 int compile_wave(qpb_plan *plan);
+int compile_row2(qpb_plan *plan);
 int compile_tree(qpb_plan *plan);
 std::string wave_source_of(const qpb_plan *plan);   // wave or row form, as the plan chose
 int set_error(int code, const char *msg);

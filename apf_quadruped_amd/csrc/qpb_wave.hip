@@ -51,6 +51,12 @@ struct qpb_args {
 #ifndef QPB_W_REGS         // 1: this lane's slices of P, A, G in registers; 0: read LDS in place
 #define QPB_W_REGS (QPB_NX <= 16 && QPB_NZ <= 32)
 #endif
+#ifndef QPB_W_BLK          // 1: blocked LDL' -- 16-column panels, rank-16 trailing updates on MFMA
+#define QPB_W_BLK 0       // measured slower on 30/68/18 AMD (29.1k vs 22.5k cycles per factor), DESIGN.md
+#endif
+#ifndef QPB_W_H0RE         // 1: the static part of the dense row recomputed per factor (not held live)
+#define QPB_W_H0RE (QPB_ND > 32)
+#endif
 #ifndef QPB_W_LDSB_SYNC     // 1: a wave fence between publishing column k+1 and reading it (diagnostic)
 #define QPB_W_LDSB_SYNC 0
 #endif
@@ -81,8 +87,13 @@ struct qpb_args {
 #define OFF_C (OFF_G + NZ * NX)
 #define OFF_T ((OFF_C + 1) & ~1)
 #define QPB_TMAX(a, b) ((a) > (b) ? (a) : (b))
+// blocked LDL' scratch (QPB_W_BLK): broadcast buffers 2 x 64 | U panel 48 x 16 | C tile
+// column 48 x 16 | the panel's reciprocal pivots 16; panel rows padded to 17 doubles
+// (a row per lane: stride 16 would put every lane on one bank)
+#define BLK_RS 17
+#define BLK_SZ (128 + 2 * 48 * BLK_RS + 16)
 #define TSZ (((QPB_TMAX(QPB_TMAX(ND * (ND - 1) / 2, QPB_W_MFMA ? 256 * ((NX + 15) / 16) * ((NX + 15) / 16) : 0), \
-                        QPB_W_LDSB ? 128 : 0) + 1) & ~1) + 2)
+                        QPB_W_BLK ? BLK_SZ : (QPB_W_LDSB ? 128 : 0)) + 1) & ~1) + 2)
 #define T_SINK (TSZ - 2)
 #define OFF_V (OFF_T + TSZ)
 #define LDS_WAVE (OFF_V + VB_SIZE)
@@ -99,6 +110,14 @@ static __device__ __forceinline__ double qpb_rcp(double v) {
     r = __builtin_fma(r, e, r);
     e = __builtin_fma(-v, r, 1.0);
     return __builtin_fma(r, e, r);
+}
+
+// an opaque copy of v: values derived from it (per-step lane masks, LDS addresses)
+// are formed where they are used instead of being hoisted out of the IPM loop and
+// held live across it (for large dense blocks they would not fit the registers)
+static __device__ __forceinline__ int qpb_opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
 }
 
 // value of lane l (l wave-uniform) in every lane, through an SGPR pair
@@ -402,7 +421,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     //   x_i  : P(i,j) (upper, symmetrised) + 1e7 sum_{leaf y} A(l,i)A(l,j) | A(l,i) | G(r,i)
     //   y_l  : A(l,j) on x columns, 0 elsewhere
     //   z_r  : G(r,j) on x columns, 0 elsewhere (the diagonal -s/z joins at pivot time)
-    double H0[ND];
+    // (large dense blocks: recomputed from the staged matrices at every factor
+    // instead of holding ND more doubles live across the iteration -- QPB_W_H0RE)
+    auto h0_row = [&](double *H0) {
     qpb_for<0, ND>([&](auto ec) {
         constexpr int e = decltype(ec)::value;
         constexpr int ke = qpb_dkind[e], je = qpb_didx[e];
@@ -421,6 +442,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         }
         H0[e] = isd ? v : 0.0;
     });
+    };
+    double H0[QPB_W_H0RE ? 1 : ND];
+    if constexpr (!QPB_W_H0RE) h0_row(H0);
     // G(r,i) G(r,j) for every structural G(r,j) of a leaf z row (x_i rows only)
     double GG[QPB_W_GG ? QPB_NNZG : 1];
     if constexpr (QPB_W_GG) {
@@ -452,8 +476,13 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     // dense block in permutation order (registers and DPP only)
     int fstamp = 0;     // timing build: factor-internal stamps base (0 = off)
     auto factor_ldl = [&]() {
+        const int ln = qpb_opaque(lane);
+        if constexpr (QPB_W_H0RE) {
+            h0_row(H);
+        } else {
 #pragma unroll
-        for (int e = 0; e < ND; e++) H[e] = H0[e];
+            for (int e = 0; e < ND; e++) H[e] = H0[e];
+        }
         if (fstamp) QPB_TS(fstamp + 0);
         if constexpr (QPB_W_GG) {      // small G: every (r, j) unrolled, products precomputed
             int e = 0;
@@ -563,19 +592,94 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         // (free between the G'WG and the transpose); step k reads it as wave-uniform
         // LDS loads, paired by the compiler
         double *Bc = Tx;                         // aliases Tx (no __restrict__: the MFMA tiles and the transpose share it)
-        Bc[lane] = H[0];
+        Bc[ln] = H[0];
 #endif
         double dpiv = qpb_xb<0>(H[0]);
         if constexpr (qpb_dkind[0] == 2) dpiv += kdz[0];
+#if QPB_W_BLK
+        // Blocked right-looking LDL': pivots in permutation order as below, but each
+        // step updates only its 16-column panel; after a panel [k0, k1) the rows and
+        // columns beyond it get the rank-16 update C(d, j) = sum_k -L(d,k) D_k L(j,k)
+        // = sum_k (-1/D_k) U(d,k) U(j,k), U(d,k) = row d's column-k value when step k
+        // reads it, as v_mfma_f64_16x16x4f64 tiles: A operand U(16I + (l & 15), kk)
+        // * (-1/D_kk), B operand U(16J + (l & 15), kk), kk = 4s + (l >> 4).  The tiles
+        // of one column block J go through LDS and each row adds its 16 values.  The
+        // pivots (and which are regularised) are those of the unblocked factor; only
+        // the summation order of the trailing updates changes.
+        double *Up = Tx + 128, *Ct = Tx + 128 + 48 * BLK_RS, *Rv = Tx + 128 + 2 * 48 * BLK_RS;
+        typedef double qpb_v4b __attribute__((ext_vector_type(4)));
+        constexpr int NTB = (ND + 15) / 16;
+#endif
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
+#if QPB_W_BLK
+            constexpr int k0 = k & ~15, k1 = (k0 + 16 < ND) ? k0 + 16 : ND;
+            const double rd = qpb_rcp_reg(dpiv);
+            if constexpr (k + 1 < k1) {
+                const double h = qpb_xb<k + 1>(H[k]), hkk = qpb_xb<k + 1>(H[k + 1]);
+                dpiv = __builtin_fma(h, h * -rd, hkk);
+                if constexpr (qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
+            }
+            rDd = ln == k ? rd : rDd;
+            if constexpr (k1 < ND) {
+                if (ln >= k1) Up[(ln - k1) * BLK_RS + (k - k0)] = H[k];     // U(d, k) of a trailing row
+                if (ln == 0) Rv[k - k0] = -rd;
+            }
+            const double nl = H[k] * -rd;
+            constexpr int cb = (k & 1) * 64, nb = ((k + 1) & 1) * 64;
+            qpb_for<k + 1, k1>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                H[j] = __builtin_fma(Tx[cb + j], nl, H[j]);
+                if constexpr (j == k + 1) Tx[nb + ln] = H[j];       // column k+1 is final
+            });
+            H[k] = ln > k ? nl : 0.0;
+            if constexpr (k == k1 - 1 && k1 < ND) {
+                qpb_wsync();
+                const int li = lane & 15, lk = lane >> 4;
+                double rv[4];
+#pragma unroll
+                for (int s4 = 0; s4 < 4; s4++) rv[s4] = Rv[4 * s4 + lk];
+                qpb_for<k1 / 16, NTB>([&](auto Jc) {
+                    constexpr int J = decltype(Jc)::value;
+                    constexpr int NI = NTB - k1 / 16;
+                    qpb_v4b acc[NI];
+#pragma unroll
+                    for (int i = 0; i < NI; i++) acc[i] = qpb_v4b{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int s4 = 0; s4 < 4; s4++) {
+                        const double bo = Up[(16 * J + li - k1) * BLK_RS + 4 * s4 + lk];
+#pragma unroll
+                        for (int i = 0; i < NI; i++) {
+                            const double ao = Up[(16 * (k1 / 16 + i) + li - k1) * BLK_RS + 4 * s4 + lk] * rv[s4];
+                            acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(ao, bo, acc[i], 0, 0, 0);
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < NI; i++)
+#pragma unroll
+                        for (int t = 0; t < 4; t++) Ct[(16 * i + lk + 4 * t) * BLK_RS + li] = acc[i][t];
+                    qpb_wsync();
+                    if (ln >= k1) {
+                        qpb_for<16 * J, (16 * J + 16 < ND ? 16 * J + 16 : ND)>([&](auto cc) {
+                            constexpr int c = decltype(cc)::value;
+                            H[c] += Ct[(ln - k1) * BLK_RS + (c - 16 * J)];
+                        });
+                    }
+                    qpb_wsync();
+                });
+                // the next panel's first pivot, after its row got the trailing update
+                dpiv = qpb_xb<k1>(H[k1]);
+                if constexpr (qpb_dkind[k1] == 2) dpiv += kdz[k1];
+                Tx[nb + ln] = H[k1];                                  // column k1 for step k1
+            }
+#else
             const double rd = qpb_rcp_reg(dpiv);
             if constexpr (k + 1 < ND) {
                 const double h = qpb_xb<k + 1>(H[k]), hkk = qpb_xb<k + 1>(H[k + 1]);
                 dpiv = __builtin_fma(h, h * -rd, hkk);
                 if constexpr (qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
             }
-            rDd = lane == k ? rd : rDd;
+            rDd = ln == k ? rd : rDd;
             // -L(d,k): kept negated so every update (and the solves) is a plain
             // v_fmac_f64 whose broadcast operand folds into it as DPP row_newbcast
             const double nl = H[k] * -rd;
@@ -584,7 +688,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             qpb_for<k + 1, ND>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 H[j] = __builtin_fma(Bc[cb + j], nl, H[j]);
-                if constexpr (j == k + 1) Bc[nb + lane] = H[j];      // column k+1 is final
+                if constexpr (j == k + 1) Bc[nb + ln] = H[j];      // column k+1 is final
             });
             if constexpr (QPB_W_LDSB_SYNC) qpb_wsync();
 #else
@@ -593,7 +697,8 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 H[j] = qpb_fmac_xb<j>(H[j], H[k], nl);
             });
 #endif
-            H[k] = lane > k ? nl : 0.0;       // -L(d,k) below the diagonal, 0 elsewhere
+            H[k] = ln > k ? nl : 0.0;       // -L(d,k) below the diagonal, 0 elsewhere
+#endif
         });
         if (fstamp) QPB_TS(fstamp + 2);
     };
@@ -604,10 +709,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         {
             // row `lane` of -L: entries e < lane at lane(lane-1)/2 + e (exec-masked
             // stores: a shared sink slot would serialise the masked lanes' writes)
-            const int base = isd ? lane * (lane - 1) / 2 : 0;
+            const int lt = qpb_opaque(lane);
+            const int base = isd ? lt * (lt - 1) / 2 : 0;
 #pragma unroll
             for (int e = 0; e < ND - 1; e++)
-                if (isd && e < lane) Tx[base + e] = H[e];
+                if (isd && e < lt) Tx[base + e] = H[e];
         }
         qpb_wsync();
 #if !QPB_W_LTLDS
@@ -666,10 +772,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         // column `id` of -L straight from the packed transpose area (intact until
         // the next factor): live only through this chain, not across the iteration
         double Ltl[ND];
+        const int ido = qpb_opaque(id);
 #pragma unroll
         for (int k = 0; k < ND; k++) {
-            const double v = Tx[k > id ? k * (k - 1) / 2 + id : T_SINK];
-            Ltl[k] = k > id ? v : 0.0;
+            const double v = Tx[k * (k - 1) / 2 + ido];      // in the area for every k <= ND - 1, id <= ND - 1
+            Ltl[k] = k > ido ? v : 0.0;
         }
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = ND - 1 - decltype(kc)::value;

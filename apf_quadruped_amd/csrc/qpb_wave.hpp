@@ -26,7 +26,9 @@ std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out);
 // Row form (qpb_row.hip, one QP per 16-lane row, four per wavefront): plans
 // with every z / y row a leaf, the x block in natural order, n, p <= 16, m <= 32.
 bool row_eligible(const Plan &pl);
-std::string generate_row_kernel(const Plan &pl, std::string *name_out);
+// wpe: waves per SIMD the register allocation must allow (QPB_R_WPE; 2 for large
+// batches, where two waves per SIMD hide the latency the single wave exposes)
+std::string generate_row_kernel(const Plan &pl, std::string *name_out, int wpe = 1);
 // One kernel for up to QPB_GROUP_MAX row-form plans (qpb_group_*): logical
 // blocks [bend[i-1], bend[i]) run member i.
 constexpr int QPB_GROUP_MAX = 16;

@@ -121,6 +121,9 @@ int  qpb_amd_order(long n, const long *Ap, const long *Ai, long *perm);
 long qpb_plan_source(const qpb_plan *plan, char *buf, long cap);
 long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap);
 long qpb_plan_tree_source(const qpb_plan *plan, char *buf, long cap);
+/* Name of the kernel qpb_solve launches for a batch of B (as the profilers list
+ * it); returns its length, copies at most cap-1 bytes plus a NUL. */
+long qpb_plan_kernel_name(const qpb_plan *plan, long B, char *buf, long cap);
 /* The tree kernel's plan tables (uploaded once per device; exposed for tests):
  * returns their size in bytes, copies at most cap bytes when buf is non-NULL. */
 long qpb_plan_tree_tables(const qpb_plan *plan, void *buf, long cap);

@@ -16,9 +16,11 @@ import torch  # noqa: E402
 from tree_bench import qp  # noqa: E402
 from apf_quadruped_amd.batch import Plan  # noqa: E402
 
-for name in sys.argv[1:] or ["c30"]:
+for spec in sys.argv[1:] or ["c30"]:
+    name, _, order = spec.partition(":")      # "c30:amd" -> the AMD-ordered plan
     d = qp(name, np.arange(1))
-    plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel="wave1")
+    plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel="wave1",
+                           order=order or "own")
     vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
     out = plan.alloc_outputs(1)
     out["stats"] = torch.zeros(384, dtype=torch.float64, device="cuda")
@@ -30,5 +32,5 @@ for name in sys.argv[1:] or ["c30"]:
     stamps = {i: st[i] for i in range(384) if st[i] != 0}
     keys = sorted(stamps)
     deltas = {f"{a}->{b}": stamps[b] - stamps[a] for a, b in zip(keys, keys[1:])}
-    print(json.dumps({"shape": name, "iters": it, "kernel": plan.kernel_name(1),
+    print(json.dumps({"shape": spec, "opts": os.environ["QPB_WAVE_OPTS"], "iters": it, "kernel": plan.kernel_name(1),
                       "total": stamps[keys[-1]] - stamps[keys[0]], "deltas": deltas}), flush=True)

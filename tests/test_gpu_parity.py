@@ -227,6 +227,30 @@ def test_large_batch_properties(kernel, oracle):
 
 
 @pytest.mark.gpu
+def test_row_two_wave_kernel_bit_identical(monkeypatch):
+    """Large batches launch the row kernel allocated for two waves per SIMD
+    (qpb_plan_kernel_name names it); same source and arithmetic as the one-wave
+    kernel, so its results are bit-identical to it."""
+    import torch
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan
+    B = 8192 + 37
+    d = W.contact_force_qp(0xD06B07 + 7, np.arange(B))
+    plans = {}
+    for occ in ("4096", "-1"):
+        monkeypatch.setenv("QPB_ROW_OCC_BATCH", occ)
+        plans[occ] = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0], kernel="wave")
+    assert plans["4096"].kernel_name(B) != plans["-1"].kernel_name(B)
+    assert plans["4096"].kernel_name(1024) == plans["-1"].kernel_name(B)
+    vals = {k: torch.from_numpy(v).cuda() for k, v in plans["-1"].pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
+    r2 = plans["4096"].unpack(plans["4096"].solve(**vals, B=B), B)
+    r1 = plans["-1"].unpack(plans["-1"].solve(**vals, B=B), B)
+    for k in ("x", "y", "z", "s", "fval", "iters", "flag"):
+        np.testing.assert_array_equal(r1[k], r2[k])
+    assert (r1["flag"] == 0).all()
+
+
+@pytest.mark.gpu
 def test_argmin_device_reduction():
     import torch
     from apf_quadruped_amd.batch import argmin
