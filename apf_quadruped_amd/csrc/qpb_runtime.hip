@@ -164,13 +164,14 @@ qpb_plan::~qpb_plan() {
             (void)hipSetDevice(cur);
         }
     }
-    for (auto &kv : tree_dev) {
-        int cur = 0;
-        if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
-            (void)hipFree(kv.second);
-            (void)hipSetDevice(cur);
+    for (auto *m : {&tree_dev, &tree2_dev})
+        for (auto &kv : *m) {
+            int cur = 0;
+            if (hipGetDevice(&cur) == hipSuccess && hipSetDevice(kv.first) == hipSuccess) {
+                (void)hipFree(kv.second);
+                (void)hipSetDevice(cur);
+            }
         }
-    }
 }
 
 namespace qpb {
@@ -561,20 +562,22 @@ int compile_row2(qpb_plan *plan) {
 
 // the tree kernel's plan tables on the current device (uploaded on first use;
 // a regular hipMalloc buffer, so they are cached in L2 like any input)
-int tree_tables_on_device(qpb_plan *plan, const void **out) {
+int tree_tables_on_device(qpb_plan *plan, const void **out, bool second) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return fail(QPB_EHIP, "hipGetDevice failed (no GPU?)");
+    std::map<int, void *> &cache = second ? plan->tree2_dev : plan->tree_dev;
+    const std::vector<char> &tab = second ? plan->tree2_tables : plan->tree_tables;
     std::lock_guard<std::mutex> lk(g_mu);
-    auto it = plan->tree_dev.find(dev);
-    if (it != plan->tree_dev.end()) { *out = it->second; return QPB_OK; }
+    auto it = cache.find(dev);
+    if (it != cache.end()) { *out = it->second; return QPB_OK; }
     void *p = nullptr;
-    const size_t n = std::max<size_t>(plan->tree_tables.size(), 8);
+    const size_t n = std::max<size_t>(tab.size(), 8);
     if (hipMalloc(&p, n) != hipSuccess) return fail(QPB_ENOMEM, "tree tables: hipMalloc failed");
-    if (hipMemcpy(p, plan->tree_tables.data(), plan->tree_tables.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMemcpy(p, tab.data(), tab.size(), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipFree(p);
         return fail(QPB_EHIP, "tree tables: upload failed");
     }
-    plan->tree_dev[dev] = p;
+    cache[dev] = p;
     *out = p;
     return QPB_OK;
 }
@@ -608,6 +611,12 @@ int compile_tree(qpb_plan *plan) {
     if (!plan->tree_ok) return fail(QPB_EINVAL, "plan is not eligible for the tree kernel");
     return compile_kernel(plan->tree_kname, [plan] { return generate_tree_kernel(plan->pl, plan->tree_wg, nullptr); },
                           false, &plan->tree_code);
+}
+
+int compile_tree2(qpb_plan *plan) {
+    if (plan->tree_occ_batch < 0) return fail(QPB_EINVAL, "plan has no large-batch tree kernel");
+    return compile_kernel(plan->tree2_kname, [plan] { return generate_tree_kernel(plan->pl, plan->tree2_wg, nullptr); },
+                          false, &plan->tree2_code);
 }
 
 int load_function(const std::string &kname, const std::shared_ptr<std::vector<char>> &code, hipFunction_t *fn) {
@@ -710,6 +719,17 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     if (plan->tree_ok) {
         plan->tree_wg = qpb::tree_wg_for(plan->pl);
         qpb::generate_tree_kernel(plan->pl, plan->tree_wg, &plan->tree_kname, nullptr, &plan->tree_tables);
+        // 256-thread plans (N > 160): beyond two QPs per CU (512 QPs) the 128-thread
+        // form, whose registers and LDS allow four (MPC 1 024 QPs: 3.04 -> 2.01 ms;
+        // at 512 and below the 256-thread form's shorter step chain wins, 1.58 vs 1.71)
+        if (plan->tree_wg == 256 && !getenv("QPB_TREE_WG")) {
+            plan->tree_occ_batch = 512;
+            if (const char *e = getenv("QPB_TREE_OCC_BATCH")) plan->tree_occ_batch = atol(e);
+            if (plan->tree_occ_batch >= 0) {
+                plan->tree2_wg = 128;
+                qpb::generate_tree_kernel(plan->pl, plan->tree2_wg, &plan->tree2_kname, nullptr, &plan->tree2_tables);
+            }
+        }
     }
     plan->wave_max_batch = 4096;   // measured crossover vs the lane kernel
     if (plan->wave_ok) {
@@ -823,7 +843,8 @@ long qpb_plan_kernel_name(const qpb_plan *plan, long B, char *buf, long cap) {
                                         (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
     const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
     const std::string &s = wave ? (plan->row_occ_batch >= 0 && B > plan->row_occ_batch ? plan->row2_kname : plan->wave_kname)
-                         : tree ? plan->tree_kname : plan->kname;
+                         : tree ? (plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch ? plan->tree2_kname : plan->tree_kname)
+                                : plan->kname;
     if (buf && cap > 0) {
         long k = std::min<long>(cap - 1, (long)s.size());
         std::memcpy(buf, s.data(), k);
@@ -840,6 +861,8 @@ int qpb_plan_compile(qpb_plan *plan) {
     if (!rc && plan->wave_ok && (k == 0 || k == 2)) rc = qpb::compile_wave(plan);
     if (!rc && plan->wave_ok && (k == 0 || k == 2) && plan->row_occ_batch >= 0) rc = qpb::compile_row2(plan);
     if (!rc && plan->tree_ok && (k == 3 || (k == 0 && plan->large_tree))) rc = qpb::compile_tree(plan);
+    if (!rc && plan->tree_ok && (k == 3 || (k == 0 && plan->large_tree)) && plan->tree_occ_batch >= 0)
+        rc = qpb::compile_tree2(plan);
     return rc;
 }
 
@@ -863,10 +886,12 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
     hipFunction_t fn;
     const bool row2 = wave && plan->row_occ_batch >= 0 && B > plan->row_occ_batch;
-    int rc = row2 ? qpb::compile_row2(plan) : wave ? qpb::compile_wave(plan) : tree ? qpb::compile_tree(plan)
-                                                                          : qpb::compile_plan(plan);
+    const bool tree2 = tree && plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch;
+    int rc = row2 ? qpb::compile_row2(plan) : wave ? qpb::compile_wave(plan)
+           : tree2 ? qpb::compile_tree2(plan) : tree ? qpb::compile_tree(plan) : qpb::compile_plan(plan);
     if (!rc) rc = row2 ? qpb::load_function(plan->row2_kname, plan->row2_code, &fn)
                 : wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
+                : tree2 ? qpb::load_function(plan->tree2_kname, plan->tree2_code, &fn)
                 : tree ? qpb::load_function(plan->tree_kname, plan->tree_code, &fn)
                        : qpb::load_function(plan->kname, plan->code, &fn);
     if (rc) return rc;
@@ -882,13 +907,13 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     a.abstol = st->abstol;
     a.sigma_d = st->sigma_d;
     a.maxit = st->maxit;
-    if (tree && (rc = qpb::tree_tables_on_device(plan, &a.tab))) return rc;
+    if (tree && (rc = qpb::tree_tables_on_device(plan, &a.tab, tree2))) return rc;
     // qpb_solve_best on the row kernel: the argmin runs inside the solve launch
     // (its last wave reduces the per-wave partials), saving the separate launch
     // and the gap between two dependent launches; up to 4 096 waves
     bool fused = false;
     void *params[] = {&a};
-    const unsigned wg = (unsigned)(wave ? plan->wave_wg : tree ? plan->tree_wg : plan->gen.wg);
+    const unsigned wg = (unsigned)(wave ? plan->wave_wg : tree2 ? plan->tree2_wg : tree ? plan->tree_wg : plan->gen.wg);
     const long per_block = wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup
     unsigned grid = (unsigned)((B + per_block - 1) / per_block);
     if (wave || tree) grid = (grid + 7) & ~7u;      // XCD-aware block order (qpb_xcd_block)

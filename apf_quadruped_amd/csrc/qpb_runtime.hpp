@@ -33,6 +33,14 @@ struct qpb_plan {
     std::shared_ptr<std::vector<char>> tree_code;
     std::vector<char> tree_tables;              // plan tables of the tree kernel (host copy)
     std::map<int, void *> tree_dev;             // device -> uploaded tables
+    // large batches of N > 160 plans: the 128-thread form (four QPs per CU by LDS
+    // and registers instead of two), used beyond tree_occ_batch QPs (-1: never)
+    int tree2_wg = 0;
+    long tree_occ_batch = -1;
+    std::string tree2_kname;
+    std::shared_ptr<std::vector<char>> tree2_code;
+    std::vector<char> tree2_tables;
+    std::map<int, void *> tree2_dev;
     std::vector<int> ctl_table;                 // controller-QP assembly entries (qpb_assemble_controller)
     std::map<int, void *> ctl_dev;              // device -> uploaded entries
     ~qpb_plan();
@@ -53,6 +61,7 @@ int strided_copy(const CopySegs &t, void *stream);
 int compile_plan(qpb_plan *plan);
 int compile_wave(qpb_plan *plan);
 int compile_row2(qpb_plan *plan);
+int compile_tree2(qpb_plan *plan);
 int compile_tree(qpb_plan *plan);
 std::string wave_source_of(const qpb_plan *plan);   // wave or row form, as the plan chose
 int set_error(int code, const char *msg);

@@ -131,6 +131,7 @@ struct Blob {
     std::ostringstream macros;
     int wg = 64;
     void ints(const char *name, const std::vector<int32_t> &v) {
+        while (i.size() % 4) i.push_back(0);       // 16-byte aligned: the kernel reads step records as int4
         macros << "#define QPB_I_" << name << " " << i.size() << "\n";
         i.insert(i.end(), v.begin(), v.end());
     }
@@ -176,9 +177,11 @@ struct Blob {
 long lds_doubles(const Plan &pl) {
     const long n = pl.n, m = pl.m, p = pl.p, N = pl.N;
     const long npag = pl.Pin.nnz() + (p ? pl.A.nnz() : 0) + pl.G.nnz();
-    // qpb_tree.hip LDS layout: PAG+1, LD+1, rD, V, S, R, W, C, H, B, DS, LAM, DZ, DSL, XP, RED
-    // (+ the program step tables, <= 2 ints per level and program: bounded by 10 N + 16 ints)
-    return (npag + 1) + (pl.lnz + 1) + 4 * N + m + n + m + std::max(p, 1L) + 4 * m + n + 64 + (10 * N + 16) / 2;
+    // qpb_tree.hip LDS layout: LD+1, rD, V, S, R, W, RED (+ the supernode records and
+    // panel lists, <= 3 N + 16 ints); P / A / G, c | b | h and the step tables stay in
+    // global memory, the z-row work vectors in registers
+    (void)npag; (void)n; (void)p;
+    return (pl.lnz + 1) + 4 * N + m + 64 + (3 * N + 16) / 2;
 }
 
 // position of row i in column k of L (Li ascends within a column), -1 if absent

@@ -43,31 +43,22 @@ struct qpb_args {
 #define NPAG (QPB_NNZP + QPB_NNZA + QPB_NNZG)
 #define NW (QPB_WG / 64)
 
-// LDS layout of a QP (doubles)
-#define O_PAG 0                        // P | A | G values, [NPAG] = 0
-#define O_LD (O_PAG + NPAG + 1)        // factor L*D in L's CSC order, [LNZ] = 0
+// LDS layout of a QP (doubles): only what other threads of the workgroup read.
+// P / A / G stay in global memory (the tiled inputs, read where a program or the
+// KKT assembly needs them: the 8 QPs sharing a cache line run on one XCD, so the
+// re-reads hit its L2); c | b | h, pinv and the z-row work vectors (ds, lambda,
+// dz, ds~) live in the registers of the thread that owns the KKT row (row r:
+// thread r % WG); the step tables are read from the plan tables (scalar loads).
+// MPC (N = 380, Lnz 3 000): 66.5 -> 39 KB, four QPs per CU instead of two.
+#define O_LD 0                         // factor L*D in L's CSC order, [LNZ] = 0
 #define O_RD (O_LD + LNZ + 1)          // 1/D (holds the assembled diagonal before the factor)
 #define O_V (O_RD + NN)                // x | y | z
 #define O_S (O_V + NN)                 // s
 #define O_R (O_S + NZ)                 // residual products / rx | ry | rz
 #define O_W (O_R + NN)                 // permuted solve vector
-#define O_C (O_W + NN)
-#define O_H (O_C + NX)
-#define O_B (O_H + NZ)
-#define O_DS (O_B + NY1)
-#define O_LAM (O_DS + NZ)
-#define O_DZ (O_LAM + NZ)
-#define O_DSL (O_DZ + NZ)
-#define O_XP (O_DSL + NZ)              // x at the start of the iteration (objective at maxit)
-#define O_RED (O_XP + NX)              // reduction scratch [NW][8]
+#define O_RED (O_W + NN)               // reduction scratch [NW][8]
 #define LDS_QP (O_RED + 64)
-// step tables of the five programs (ints, in LDS)
-#define QPB_MS_FAC 0
-#define QPB_MS_FWD (QPB_MS_FAC + 4 * QPB_fac_NSTEPS)
-#define QPB_MS_BWD (QPB_MS_FWD + 4 * QPB_fwd_NSTEPS)
-#define QPB_MS_MV (QPB_MS_BWD + 4 * QPB_bwd_NSTEPS)
-#define QPB_MS_OBJ (QPB_MS_MV + 4 * QPB_mv_NSTEPS)
-#define QPB_MS_TOTAL (QPB_MS_OBJ + 4 * QPB_obj_NSTEPS + 4)
+#define RU ((NN + QPB_WG - 1) / QPB_WG)   // KKT rows per thread (row t + u WG)
 
 static __device__ __forceinline__ double qpb_rcp(double v) {
     double r = __builtin_amdgcn_rcp(v);
@@ -431,11 +422,12 @@ static __device__ __forceinline__ long qpb_xcd_block() {
     return (nb & 7) ? (long)b : (long)(b & 7) * (nb >> 3) + (b >> 3);
 }
 
-extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a) {
+#ifndef QPB_T_WPE
+#define QPB_T_WPE 1     // waves per SIMD the register allocation must allow (launch bound)
+#endif
+extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double L[LDS_QP];
-    __shared__ __attribute__((aligned(16))) int MS[QPB_MS_TOTAL];      // program step tables
     __shared__ int SN[QPB_PANEL_INTS > 0 ? QPB_PANEL_INTS : 1];       // supernode records + panel lists
-    __shared__ int PINV[NN];                                           // KKT row -> factor position
     const int t = threadIdx.x;
     const long q = qpb_xcd_block();
     if (q >= a.B) return;                        // workgroup-uniform
@@ -446,48 +438,50 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     const unsigned long long *__restrict__ TD = (const unsigned long long *)a.tab;
     const unsigned *__restrict__ TD32 = (const unsigned *)(TD + QPB_NDESC);
     const int *__restrict__ TI = (const int *)(TD32 + QPB_NDESC32);
-#define qpb_pinv PINV
 #define qpb_asrc_i (TI + QPB_I_asrc_i)
 #define qpb_asrc_l (TI + QPB_I_asrc_l)
-    double *__restrict__ PAG = L + O_PAG;
     double *__restrict__ LD = L + O_LD;
     double *__restrict__ rD = L + O_RD;
     double *__restrict__ V = L + O_V;
     double *__restrict__ S = L + O_S;
     double *__restrict__ R = L + O_R;
     double *__restrict__ W = L + O_W;
-    double *__restrict__ Cv = L + O_C;
-    double *__restrict__ Hv = L + O_H;
-    double *__restrict__ Bv = L + O_B;
-    double *__restrict__ DS = L + O_DS;
-    double *__restrict__ LAM = L + O_LAM;
-    double *__restrict__ DZ = L + O_DZ;
-    double *__restrict__ DSL = L + O_DSL;
-    double *__restrict__ XP = L + O_XP;
     double *__restrict__ RED = L + O_RED;
+    // this QP's P / A / G values in the tiled inputs: entry e of the P | A | G
+    // concatenation (e = NPAG: the zero the dummy terms read)
+    // (branch-free: one load per term, the zero entry masked)
+    const double *__restrict__ gP = a.P + tile * (QPB_NNZP * 64) + ql;
+    const double *__restrict__ gA = (QPB_NNZA > 0 ? a.A + tile * (QPB_NNZA * 64) : a.P + tile * (QPB_NNZP * 64)) + ql;
+    const double *__restrict__ gG = a.G + tile * (QPB_NNZG * 64) + ql;
+    auto pag = [&](int e) -> double {
+        const bool inA = e >= QPB_NNZP, inG = e >= QPB_NNZP + QPB_NNZA, in = e < NPAG;
+        const double *b = inG ? gG : (inA ? gA : gP);
+        const int k = (in ? e : NPAG - 1) - (inG ? QPB_NNZP + QPB_NNZA : (inA ? QPB_NNZP : 0));
+        const double v = b[(long)k * 64];
+        return in ? v : 0.0;
+    };
 
-    // ---- stage the inputs (tiled SoA: value j of QP q at tile*nv*64 + j*64 + q%64)
-    for (int j = t; j < QPB_NNZP; j += QPB_WG) PAG[j] = a.P[tile * (QPB_NNZP * 64) + j * 64 + ql];
-#if QPB_NNZA > 0
-    for (int j = t; j < QPB_NNZA; j += QPB_WG) PAG[QPB_NNZP + j] = a.A[tile * (QPB_NNZA * 64) + j * 64 + ql];
-#endif
-    for (int j = t; j < QPB_NNZG; j += QPB_WG) PAG[QPB_NNZP + QPB_NNZA + j] = a.G[tile * (QPB_NNZG * 64) + j * 64 + ql];
-    for (int j = t; j < NX; j += QPB_WG) Cv[j] = a.c[tile * (NX * 64) + j * 64 + ql];
-    for (int j = t; j < NZ; j += QPB_WG) Hv[j] = a.h[tile * (NZ * 64) + j * 64 + ql];
+    // the rows this thread owns: r = t + u WG
+    double chb[RU], ds[RU], lam[RU], dzr[RU], dsl[RU], xp[RU];
+    int pv[RU];
+#pragma unroll
+    for (int u = 0; u < RU; u++) {
+        const int r = t + u * QPB_WG;
+        double v = 0.0;
+        if (r < NX) v = a.c[tile * (NX * 64) + r * 64 + ql];
 #if NY > 0
-    for (int j = t; j < NY; j += QPB_WG) Bv[j] = a.b[tile * (NY * 64) + j * 64 + ql];
+        else if (r < NX + NY) v = a.b[tile * (NY * 64) + (r - NX) * 64 + ql];
 #endif
-    if (t == 0) { PAG[NPAG] = 0.0; LD[LNZ] = 0.0; }
+        else if (r < NN) v = a.h[tile * (NZ * 64) + (r - NX - NY) * 64 + ql];
+        chb[u] = v;
+        pv[u] = r < NN ? TI[QPB_I_pinv + r] : 0;
+        ds[u] = lam[u] = dzr[u] = dsl[u] = xp[u] = 0.0;
+    }
+    if (t == 0) LD[LNZ] = 0.0;
 #if QPB_T_TIMING == 2
     if (t < 8) qpb_seg[t] = 0.0;
 #endif
     for (int j = t; j < QPB_PANEL_INTS; j += QPB_WG) SN[j] = TI[j];
-    for (int j = t; j < NN; j += QPB_WG) PINV[j] = TI[QPB_I_pinv + j];
-    for (int j = t; j < 4 * QPB_fac_NSTEPS; j += QPB_WG) MS[QPB_MS_FAC + j] = TI[QPB_I_fac_steps + j];
-    for (int j = t; j < 4 * QPB_fwd_NSTEPS; j += QPB_WG) MS[QPB_MS_FWD + j] = TI[QPB_I_fwd_steps + j];
-    for (int j = t; j < 4 * QPB_bwd_NSTEPS; j += QPB_WG) MS[QPB_MS_BWD + j] = TI[QPB_I_bwd_steps + j];
-    for (int j = t; j < 4 * QPB_mv_NSTEPS; j += QPB_WG) MS[QPB_MS_MV + j] = TI[QPB_I_mv_steps + j];
-    for (int j = t; j < 4 * QPB_obj_NSTEPS; j += QPB_WG) MS[QPB_MS_OBJ + j] = TI[QPB_I_obj_steps + j];
     __syncthreads();
 
     // KKT values into the factor layout (init: z diagonal -1; loop: -s/z)
@@ -495,7 +489,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
         for (int e = t; e < LNZ + NN; e += QPB_WG) {
             const int sc = src[e];
             double v;
-            if (sc >= 0) v = PAG[sc];
+            if (sc >= 0) v = pag(sc);
             else if (sc == -1) v = 0.0;
             else if (sc == -2) v = -1.0;
             else { const int r = -3 - sc; v = -S[r] * qpb_rcp(V[NX + NY + r]); }
@@ -505,7 +499,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     };
     auto factor = [&]() {
         QPB_TIC();
-        qpb_run(MS + QPB_MS_FAC, QPB_fac_NSTEPS, TI + QPB_I_fac_hdr, TD + QPB_D_fac,
+        qpb_run(TI + QPB_I_fac_steps, QPB_fac_NSTEPS, TI + QPB_I_fac_hdr, TD + QPB_D_fac,
                 [&](double acc, unsigned long long d) {
                     const unsigned lo = (unsigned)d, hi = (unsigned)(d >> 32);
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(lo)) * QPB_AT(O_RD, qpb_lo16(hi)),
@@ -532,7 +526,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     // W (permuted rhs) -> W (permuted solution)
     auto solve = [&]() {
         QPB_TIC();
-        qpb_run(MS + QPB_MS_FWD, QPB_fwd_NSTEPS, TI + QPB_I_fwd_hdr, TD32 + QPB_D_fwd,
+        qpb_run(TI + QPB_I_fwd_steps, QPB_fwd_NSTEPS, TI + QPB_I_fwd_hdr, TD32 + QPB_D_fwd,
                 [&](double acc, unsigned d) {
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(d)), QPB_AT(O_W, qpb_hi16(d)), acc);
                 },
@@ -551,7 +545,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
                         }
                     }
                 });
-        qpb_run(MS + QPB_MS_BWD, QPB_bwd_NSTEPS, TI + QPB_I_bwd_hdr, TD32 + QPB_D_bwd,
+        qpb_run(TI + QPB_I_bwd_steps, QPB_bwd_NSTEPS, TI + QPB_I_bwd_hdr, TD32 + QPB_D_bwd,
                 [&](double acc, unsigned d) {
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(d)), QPB_AT(O_W, qpb_hi16(d)), acc);
                 },
@@ -572,45 +566,47 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
     // R = [P A' G'; A 0 0; G 0 0] V (raw products)
     auto products = [&](const double *__restrict__ vec) {
         QPB_TIC();
-        qpb_run(MS + QPB_MS_MV, QPB_mv_NSTEPS, TI + QPB_I_mv_hdr, TD32 + QPB_D_mv,
+        qpb_run(TI + QPB_I_mv_steps, QPB_mv_NSTEPS, TI + QPB_I_mv_hdr, TD32 + QPB_D_mv,
                 [&](double acc, unsigned d) {
-                    return __builtin_fma(QPB_AT(O_PAG, qpb_lo16(d)),
+                    return __builtin_fma(pag((int)(qpb_lo16(d) >> 3)),
                                          *(const double *)((const char *)vec + qpb_hi16(d)), acc);
                 },
                 [&](int) { return qpb_pre{0.0, 0.0}; },
                 [&](int r, double acc, qpb_pre) { R[r] = acc; }, [](int, int) {});
         QPB_TOC(tm_mv);
     };
+    // the owner loop: f(u, r) for every KKT row r = t + u WG < NN
+#define QPB_ROWS(...) _Pragma("unroll") for (int u = 0; u < RU; u++) { const int r = t + u * QPB_WG; \
+        if (r < NN) { __VA_ARGS__ } }
 
     // ---- kkt_initialize (Auxilary.c:992-1089): K with the -I block, rhs [-c; b; h]
 #if QPB_T_TIMING
     const long qpb_tall = (long)__builtin_readcyclecounter();
 #endif
     assemble(qpb_asrc_i);
-    for (int r = t; r < NN; r += QPB_WG)
-        W[qpb_pinv[r]] = r < NX ? -Cv[r] : (r < NX + NY ? Bv[r - NX] : Hv[r - NX - NY]);
+    QPB_ROWS(W[pv[u]] = r < NX ? -chb[u] : chb[u];)
     factor();
     solve();
-    for (int r = t; r < NN; r += QPB_WG) V[r] = r < NX + NY ? W[qpb_pinv[r]] : 0.0;
+    QPB_ROWS(V[r] = r < NX + NY ? W[pv[u]] : 0.0;)
     __syncthreads();
     products(V);
     {
         double lo = 1e300, hi = -1e300;
-        for (int r = t; r < NZ; r += QPB_WG) {
-            const double zi = Hv[r] - R[NX + NY + r];
+        QPB_ROWS(if (r >= NX + NY) {
+            const double zi = chb[u] - R[r];
             lo = __builtin_fmin(lo, zi);
             hi = __builtin_fmax(hi, zi);
-        }
+        })
         double mm[2] = {lo, -hi};
         qpb_bmin(mm, RED);
         lo = mm[0];
         hi = -mm[1];
         const double shift = -lo;
-        for (int r = t; r < NZ; r += QPB_WG) {
-            const double zi = Hv[r] - R[NX + NY + r];
-            S[r] = shift < 0 ? zi : zi + (1.0 + shift);
-            V[NX + NY + r] = hi < 0 ? -zi : -zi + (1.0 + hi);
-        }
+        QPB_ROWS(if (r >= NX + NY) {
+            const double zi = chb[u] - R[r];
+            S[r - NX - NY] = shift < 0 ? zi : zi + (1.0 + shift);
+            V[r] = hi < 0 ? -zi : -zi + (1.0 + hi);
+        })
         __syncthreads();
     }
 
@@ -624,18 +620,18 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
         products(V);
         {
             double acc[4] = {0.0, 0.0, 0.0, 0.0};
-            for (int r = t; r < NN; r += QPB_WG) {
+            QPB_ROWS(
                 double v;
-                if (r < NX) { v = -R[r] - Cv[r]; XP[r] = V[r]; acc[0] = __builtin_fma(v, v, acc[0]); }
-                else if (r < NX + NY) { v = Bv[r - NX] - R[r]; acc[1] = __builtin_fma(v, v, acc[1]); }
+                if (r < NX) { v = -R[r] - chb[u]; xp[u] = V[r]; acc[0] = __builtin_fma(v, v, acc[0]); }
+                else if (r < NX + NY) { v = chb[u] - R[r]; acc[1] = __builtin_fma(v, v, acc[1]); }
                 else {
-                    const int i = r - NX - NY;
-                    v = Hv[i] - R[r] - S[i];
+                    const double si = S[r - NX - NY];
+                    v = chb[u] - R[r] - si;
                     acc[2] = __builtin_fma(v, v, acc[2]);
-                    acc[3] = __builtin_fma(S[i], V[r], acc[3]);
+                    acc[3] = __builtin_fma(si, V[r], acc[3]);
                 }
                 R[r] = v;
-            }
+            )
             qpb_bsum(acc, RED);
             n_rx = __builtin_sqrt(acc[0]);
             n_ry = __builtin_sqrt(acc[1]);
@@ -646,54 +642,59 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
         double mu;
         {
             double acc[1] = {0.0};
-            for (int i = t; i < NZ; i += QPB_WG) {
-                const double lm = __builtin_sqrt(S[i] * V[NX + NY + i]);
-                LAM[i] = lm;
+            QPB_ROWS(if (r >= NX + NY) {
+                const double lm = __builtin_sqrt(S[r - NX - NY] * V[r]);
+                lam[u] = lm;
                 acc[0] = __builtin_fma(lm, lm, acc[0]);
-            }
+            })
             qpb_bsum(acc, RED);
             mu = acc[0] * invm;
         }
         // rhs b = [rx; ry; rz - ds/z] (updatekktmatrix_b, Auxilary.c:274-295)
         auto rhs = [&]() {
-            for (int r = t; r < NN; r += QPB_WG) {
+            QPB_ROWS(
                 double v = R[r];
-                if (r >= NX + NY) { const int i = r - NX - NY; v -= DS[i] * qpb_rcp(V[r]); }
-                W[qpb_pinv[r]] = v;
-            }
+                if (r >= NX + NY) v -= ds[u] * qpb_rcp(V[r]);
+                W[pv[u]] = v;
+            )
+        };
+        // kktsolve_2 extraction: dz, ds~ and the step-length minima of this thread's rows
+        auto extract = [&](double (&ab)[2]) {
+            QPB_ROWS(if (r >= NX + NY) {
+                const double si = S[r - NX - NY], zi = V[r], dz = W[pv[u]];
+                const double d = (ds[u] - si * dz) * qpb_rcp(zi);
+                dzr[u] = dz;
+                dsl[u] = d;
+                if (d < 0) ab[0] = __builtin_fmin(ab[0], -(si / d));
+                if (dz < 0) ab[1] = __builtin_fmin(ab[1], -(zi / dz));
+            })
         };
         if (sigma > a.sigma_d) {
             // predictor: ds = -lambda^2 (form_ds, Auxilary.c:319-326); kktsolve_1
-            for (int i = t; i < NZ; i += QPB_WG) DS[i] = -LAM[i] * LAM[i];
-            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RU; u++) ds[u] = -lam[u] * lam[u];
             assemble(qpb_asrc_l);
             rhs();
             factor();
             solve();
             double ab[2] = {1e300, 1e300};
-            for (int i = t; i < NZ; i += QPB_WG) {
-                const double zi = V[NX + NY + i], dz = W[qpb_pinv[NX + NY + i]];
-                const double dsl = (DS[i] - S[i] * dz) * qpb_rcp(zi);
-                DZ[i] = dz;
-                DSL[i] = dsl;
-                if (dsl < 0) ab[0] = __builtin_fmin(ab[0], -(S[i] / dsl));
-                if (dz < 0) ab[1] = __builtin_fmin(ab[1], -(zi / dz));
-            }
+            extract(ab);
             qpb_bmin(ab, RED);
             const double ap = ab[0] < 1e10 ? ab[0] : 1.0, ad = ab[1] < 1e10 ? ab[1] : 1.0;
             double rr[2] = {0.0, 0.0};
-            for (int i = t; i < NZ; i += QPB_WG) {
-                const double zi = V[NX + NY + i];
-                rr[0] = __builtin_fma(__builtin_fma(ap, DSL[i], S[i]), __builtin_fma(ad, DZ[i], zi), rr[0]);
-                rr[1] = __builtin_fma(S[i], zi, rr[1]);
-            }
+            QPB_ROWS(if (r >= NX + NY) {
+                const double si = S[r - NX - NY], zi = V[r];
+                rr[0] = __builtin_fma(__builtin_fma(ap, dsl[u], si), __builtin_fma(ad, dzr[u], zi), rr[0]);
+                rr[1] = __builtin_fma(si, zi, rr[1]);
+            })
             qpb_bsum(rr, RED);
             const double rho = rr[0] / rr[1];
             const double r1 = rho < 1.0 ? rho : 1.0, cube = r1 * r1 * r1;
             sigma = a.sigma_d < cube ? cube : a.sigma_d;
             const double smu = sigma * mu;
-            for (int i = t; i < NZ; i += QPB_WG) DS[i] = -(LAM[i] * LAM[i]) - DSL[i] * DZ[i] + smu;
-            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RU; u++) ds[u] = -(lam[u] * lam[u]) - dsl[u] * dzr[u] + smu;
+            __syncthreads();              // every thread's reads of W (extract) before the new rhs
             rhs();
             __syncthreads();
             solve();
@@ -701,8 +702,8 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
             // pure centering (qpSWIFT.c:572-579): refactor
             sigma = a.sigma_d;
             const double smu = sigma * mu;
-            for (int i = t; i < NZ; i += QPB_WG) DS[i] = -(LAM[i] * LAM[i]) + smu;
-            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RU; u++) ds[u] = -(lam[u] * lam[u]) + smu;
             assemble(qpb_asrc_l);
             rhs();
             factor();
@@ -711,45 +712,44 @@ extern "C" __global__ void __launch_bounds__(QPB_WG) QPB_KERNEL_NAME(qpb_args a)
         // kktsolve_2 extraction, step length, updates (qpSWIFT.c:583-600)
         {
             double ab[2] = {1e300, 1e300};
-            for (int i = t; i < NZ; i += QPB_WG) {
-                const double zi = V[NX + NY + i], dz = W[qpb_pinv[NX + NY + i]];
-                const double dsl = (DS[i] - S[i] * dz) * qpb_rcp(zi);
-                DZ[i] = dz;
-                DSL[i] = dsl;
-                if (dsl < 0) ab[0] = __builtin_fmin(ab[0], -(S[i] / dsl));
-                if (dz < 0) ab[1] = __builtin_fmin(ab[1], -(zi / dz));
-            }
+            extract(ab);
             qpb_bmin(ab, RED);
             alpha_p = ab[0] < 1e10 ? ab[0] : 1.0;
             alpha_d = ab[1] < 1e10 ? ab[1] : 1.0;
             alpha_p = 0.99 * alpha_p > 1.0 ? 1.0 : 0.99 * alpha_p;
             alpha_d = 0.99 * alpha_d > 1.0 ? 1.0 : 0.99 * alpha_d;
-            for (int r = t; r < NN; r += QPB_WG) {
-                if (r < NX) V[r] = __builtin_fma(W[qpb_pinv[r]], alpha_p, V[r]);
-                else if (r < NX + NY) V[r] = __builtin_fma(W[qpb_pinv[r]], alpha_d, V[r]);
+            QPB_ROWS(
+                if (r < NX) V[r] = __builtin_fma(W[pv[u]], alpha_p, V[r]);
+                else if (r < NX + NY) V[r] = __builtin_fma(W[pv[u]], alpha_d, V[r]);
                 else {
-                    const int i = r - NX - NY;
-                    S[i] = __builtin_fma(DSL[i], alpha_p, S[i]);
-                    V[r] = __builtin_fma(DZ[i], alpha_d, V[r]);
+                    S[r - NX - NY] = __builtin_fma(dsl[u], alpha_p, S[r - NX - NY]);
+                    V[r] = __builtin_fma(dzr[u], alpha_d, V[r]);
                 }
-            }
+            )
             __syncthreads();
         }
     }
     if (it == a.maxit) flag = 2;
 
-    // ---- objective of the x the last residuals were computed at (qpSWIFT.c:515)
-    const double *xo = flag == 0 ? V : XP;
-    qpb_run(MS + QPB_MS_OBJ, QPB_obj_NSTEPS, TI + QPB_I_obj_hdr, TD32 + QPB_D_obj,
+    // ---- objective of the x the last residuals were computed at (qpSWIFT.c:515):
+    // V itself after convergence, else the iteration's starting x (owner registers)
+    if (flag != 0) {
+        QPB_ROWS(if (r < NX) R[r] = xp[u];)     // R is free here: the objective's x
+    } else {
+        QPB_ROWS(if (r < NX) R[r] = V[r];)
+    }
+    __syncthreads();
+    qpb_run(TI + QPB_I_obj_steps, QPB_obj_NSTEPS, TI + QPB_I_obj_hdr, TD32 + QPB_D_obj,
             [&](double acc, unsigned d) {
-                return __builtin_fma(QPB_AT(O_PAG, qpb_lo16(d)), *(const double *)((const char *)xo + qpb_hi16(d)),
+                return __builtin_fma(pag((int)(qpb_lo16(d) >> 3)), *(const double *)((const char *)R + qpb_hi16(d)),
                                      acc);
             },
             [&](int) { return qpb_pre{0.0, 0.0}; },
-            [&](int r, double acc, qpb_pre) { R[r] = acc; }, [](int, int) {});
+            [&](int r, double acc, qpb_pre) { W[r] = acc; }, [](int, int) {});
     double fv[1] = {0.0};
-    for (int r = t; r < NX; r += QPB_WG) fv[0] += xo[r] * (0.5 * R[r] + Cv[r]);
+    QPB_ROWS(if (r < NX) fv[0] += R[r] * (0.5 * W[r] + chb[u]);)
     qpb_bsum(fv, RED);
+#undef QPB_ROWS
 
     // ---- outputs
     for (int j = t; j < NX; j += QPB_WG) a.x[tile * (NX * 64) + j * 64 + ql] = V[j];

@@ -52,10 +52,13 @@ struct qpb_args {
 #define QPB_W_REGS (QPB_NX <= 16 && QPB_NZ <= 32)
 #endif
 #ifndef QPB_W_BLK          // 1: blocked LDL' -- 16-column panels, rank-16 trailing updates on MFMA
-#define QPB_W_BLK 0       // measured slower on 30/68/18 AMD (29.1k vs 22.5k cycles per factor), DESIGN.md
+#define QPB_W_BLK 0       // 1 measured slower on 30/68/18 AMD (29.1k vs 22.5k cycles per factor), DESIGN.md
 #endif
 #ifndef QPB_W_H0RE         // 1: the static part of the dense row recomputed per factor (not held live)
 #define QPB_W_H0RE (QPB_ND > 32)
+#endif
+#ifndef QPB_W_ABL          // cost attribution only (wrong results): skip 1 LDL' 2 G'WG 4 solve chains
+#define QPB_W_ABL 0       // 8 residual products 16 transpose (scripts/lat_bench.py, fixed iteration count)
 #endif
 #ifndef QPB_W_LDSB_SYNC     // 1: a wave fence between publishing column k+1 and reading it (diagnostic)
 #define QPB_W_LDSB_SYNC 0
@@ -76,15 +79,21 @@ struct qpb_args {
 #define NV (NX + NZ + NY)
 // vector exchange area: x | z | y  (residual gather); solve: bx | by | bz | v | out
 #define VB_SIZE (((2 * NV + NZ + NX) + 1) & ~1)
-// per-wave LDS (doubles): Pd[NX*NX] Ad[NY*NX] Gd[NZ*NX] | T | Vb.  T holds the
+// per-wave LDS (doubles): Pd[NX*LDP] Ad[NX*LDY] Gd[NX*LDZ] | T | Vb.  T holds the
 // strictly lower triangle of -L, packed by rows (row d at d(d-1)/2), for the
 // transpose; between a transpose and the next factor it is scratch for the MFMA
 // G'WG tiles (NXP^2) and the LDL' broadcast buffers (2 x 64); its last two slots
 // are a read target for masked lanes.  (Packing, instead of ND^2, keeps the
 // 30/68/18 QP at 39.6 KB: four QPs per CU.)
-#define OFF_A (NX * NX)
-#define OFF_G (OFF_A + NY * NX)
-#define OFF_C (OFF_G + NZ * NX)
+// leading dimensions of the staged matrices, odd: a lane-strided access (lane i
+// reading column i) then spreads over all LDS banks instead of a few (stride 68
+// doubles put 30 lanes on 4 bank pairs)
+#define LDP (NX | 1)
+#define LDY (NY1 | 1)
+#define LDZ (NZ | 1)
+#define OFF_A (NX * LDP)
+#define OFF_G (OFF_A + (NY > 0 ? LDY : 0) * NX)
+#define OFF_C (OFF_G + LDZ * NX)
 #define OFF_T ((OFF_C + 1) & ~1)
 #define QPB_TMAX(a, b) ((a) > (b) ? (a) : (b))
 // blocked LDL' scratch (QPB_W_BLK): broadcast buffers 2 x 64 | U panel 48 x 16 | C tile
@@ -388,34 +397,34 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     qpb_wsync();
     const double *Pd = Ls, *Ad = Ls + OFF_A, *Gd = Ls + OFF_G;
     double *Tx = Ls + OFF_T, *Vb = Ls + OFF_V;
-    // Pd[j*NX+i] = P(i,j) as given; Ad[j*NY+l] = A(l,j); Gd[j*NZ+r] = G(r,j)
+    // Pd[j*LDP+i] = P(i,j) as given; Ad[j*LDY+l] = A(l,j); Gd[j*LDZ+r] = G(r,j)
 
     // this lane's slices of the (constant) matrices: registers when small (REGS)
     double Prow[QPB_W_REGS ? NX : 1], Grow[QPB_W_REGS ? ZC * NX : 1], Arow[QPB_W_REGS ? NX : 1];
     if constexpr (QPB_W_REGS) {
 #pragma unroll
         for (int j = 0; j < NX; j++) {
-            Prow[j] = Pd[j * NX + ix];
-            Arow[j] = NY > 0 ? Ad[j * NY + iy] : 0.0;
+            Prow[j] = Pd[j * LDP + ix];
+            Arow[j] = NY > 0 ? Ad[j * LDY + iy] : 0.0;
 #pragma unroll
-            for (int t = 0; t < ZC; t++) Grow[t * NX + j] = Gd[j * NZ + iz[t]];
+            for (int t = 0; t < ZC; t++) Grow[t * NX + j] = Gd[j * LDZ + iz[t]];
         }
     }
-    auto PR = [&](int j) { if constexpr (QPB_W_REGS) return Prow[j]; else return Pd[j * NX + ix]; };   // P(i, j)
-    auto GR = [&](int t, int j) { if constexpr (QPB_W_REGS) return Grow[t * NX + j]; else return Gd[j * NZ + iz[t]]; };  // G(r, j)
-    auto AR = [&](int j) { if constexpr (QPB_W_REGS) return Arow[j]; else return Ad[j * NY + iy]; };   // A(l, j)
+    auto PR = [&](int j) { if constexpr (QPB_W_REGS) return Prow[j]; else return Pd[j * LDP + ix]; };   // P(i, j)
+    auto GR = [&](int t, int j) { if constexpr (QPB_W_REGS) return Grow[t * NX + j]; else return Gd[j * LDZ + iz[t]]; };  // G(r, j)
+    auto AR = [&](int j) { if constexpr (QPB_W_REGS) return Arow[j]; else return Ad[j * LDY + iy]; };   // A(l, j)
     // dense-row slices: G(r, i) / A(l, i) of this lane's dense row when it is x_i, else 0
     const int dxi = dk == 0 ? di : 0;
     const double dxm = dk == 0 ? 1.0 : 0.0;
     double Gcol[QPB_W_REGS ? NZ : 1], Acol[QPB_W_REGS ? NY1 : 1];
     if constexpr (QPB_W_REGS) {
 #pragma unroll
-        for (int r = 0; r < NZ; r++) Gcol[r] = dxm * Gd[dxi * NZ + r];
+        for (int r = 0; r < NZ; r++) Gcol[r] = dxm * Gd[dxi * LDZ + r];
 #pragma unroll
-        for (int l = 0; l < NY1; l++) Acol[l] = NY > 0 ? dxm * Ad[dxi * NY + l] : 0.0;
+        for (int l = 0; l < NY1; l++) Acol[l] = NY > 0 ? dxm * Ad[dxi * LDY + l] : 0.0;
     }
-    auto GC = [&](int r) { if constexpr (QPB_W_REGS) return Gcol[r]; else return dxm * Gd[dxi * NZ + r]; };
-    auto AC = [&](int l) { if constexpr (QPB_W_REGS) return Acol[l]; else return dxm * Ad[dxi * NY + l]; };
+    auto GC = [&](int r) { if constexpr (QPB_W_REGS) return Gcol[r]; else return dxm * Gd[dxi * LDZ + r]; };
+    auto AC = [&](int l) { if constexpr (QPB_W_REGS) return Acol[l]; else return dxm * Ad[dxi * LDY + l]; };
 
     // H0: the static part of this lane's dense row (perm order of the columns):
     //   x_i  : P(i,j) (upper, symmetrised) + 1e7 sum_{leaf y} A(l,i)A(l,j) | A(l,i) | G(r,i)
@@ -429,16 +438,16 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         constexpr int ke = qpb_dkind[e], je = qpb_didx[e];
         double v = 0.0;
         if constexpr (ke == 0) {
-            const double px = dxi <= je ? Pd[je * NX + dxi] : Pd[dxi * NX + je];
+            const double px = dxi <= je ? Pd[je * LDP + dxi] : Pd[dxi * LDP + je];
             double vx = px;
 #pragma unroll
             for (int l = 0; l < NY; l++)
-                if (qpb_yleaf[l]) vx = __builtin_fma(Ad[dxi * NY + l], -RDY * Ad[je * NY + l], vx);
-            v = dk == 0 ? vx : (dk == 1 ? Ad[je * NY + (NY > 0 ? di : 0)] : Gd[je * NZ + di]);
+                if (qpb_yleaf[l]) vx = __builtin_fma(Ad[dxi * LDY + l], -RDY * Ad[je * LDY + l], vx);
+            v = dk == 0 ? vx : (dk == 1 ? Ad[je * LDY + (NY > 0 ? di : 0)] : Gd[je * LDZ + di]);
         } else if constexpr (ke == 1) {
-            v = dk == 0 ? Ad[dxi * NY + je] : 0.0;
+            v = dk == 0 ? Ad[dxi * LDY + je] : 0.0;
         } else {
-            v = dk == 0 ? Gd[dxi * NZ + je] : 0.0;
+            v = dk == 0 ? Gd[dxi * LDZ + je] : 0.0;
         }
         H0[e] = isd ? v : 0.0;
     });
@@ -453,7 +462,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         for (int r = 0; r < NZ; r++)
 #pragma unroll
             for (int j = 0; j < NX; j++)
-                if (qpb_Gnz[r][j]) GG[e++] = GC(r) * Gd[j * NZ + r];
+                if (qpb_Gnz[r][j]) GG[e++] = GC(r) * Gd[j * LDZ + r];
     }
 
     double H[ND], Lt[QPB_W_LTLDS ? 1 : ND], rDd = 0.0, w[ZC];
@@ -496,6 +505,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                         e++;
                     }
             }
+        } else if constexpr (QPB_W_ABL & 2) {
         } else if constexpr (QPB_W_MFMA) {
             // C = G_L' diag(w) G_L over the x columns as a dense GEMM on the matrix
             // cores: 16 x 16 output tiles (I <= J; C is symmetric), K = 4 z rows per
@@ -518,7 +528,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
             for (int I = 0; I < NT; I++) {
                 const int i = 16 * I + li;
-                gi[I] = (i < NX ? i : NX - 1) * NZ;
+                gi[I] = (i < NX ? i : NX - 1) * LDZ;
                 gm[I] = i < NX ? 1.0 : 0.0;
             }
             qpb_for<0, (NZ + 3) / 4>([&](auto sc) {
@@ -567,10 +577,10 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma nounroll
                 for (int u = qpb_goff[g]; u < qpb_goff[g + 1]; u++) {
                     const int r = __builtin_amdgcn_readfirstlane(qpb_grow[u]);
-                    const double t = dxm * Gd[dxi * NZ + r] * Vb[VBW + r];     // G(r, i) w_r
+                    const double t = dxm * Gd[dxi * LDZ + r] * Vb[VBW + r];     // G(r, i) w_r
                     qpb_for<0, qpb_gncol[g]>([&](auto cc) {
                         constexpr int j = qpb_gcol[g][decltype(cc)::value];
-                        H[qpb_xpos[j]] = __builtin_fma(t, Gd[j * NZ + r], H[qpb_xpos[j]]);
+                        H[qpb_xpos[j]] = __builtin_fma(t, Gd[j * LDZ + r], H[qpb_xpos[j]]);
                     });
                 }
             });
@@ -612,6 +622,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #endif
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
+            if constexpr ((QPB_W_ABL & 1) != 0) return;
 #if QPB_W_BLK
             constexpr int k0 = k & ~15, k1 = (k0 + 16 < ND) ? k0 + 16 : ND;
             const double rd = qpb_rcp_reg(dpiv);
@@ -706,6 +717,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     // diagonal); the first wsync also orders every earlier Vb read before the
     // solve's stores
     auto factor_transpose = [&]() {
+        if constexpr ((QPB_W_ABL & 16) != 0) return;
         {
             // row `lane` of -L: entries e < lane at lane(lane-1)/2 + e (exec-masked
             // stores: a shared sink slot would serialise the masked lanes' writes)
@@ -765,6 +777,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         if (sstamp) QPB_TS(sstamp + 2);
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
+            if constexpr ((QPB_W_ABL & 4) != 0) return;
             t = qpb_fmac_xb_dep<k>(t, t, H[k]);
         });
         t *= rDd;
@@ -780,6 +793,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         }
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = ND - 1 - decltype(kc)::value;
+            if constexpr ((QPB_W_ABL & 4) != 0) return;
             t = qpb_fmac_xb_dep<k>(t, t, Ltl[k]);
         });
 #else
@@ -878,11 +892,13 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         if (lane < NY) Vb[NX + NZ + lane] = y;
         qpb_wsync();
         factor_ldl();
+        if (QPB_W_TIMING && it == 1) QPB_TS(364);
         double tp = 0.0;
         ry = by;
         rx = -cx;
 #pragma unroll
         for (int t = 0; t < ZC; t++) rz[t] = hz[t] - s[t];
+        if constexpr (!(QPB_W_ABL & 8)) {
 #pragma unroll
         for (int j = 0; j < NX; j++) {
             const double xj = Vb[j];
@@ -897,16 +913,18 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             for (int k = 0; k < QPB_W_SPLIT; k++) ra[k] = k ? 0.0 : rx;
 #pragma unroll
             for (int r = 0; r < NZ; r++)   // G(r, i): the dense-row slice when dense row i is x_i
-                ra[r % QPB_W_SPLIT] = __builtin_fma(-(QPB_XID ? GC(r) : Gd[ix * NZ + r]), Vb[NX + r], ra[r % QPB_W_SPLIT]);
+                ra[r % QPB_W_SPLIT] = __builtin_fma(-(QPB_XID ? GC(r) : Gd[ix * LDZ + r]), Vb[NX + r], ra[r % QPB_W_SPLIT]);
 #pragma unroll
             for (int l = 0; l < NY; l++)
                 ra[(NZ + l) % QPB_W_SPLIT] =
-                    __builtin_fma(-(QPB_XID ? AC(l) : Ad[ix * NY + l]), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
+                    __builtin_fma(-(QPB_XID ? AC(l) : Ad[ix * LDY + l]), Vb[NX + NZ + l], ra[(NZ + l) % QPB_W_SPLIT]);
             rx = ra[0];
 #pragma unroll
             for (int k = 1; k < QPB_W_SPLIT; k++) rx += ra[k];
         }
+        }
         rx += tp;
+        if (QPB_W_TIMING && it == 1) QPB_TS(365);
         {
             double red[4] = {isx ? rx * rx : 0.0, isy ? ry * ry : 0.0, 0.0, 0.0};
 #pragma unroll
@@ -916,6 +934,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                     red[3] = __builtin_fma(s[t], z[t], red[3]);
                 }
             qpb_rsum_n<ROWS_R>(red);
+            if (QPB_W_TIMING && it == 1) QPB_TS(366);
             sz = red[3];
             if (it >= 0) {
                 fv = isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0;      // summed at exit

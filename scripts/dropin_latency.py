@@ -39,32 +39,43 @@ def main():
     P, A, G = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
     c, h, b = (np.ascontiguousarray(d[k]) for k in ("c", "h", "b"))
 
+    # the argument pointers are formed before the timed region: numpy -> ctypes
+    # conversion costs ~4 us per array on this host, which the C controller does not pay
+    args = [tuple(abi.dptr(X[t]) for X in (P, A, G, c, h, b)) for t in range(a.ticks)]
+
     def run(lib):
-        lat, flags, xs = [], [], []
+        lat, flags, xs, seg = [], [], [], []
         for t in range(a.ticks):
+            Pt, At, Gt, ct, ht, bt = args[t]
             t0 = time.perf_counter()
-            qp = lib.QP_SETUP_dense(n, m, p, abi.dptr(P[t]), abi.dptr(A[t]), abi.dptr(G[t]), abi.dptr(c[t]),
-                                    abi.dptr(h[t]), abi.dptr(b[t]), None, abi.COLUMN_MAJOR_ORDERING)
+            qp = lib.QP_SETUP_dense(n, m, p, Pt, At, Gt, ct, ht, bt, None, abi.COLUMN_MAJOR_ORDERING)
+            t1 = time.perf_counter()
             o = qp.contents.options.contents
             o.reltol = a.tol
             o.abstol = a.tol
+            t2 = time.perf_counter()
             flags.append(int(lib.QP_SOLVE(qp)))
+            t3 = time.perf_counter()
             xs.append(np.ctypeslib.as_array(qp.contents.x, (n,)).copy())
             lib.QP_CLEANUP_dense(qp)
             lat.append(time.perf_counter() - t0)
+            seg.append((t1 - t0, t3 - t2))
+        run.seg = np.median(np.array(seg), axis=0) * 1e6
         return np.array(lat), np.array(flags), np.array(xs)
 
     L = _lib.lib()
     run(L)                                   # first ticks: plan + kernel (cache) + device buffers
     lat, flags, xs = run(L)
     out = dict(shape=a.shape, mode=a.mode, tol=a.tol, ticks=a.ticks, optimal=float((flags == 0).mean()),
-               gpu_us_median=float(np.median(lat) * 1e6), gpu_us_p99=float(np.percentile(lat, 99) * 1e6))
+               gpu_us_median=float(np.median(lat) * 1e6), gpu_us_p99=float(np.percentile(lat, 99) * 1e6),
+               gpu_setup_us=float(run.seg[0]), gpu_solve_us=float(run.seg[1]))
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libqpswift_ref.so")
     if os.path.exists(ref_so):
         R = abi.bind_qpswift(C.CDLL(ref_so))
         run(R)
         rl, rf, rx = run(R)
         out.update(cpu_ref_us_median=float(np.median(rl) * 1e6), cpu_ref_us_p99=float(np.percentile(rl, 99) * 1e6),
+                   cpu_ref_setup_us=float(run.seg[0]), cpu_ref_solve_us=float(run.seg[1]),
                    max_abs_x_diff=float(np.abs(rx - xs).max()),
                    max_rel_x_diff=float((np.abs(rx - xs).max(1) / np.maximum(1, np.abs(rx).max(1))).max()))
     print(json.dumps(out))

@@ -136,3 +136,28 @@ def test_tree_kernel_sigma_d(oracle):
         np.testing.assert_array_equal(r["flag"], g["flag"])
         for k in ("x", "z", "s") + (("y",) if p else ()):
             _close(r[k], g[k], f"{name}.{k}", TOL)
+
+
+@pytest.mark.gpu
+def test_tree_large_batch_form_matches_oracle(oracle):
+    """Beyond 512 QPs an N > 160 plan launches its 128-thread tree kernel (four QPs
+    per CU): same algorithm, its own level packing -- checked against the oracle in
+    the plan's order, and its kernel name is the one qpb_plan_kernel_name reports."""
+    import torch
+    from apf_quadruped_amd import plans
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan
+    B = 600
+    d = plans.standard_qp("mpc_h10", np.arange(B))
+    plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel="tree")
+    assert plan.kernel_name(B) != plan.kernel_name(512) and "_w128_" in plan.kernel_name(B)
+    vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
+    r = plan.unpack(plan.solve(**vals, B=B), B)
+    assert (r["flag"] == 0).all()
+    Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    n, m, p = d["n"], d["m"], d["p"]
+    for q in (0, 257, B - 1):
+        o = oracle.solve_dense(n, m, p, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm)
+        assert o["flag"] == r["flag"][q] and o["iters"] == r["iters"][q]
+        for k in ("x", "z", "s"):
+            _close(r[k][q], o[k], f"q{q}.{k}", 1e-9)
