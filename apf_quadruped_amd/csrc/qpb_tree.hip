@@ -60,6 +60,16 @@ struct qpb_args {
 #define LDS_QP (O_RED + 64)
 #define RU ((NN + QPB_WG - 1) / QPB_WG)   // KKT rows per thread (row t + u WG)
 
+// compile-time loop (the owner-row registers are only ever indexed by constants:
+// a runtime index would put them in scratch memory)
+template <int V> struct qpb_tic { static constexpr int value = V; };
+template <int J0, int J1, class F> static __device__ __forceinline__ void qpb_tfor(F &&f) {
+    if constexpr (J0 < J1) {
+        f(qpb_tic<J0>{});
+        qpb_tfor<J0 + 1, J1>(f);
+    }
+}
+
 static __device__ __forceinline__ double qpb_rcp(double v) {
     double r = __builtin_amdgcn_rcp(v);
     double e = __builtin_fma(-v, r, 1.0);
@@ -449,23 +459,26 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     double *__restrict__ RED = L + O_RED;
     // this QP's P / A / G values in the tiled inputs: entry e of the P | A | G
     // concatenation (e = NPAG: the zero the dummy terms read)
-    // (branch-free: one load per term, the zero entry masked)
-    const double *__restrict__ gP = a.P + tile * (QPB_NNZP * 64) + ql;
-    const double *__restrict__ gA = (QPB_NNZA > 0 ? a.A + tile * (QPB_NNZA * 64) : a.P + tile * (QPB_NNZP * 64)) + ql;
-    const double *__restrict__ gG = a.G + tile * (QPB_NNZG * 64) + ql;
+    // (branch-free: one global load per term, the zero entry masked; the address is
+    // integer arithmetic -- a choice between pointers becomes a scratch table)
+    typedef const double __attribute__((address_space(1))) qpb_gdouble;
+    typedef unsigned long long qpb_u64;
+    const qpb_u64 bP = (qpb_u64)(a.P + tile * (QPB_NNZP * 64) + ql);
+    const qpb_u64 bA = QPB_NNZA > 0 ? (qpb_u64)(a.A + tile * (QPB_NNZA * 64) + ql) : bP;
+    const qpb_u64 bG = (qpb_u64)(a.G + tile * (QPB_NNZG * 64) + ql);
+    const qpb_u64 dA = bA - bP - (qpb_u64)QPB_NNZP * 512, dG = bG - bA - (qpb_u64)QPB_NNZA * 512;
     auto pag = [&](int e) -> double {
         const bool inA = e >= QPB_NNZP, inG = e >= QPB_NNZP + QPB_NNZA, in = e < NPAG;
-        const double *b = inG ? gG : (inA ? gA : gP);
-        const int k = (in ? e : NPAG - 1) - (inG ? QPB_NNZP + QPB_NNZA : (inA ? QPB_NNZP : 0));
-        const double v = b[(long)k * 64];
+        const qpb_u64 ad = bP + (qpb_u64)(in ? e : NPAG - 1) * 512 + (inA ? dA : 0ull) + (inG ? dG : 0ull);
+        const double v = *(qpb_gdouble *)ad;
         return in ? v : 0.0;
     };
 
     // the rows this thread owns: r = t + u WG
     double chb[RU], ds[RU], lam[RU], dzr[RU], dsl[RU], xp[RU];
     int pv[RU];
-#pragma unroll
-    for (int u = 0; u < RU; u++) {
+    qpb_tfor<0, RU>([&](auto uc_) {
+        constexpr int u = decltype(uc_)::value;
         const int r = t + u * QPB_WG;
         double v = 0.0;
         if (r < NX) v = a.c[tile * (NX * 64) + r * 64 + ql];
@@ -476,7 +489,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         chb[u] = v;
         pv[u] = r < NN ? TI[QPB_I_pinv + r] : 0;
         ds[u] = lam[u] = dzr[u] = dsl[u] = xp[u] = 0.0;
-    }
+    });
     if (t == 0) LD[LNZ] = 0.0;
 #if QPB_T_TIMING == 2
     if (t < 8) qpb_seg[t] = 0.0;
@@ -505,7 +518,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(lo)) * QPB_AT(O_RD, qpb_lo16(hi)),
                                          QPB_AT(O_LD, qpb_hi16(lo)), acc);
                 },
-                [&](int out) { return qpb_pre{out >= 0 ? LD[out] : rD[out >= -NN ? -1 - out : -1 - NN - out], 0.0}; },
+                // one LDS index, not a choice of pointers (which the compiler turns into a
+                // scratch table of generic pointers and a flat load)
+                [&](int out) { return qpb_pre{L[out >= 0 ? O_LD + out : O_RD + (out >= -NN ? -1 - out : -1 - NN - out)], 0.0}; },
                 [&](int out, double acc, qpb_pre e) {
                     if (out >= 0) LD[out] = e.a + acc;
                     else if (out >= -NN) rD[-1 - out] = qpb_rcp_reg(e.a + acc);
@@ -576,8 +591,8 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         QPB_TOC(tm_mv);
     };
     // the owner loop: f(u, r) for every KKT row r = t + u WG < NN
-#define QPB_ROWS(...) _Pragma("unroll") for (int u = 0; u < RU; u++) { const int r = t + u * QPB_WG; \
-        if (r < NN) { __VA_ARGS__ } }
+#define QPB_ROWS(...) qpb_tfor<0, RU>([&](auto uc_) { constexpr int u = decltype(uc_)::value; \
+        const int r = t + u * QPB_WG; if (r < NN) { __VA_ARGS__ } });
 
     // ---- kkt_initialize (Auxilary.c:992-1089): K with the -I block, rhs [-c; b; h]
 #if QPB_T_TIMING
@@ -671,8 +686,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         };
         if (sigma > a.sigma_d) {
             // predictor: ds = -lambda^2 (form_ds, Auxilary.c:319-326); kktsolve_1
-#pragma unroll
-            for (int u = 0; u < RU; u++) ds[u] = -lam[u] * lam[u];
+            qpb_tfor<0, RU>([&](auto uc_) { constexpr int u = decltype(uc_)::value; ds[u] = -lam[u] * lam[u]; });
             assemble(qpb_asrc_l);
             rhs();
             factor();
@@ -692,8 +706,10 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
             const double r1 = rho < 1.0 ? rho : 1.0, cube = r1 * r1 * r1;
             sigma = a.sigma_d < cube ? cube : a.sigma_d;
             const double smu = sigma * mu;
-#pragma unroll
-            for (int u = 0; u < RU; u++) ds[u] = -(lam[u] * lam[u]) - dsl[u] * dzr[u] + smu;
+            qpb_tfor<0, RU>([&](auto uc_) {
+                constexpr int u = decltype(uc_)::value;
+                ds[u] = -(lam[u] * lam[u]) - dsl[u] * dzr[u] + smu;
+            });
             __syncthreads();              // every thread's reads of W (extract) before the new rhs
             rhs();
             __syncthreads();
@@ -702,8 +718,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
             // pure centering (qpSWIFT.c:572-579): refactor
             sigma = a.sigma_d;
             const double smu = sigma * mu;
-#pragma unroll
-            for (int u = 0; u < RU; u++) ds[u] = -(lam[u] * lam[u]) + smu;
+            qpb_tfor<0, RU>([&](auto uc_) { constexpr int u = decltype(uc_)::value; ds[u] = -(lam[u] * lam[u]) + smu; });
             assemble(qpb_asrc_l);
             rhs();
             factor();

@@ -460,7 +460,7 @@ def limiter_for(B):
     if not r:
         return None
     fr = r["frac_of_wave_cycles"]
-    return {"kind": "VALU issue + LDS/memory latency at one wave per SIMD (neither HBM nor FP64 peak)",
+    return {"kind": r.get("kind", "VALU issue + LDS/memory latency (neither HBM nor FP64 peak)"),
             "valu_active_frac": fr["valu_active"], "waitcnt_frac": fr["wait_any (s_waitcnt: LDS / memory)"],
             "waves_per_simd": r["waves_per_simd_avg"], "fp64_lane_fma_per_qp": r["per_qp"]["fma_f64_lane_ops"],
             "source": "profiles/r02_sq_row.json"}

@@ -47,7 +47,13 @@ def main():
         waves = c["SQ_WAVES"]
         fma_lane = c["SQ_INSTS_VALU_FMA_F64"] * 64 / B
         flops_issued = (2 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"]) * 64
+        wps = wc / (SIMDS * cyc)
+        simd_valu = c["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cyc)       # VALU-issue cycles per SIMD cycle
+        kind = (f"VALU issue at {wps:.1f} waves per SIMD (SIMD VALU busy {simd_valu:.0%}; neither HBM nor FP64 peak)"
+                if wps > 1.5 else
+                f"latency: one wave on {wps:.0%} of the SIMDs, VALU issue + LDS/memory waits (neither HBM nor FP64 peak)")
         res[f"B={B}"] = {
+            "kind": kind, "simd_valu_busy": simd_valu,
             "kernel_s": t, "clock_ghz": clock / 1e9, "waves": waves,
             "waves_per_simd_avg": wc / (SIMDS * cyc),
             "wave_lifetime_cycles": wc / waves,
@@ -62,10 +68,12 @@ def main():
             "fp64_issue_frac_of_peak": flops_issued / (FP64_PEAK_FLOP_PER_CYC_SIMD * SIMDS * cyc),
             "counters": c,
         }
-    res["reading"] = ("one wave per SIMD (265 VGPRs: 256 + 9 AGPRs), each wave issues VALU in ~55 % of its "
-                      "cycles and waits on LDS / memory in ~33 %: issue- and latency-bound, not HBM- (4-5 % of "
-                      "8 TB/s) or FP64-bound; FP64 lane-FMAs per QP are ~3.8x the algorithmic count (16 lanes "
-                      "per QP, sparse G rows and the dense-row LDL' update every lane)")
+    res["reading"] = ("1 024 QPs: 256 waves, one on a quarter of the SIMDs -- the per-wave dependency chain "
+                      "(VALU issue ~50 %, LDS / memory waits ~40 % of its cycles) is the bound.  2^20 QPs: the "
+                      "two-wave form (<= 256 registers, 3.6 KB LDS per QP) keeps ~1.9 waves per SIMD and the "
+                      "SIMD's VALU busy most cycles: issue-bound, not HBM- (6-7 % of 8 TB/s) or FP64-bound; FP64 "
+                      "lane-FMAs per QP are ~3.8x the algorithmic count (16 lanes per QP, sparse G rows and the "
+                      "dense-row LDL' update every lane)")
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
         if isinstance(v, dict):
