@@ -236,10 +236,12 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
     std::vector<Snode> sns;
     std::vector<long> sn_of(N, -1);
     const bool panels = !getenv("QPB_TREE_NOPANEL");
-    // widest panel: 24 columns (48 VGPRs per lane for its register row); wider
-    // supernodes split into 24-column panels.  Measured on 30/68/18 (one 36-wide
-    // supernode): 24 -> 1.38 ms per 1 024 QPs, 48 -> 2.21 ms (VGPRs 209 vs 264)
-    long maxw = 24;
+    // widest panel: 12 columns; wider supernodes split into 12-column panels.
+    // Measured on 30/68/18 (one 36-wide supernode): 24 -> 1.38 ms per 1 024 QPs, 48 ->
+    // 2.21 ms (VGPRs 209 vs 264); on MPC 12 (with QPB_T_XR 8) keeps the kernel at 72 KB
+    // of code and 223 registers (24: 139 KB, 256 + AGPRs -> one wave per SIMD):
+    // 1 024 QPs 1.77 ms (24 wide: 3.06 ms)
+    long maxw = 12;
     if (const char *e = getenv("QPB_TREE_MAXW")) maxw = std::max(2L, std::min(48L, atol(e)));
     for (long j = 0; j < N;) {
         long e = j;

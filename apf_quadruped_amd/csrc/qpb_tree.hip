@@ -149,7 +149,8 @@ __shared__ double qpb_seg[8];
 #define QPB_T_DEPTH 2   // register sets of prefetched steps (2 or 4): a step's tables are loaded DEPTH steps ahead
 #endif
 #ifndef QPB_T_XR
-#define QPB_T_XR 24     // extra rounds a step loads at its start (beyond the prefetched ones)
+#define QPB_T_XR 8      // extra rounds a step loads at its start (beyond the prefetched ones;
+                        // 24 -> 8: -16 KB of code, same speed)
 #endif
 #ifndef QPB_T_PF
 #define QPB_T_PF 8      // descriptor rounds prefetched per step
@@ -433,7 +434,9 @@ static __device__ __forceinline__ long qpb_xcd_block() {
 }
 
 #ifndef QPB_T_WPE
-#define QPB_T_WPE 1     // waves per SIMD the register allocation must allow (launch bound)
+#define QPB_T_WPE 2     // waves per SIMD the register allocation must allow (launch bound): two
+                        // 256-thread or four 128-thread workgroups per CU need <= 256 registers
+                        // (VGPRs + AGPRs); above that one wave per SIMD halves the QPs per CU
 #endif
 extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double L[LDS_QP];
@@ -594,106 +597,132 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
 #define QPB_ROWS(...) qpb_tfor<0, RU>([&](auto uc_) { constexpr int u = decltype(uc_)::value; \
         const int r = t + u * QPB_WG; if (r < NN) { __VA_ARGS__ } });
 
-    // ---- kkt_initialize (Auxilary.c:992-1089): K with the -I block, rhs [-c; b; h]
+    // ---- kkt_initialize (Auxilary.c:992-1089) and the QP_SOLVE loop (qpSWIFT.c:502-602)
+    // as one state machine, so that assemble / factor / solve / products each have a
+    // single call site: inlined at every use they made a 378 KB kernel, several times
+    // the instruction cache
 #if QPB_T_TIMING
     const long qpb_tall = (long)__builtin_readcyclecounter();
 #endif
-    assemble(qpb_asrc_i);
-    QPB_ROWS(W[pv[u]] = r < NX ? -chb[u] : chb[u];)
-    factor();
-    solve();
-    QPB_ROWS(V[r] = r < NX + NY ? W[pv[u]] : 0.0;)
-    __syncthreads();
-    products(V);
-    {
-        double lo = 1e300, hi = -1e300;
-        QPB_ROWS(if (r >= NX + NY) {
-            const double zi = chb[u] - R[r];
-            lo = __builtin_fmin(lo, zi);
-            hi = __builtin_fmax(hi, zi);
-        })
-        double mm[2] = {lo, -hi};
-        qpb_bmin(mm, RED);
-        lo = mm[0];
-        hi = -mm[1];
-        const double shift = -lo;
-        QPB_ROWS(if (r >= NX + NY) {
-            const double zi = chb[u] - R[r];
-            S[r - NX - NY] = shift < 0 ? zi : zi + (1.0 + shift);
-            V[r] = hi < 0 ? -zi : -zi + (1.0 + hi);
-        })
-        __syncthreads();
-    }
-
-    // ---- QP_SOLVE (qpSWIFT.c:502-602)
     double sigma = 100.0, alpha_p = 0.0, alpha_d = 0.0;
-    double n_rx = 0.0, n_ry = 0.0, n_rz = 0.0, n_mu = 0.0;
+    double n_rx = 0.0, n_ry = 0.0, n_rz = 0.0, n_mu = 0.0, mu = 0.0;
     long it = 0;
     int flag = 2;
     const double invm = 1.0 / (double)NZ;
-    for (; it < a.maxit; it++) {
-        products(V);
-        {
-            double acc[4] = {0.0, 0.0, 0.0, 0.0};
-            QPB_ROWS(
-                double v;
-                if (r < NX) { v = -R[r] - chb[u]; xp[u] = V[r]; acc[0] = __builtin_fma(v, v, acc[0]); }
-                else if (r < NX + NY) { v = chb[u] - R[r]; acc[1] = __builtin_fma(v, v, acc[1]); }
-                else {
-                    const double si = S[r - NX - NY];
-                    v = chb[u] - R[r] - si;
-                    acc[2] = __builtin_fma(v, v, acc[2]);
-                    acc[3] = __builtin_fma(si, V[r], acc[3]);
-                }
-                R[r] = v;
-            )
-            qpb_bsum(acc, RED);
-            n_rx = __builtin_sqrt(acc[0]);
-            n_ry = __builtin_sqrt(acc[1]);
-            n_rz = __builtin_sqrt(acc[2]);
-            n_mu = acc[3] * invm;
+    // rhs b = [rx; ry; rz - ds/z] (updatekktmatrix_b, Auxilary.c:274-295)
+    auto rhs = [&]() {
+        QPB_ROWS(
+            double v = R[r];
+            if (r >= NX + NY) v -= ds[u] * qpb_rcp(V[r]);
+            W[pv[u]] = v;
+        )
+    };
+    // kktsolve_2 extraction: dz, ds~ and the step-length minima of this thread's rows
+    auto extract = [&](double (&ab)[2]) {
+        QPB_ROWS(if (r >= NX + NY) {
+            const double si = S[r - NX - NY], zi = V[r], dz = W[pv[u]];
+            const double d = (ds[u] - si * dz) * qpb_rcp(zi);
+            dzr[u] = dz;
+            dsl[u] = d;
+            if (d < 0) ab[0] = __builtin_fmin(ab[0], -(si / d));
+            if (dz < 0) ab[1] = __builtin_fmin(ab[1], -(zi / dz));
+        })
+    };
+    // stages: INIT the setup solve (rhs [-c; b; h], z block -I), INITZ the initial
+    // s / z, TOP an iteration's residuals and exit test, PRED the predictor
+    // (kktsolve_1), CORR the corrector on the same factor, CENT pure centering
+    // (sigma <= sigma_d: refactor, qpSWIFT.c:572-579)
+    enum { ST_INIT, ST_INITZ, ST_TOP, ST_PRED, ST_CORR, ST_CENT };
+    int stage = ST_INIT;
+    for (;;) {
+        if (stage == ST_INITZ || stage == ST_TOP) {
+            if (stage == ST_TOP && it >= a.maxit) break;
+            products(V);
+            if (stage == ST_INITZ) {
+                double lo = 1e300, hi = -1e300;
+                QPB_ROWS(if (r >= NX + NY) {
+                    const double zi = chb[u] - R[r];
+                    lo = __builtin_fmin(lo, zi);
+                    hi = __builtin_fmax(hi, zi);
+                })
+                double mm[2] = {lo, -hi};
+                qpb_bmin(mm, RED);
+                lo = mm[0];
+                hi = -mm[1];
+                const double shift = -lo;
+                QPB_ROWS(if (r >= NX + NY) {
+                    const double zi = chb[u] - R[r];
+                    S[r - NX - NY] = shift < 0 ? zi : zi + (1.0 + shift);
+                    V[r] = hi < 0 ? -zi : -zi + (1.0 + hi);
+                })
+                __syncthreads();
+                stage = ST_TOP;
+                continue;
+            }
+            {
+                double acc[4] = {0.0, 0.0, 0.0, 0.0};
+                QPB_ROWS(
+                    double v;
+                    if (r < NX) { v = -R[r] - chb[u]; xp[u] = V[r]; acc[0] = __builtin_fma(v, v, acc[0]); }
+                    else if (r < NX + NY) { v = chb[u] - R[r]; acc[1] = __builtin_fma(v, v, acc[1]); }
+                    else {
+                        const double si = S[r - NX - NY];
+                        v = chb[u] - R[r] - si;
+                        acc[2] = __builtin_fma(v, v, acc[2]);
+                        acc[3] = __builtin_fma(si, V[r], acc[3]);
+                    }
+                    R[r] = v;
+                )
+                qpb_bsum(acc, RED);
+                n_rx = __builtin_sqrt(acc[0]);
+                n_ry = __builtin_sqrt(acc[1]);
+                n_rz = __builtin_sqrt(acc[2]);
+                n_mu = acc[3] * invm;
+            }
+            if (n_rx < a.tol && n_rz < a.tol && (NY == 0 || n_ry < a.tol) && n_mu < a.abstol) { flag = 0; break; }
+            {
+                double acc[1] = {0.0};
+                QPB_ROWS(if (r >= NX + NY) {
+                    const double lm = __builtin_sqrt(S[r - NX - NY] * V[r]);
+                    lam[u] = lm;
+                    acc[0] = __builtin_fma(lm, lm, acc[0]);
+                })
+                qpb_bsum(acc, RED);
+                mu = acc[0] * invm;
+            }
+            if (sigma > a.sigma_d) {
+                // predictor: ds = -lambda^2 (form_ds, Auxilary.c:319-326)
+                qpb_tfor<0, RU>([&](auto uc_) { constexpr int u = decltype(uc_)::value; ds[u] = -lam[u] * lam[u]; });
+                stage = ST_PRED;
+            } else {
+                sigma = a.sigma_d;
+                const double smu = sigma * mu;
+                qpb_tfor<0, RU>([&](auto uc_) { constexpr int u = decltype(uc_)::value; ds[u] = -(lam[u] * lam[u]) + smu; });
+                stage = ST_CENT;
+            }
         }
-        if (n_rx < a.tol && n_rz < a.tol && (NY == 0 || n_ry < a.tol) && n_mu < a.abstol) { flag = 0; break; }
-        double mu;
-        {
-            double acc[1] = {0.0};
-            QPB_ROWS(if (r >= NX + NY) {
-                const double lm = __builtin_sqrt(S[r - NX - NY] * V[r]);
-                lam[u] = lm;
-                acc[0] = __builtin_fma(lm, lm, acc[0]);
-            })
-            qpb_bsum(acc, RED);
-            mu = acc[0] * invm;
-        }
-        // rhs b = [rx; ry; rz - ds/z] (updatekktmatrix_b, Auxilary.c:274-295)
-        auto rhs = [&]() {
-            QPB_ROWS(
-                double v = R[r];
-                if (r >= NX + NY) v -= ds[u] * qpb_rcp(V[r]);
-                W[pv[u]] = v;
-            )
-        };
-        // kktsolve_2 extraction: dz, ds~ and the step-length minima of this thread's rows
-        auto extract = [&](double (&ab)[2]) {
-            QPB_ROWS(if (r >= NX + NY) {
-                const double si = S[r - NX - NY], zi = V[r], dz = W[pv[u]];
-                const double d = (ds[u] - si * dz) * qpb_rcp(zi);
-                dzr[u] = dz;
-                dsl[u] = d;
-                if (d < 0) ab[0] = __builtin_fmin(ab[0], -(si / d));
-                if (dz < 0) ab[1] = __builtin_fmin(ab[1], -(zi / dz));
-            })
-        };
-        if (sigma > a.sigma_d) {
-            // predictor: ds = -lambda^2 (form_ds, Auxilary.c:319-326); kktsolve_1
-            qpb_tfor<0, RU>([&](auto uc_) { constexpr int u = decltype(uc_)::value; ds[u] = -lam[u] * lam[u]; });
-            assemble(qpb_asrc_l);
+        // this stage's system: K assembled and factored, except for the corrector
+        // (same factor as the predictor), then the solve
+        const bool fac = stage != ST_CORR;
+        if (fac) assemble(stage == ST_INIT ? qpb_asrc_i : qpb_asrc_l);
+        if (stage == ST_INIT) {
+            QPB_ROWS(W[pv[u]] = r < NX ? -chb[u] : chb[u];)
+        } else {
             rhs();
-            factor();
-            solve();
-            double ab[2] = {1e300, 1e300};
-            extract(ab);
-            qpb_bmin(ab, RED);
+        }
+        if (fac) factor();                // its level barriers order the rhs before the solve
+        else __syncthreads();
+        solve();
+        if (stage == ST_INIT) {
+            QPB_ROWS(V[r] = r < NX + NY ? W[pv[u]] : 0.0;)
+            __syncthreads();
+            stage = ST_INITZ;
+            continue;
+        }
+        double ab[2] = {1e300, 1e300};
+        extract(ab);
+        qpb_bmin(ab, RED);                // (its barriers also end every read of W above)
+        if (stage == ST_PRED) {
             const double ap = ab[0] < 1e10 ? ab[0] : 1.0, ad = ab[1] < 1e10 ? ab[1] : 1.0;
             double rr[2] = {0.0, 0.0};
             QPB_ROWS(if (r >= NX + NY) {
@@ -710,39 +739,25 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
                 constexpr int u = decltype(uc_)::value;
                 ds[u] = -(lam[u] * lam[u]) - dsl[u] * dzr[u] + smu;
             });
-            __syncthreads();              // every thread's reads of W (extract) before the new rhs
-            rhs();
-            __syncthreads();
-            solve();
-        } else {
-            // pure centering (qpSWIFT.c:572-579): refactor
-            sigma = a.sigma_d;
-            const double smu = sigma * mu;
-            qpb_tfor<0, RU>([&](auto uc_) { constexpr int u = decltype(uc_)::value; ds[u] = -(lam[u] * lam[u]) + smu; });
-            assemble(qpb_asrc_l);
-            rhs();
-            factor();
-            solve();
+            stage = ST_CORR;
+            continue;
         }
-        // kktsolve_2 extraction, step length, updates (qpSWIFT.c:583-600)
-        {
-            double ab[2] = {1e300, 1e300};
-            extract(ab);
-            qpb_bmin(ab, RED);
-            alpha_p = ab[0] < 1e10 ? ab[0] : 1.0;
-            alpha_d = ab[1] < 1e10 ? ab[1] : 1.0;
-            alpha_p = 0.99 * alpha_p > 1.0 ? 1.0 : 0.99 * alpha_p;
-            alpha_d = 0.99 * alpha_d > 1.0 ? 1.0 : 0.99 * alpha_d;
-            QPB_ROWS(
-                if (r < NX) V[r] = __builtin_fma(W[pv[u]], alpha_p, V[r]);
-                else if (r < NX + NY) V[r] = __builtin_fma(W[pv[u]], alpha_d, V[r]);
-                else {
-                    S[r - NX - NY] = __builtin_fma(dsl[u], alpha_p, S[r - NX - NY]);
-                    V[r] = __builtin_fma(dzr[u], alpha_d, V[r]);
-                }
-            )
-            __syncthreads();
-        }
+        // corrector / centering: step length and updates (qpSWIFT.c:583-600)
+        alpha_p = ab[0] < 1e10 ? ab[0] : 1.0;
+        alpha_d = ab[1] < 1e10 ? ab[1] : 1.0;
+        alpha_p = 0.99 * alpha_p > 1.0 ? 1.0 : 0.99 * alpha_p;
+        alpha_d = 0.99 * alpha_d > 1.0 ? 1.0 : 0.99 * alpha_d;
+        QPB_ROWS(
+            if (r < NX) V[r] = __builtin_fma(W[pv[u]], alpha_p, V[r]);
+            else if (r < NX + NY) V[r] = __builtin_fma(W[pv[u]], alpha_d, V[r]);
+            else {
+                S[r - NX - NY] = __builtin_fma(dsl[u], alpha_p, S[r - NX - NY]);
+                V[r] = __builtin_fma(dzr[u], alpha_d, V[r]);
+            }
+        )
+        __syncthreads();
+        it++;
+        stage = ST_TOP;
     }
     if (it == a.maxit) flag = 2;
 
