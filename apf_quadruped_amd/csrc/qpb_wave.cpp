@@ -55,6 +55,13 @@ WaveLayout wave_layout(const Plan &pl) {
     return L;
 }
 
+// odd leading dimensions of the staged P, A, G (qpb_wave.hip QPB_W_PAD, off by
+// default; QPB_WAVE_OPTS="QPB_W_PAD=1" turns them on on both sides)
+static bool wave_pad() {
+    const char *e = getenv("QPB_WAVE_OPTS");
+    return e && strstr(e, "QPB_W_PAD=1");
+}
+
 // per-wave LDS doubles (qpb_wave.hip LDS_WAVE): dense P, A, G, the L transpose
 // and the vector exchange area
 static long wave_lds_doubles(const Plan &pl, long nd) {
@@ -68,7 +75,8 @@ static long wave_lds_doubles(const Plan &pl, long nd) {
         t = std::max(t, 128L + 2 * 48 * 17 + 16);               // blocked LDL' scratch (QPB_W_BLK)
     t = ((t + 1) & ~1L) + 2;
     // staged P, A, G with odd leading dimensions (LDP, LDY, LDZ)
-    const long stage = pl.n * (pl.n | 1) + (pl.p ? pl.n * (pl.p | 1) : 0) + pl.n * (pl.m | 1);
+    const long pad = wave_pad() ? 1 : 0;
+    const long stage = pl.n * (pl.n | pad) + (pl.p ? pl.n * (pl.p | pad) : 0) + pl.n * (pl.m | pad);
     return stage + t + 2 * pl.N + pl.m + pl.n + 8;
 }
 
@@ -243,7 +251,8 @@ std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out) 
     const long n = pl.n, m = pl.m, p = pl.p;
     std::ostringstream o;
     std::vector<long> gcol;
-    common_header(o, pl, wg, "wave-cooperative", &gcol, pl.n | 1, (pl.p ? pl.p : 1) | 1, pl.m | 1);
+    const long pad = wave_pad() ? 1 : 0;
+    common_header(o, pl, wg, "wave-cooperative", &gcol, pl.n | pad, (pl.p ? pl.p : 1) | pad, pl.m | pad);
     const long nG = pl.G.nnz();
     // elimination layout: leaves first, the rest as a dense block in perm order
     const WaveLayout L = wave_layout(pl);

@@ -85,12 +85,16 @@ struct qpb_args {
 // G'WG tiles (NXP^2) and the LDL' broadcast buffers (2 x 64); its last two slots
 // are a read target for masked lanes.  (Packing, instead of ND^2, keeps the
 // 30/68/18 QP at 39.6 KB: four QPs per CU.)
-// leading dimensions of the staged matrices, odd: a lane-strided access (lane i
-// reading column i) then spreads over all LDS banks instead of a few (stride 68
-// doubles put 30 lanes on 4 bank pairs)
-#define LDP (NX | 1)
-#define LDY (NY1 | 1)
-#define LDZ (NZ | 1)
+// leading dimensions of the staged matrices.  QPB_W_PAD=1 makes them odd (a
+// lane-strided access then spreads over all LDS banks) but costs the 16-byte
+// alignment of the columns the uniform paired loads read: measured slower
+// (30/68/18, 1 024 QPs 380 vs 365 us; one AMD-ordered QP 296 vs 289 us), so off
+#ifndef QPB_W_PAD
+#define QPB_W_PAD 0       // (the host's scatter tables follow QPB_WAVE_OPTS, qpb_wave.cpp wave_pad)
+#endif
+#define LDP (QPB_W_PAD ? (NX | 1) : NX)
+#define LDY (QPB_W_PAD ? (NY1 | 1) : NY1)
+#define LDZ (QPB_W_PAD ? (NZ | 1) : NZ)
 #define OFF_A (NX * LDP)
 #define OFF_G (OFF_A + (NY > 0 ? LDY : 0) * NX)
 #define OFF_C (OFF_G + LDZ * NX)
@@ -124,8 +128,11 @@ static __device__ __forceinline__ double qpb_rcp(double v) {
 // an opaque copy of v: values derived from it (per-step lane masks, LDS addresses)
 // are formed where they are used instead of being hoisted out of the IPM loop and
 // held live across it (for large dense blocks they would not fit the registers)
+#ifndef QPB_W_OPQ
+#define QPB_W_OPQ 1       // 0: plain lane ids (the compiler may hoist what derives from them)
+#endif
 static __device__ __forceinline__ int qpb_opaque(int v) {
-    asm volatile("" : "+v"(v));
+    if constexpr (QPB_W_OPQ) asm volatile("" : "+v"(v));
     return v;
 }
 
