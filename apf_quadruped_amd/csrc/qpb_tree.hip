@@ -356,6 +356,13 @@ static __device__ __forceinline__ double qpb_rl(double v, int lane) {
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
+// value of lane J of this lane's 16-lane row (DPP row_newbcast): a panel's solve
+// runs on its first W <= 16 lanes, all in row 0, so this is lane J's value there
+// -- one VALU operation instead of two v_readlane and a move
+template <int J> static __device__ __forceinline__ double qpb_nb(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, true);
+}
+
 // right-looking LDL' of the panel (the supernode's external updates are already
 // applied; its diagonal arrives raw in rD): pivot k -> 1/D_k with the reference's
 // regularisation (ldl.c:273-274, 319-320), then A(r,c) -= A(r,k) A(c,k) / D_k for
@@ -397,8 +404,17 @@ static __device__ __forceinline__ void qpb_pfwd(double *__restrict__ L, const in
     for (int k = 0; k < W; k++) Lr[k] = -L[O_LD + ((on && lane > k) ? lp[k] + lane - k - 1 : LNZ)];
     double t = L[O_W + j0 + (on ? lane : 0)];
     const double rd = L[O_RD + j0 + (on ? lane : 0)];
+    if constexpr (W <= 16) {
+        // (t_k rd_k formed on every lane, lane k's taken: the same product)
+        qpb_tfor<0, W>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const double u = t * rd;
+            t = __builtin_fma(Lr[k], qpb_nb<k>(u), t);
+        });
+    } else {
 #pragma unroll
-    for (int k = 0; k < W; k++) t = __builtin_fma(Lr[k], qpb_rl(t, k) * qpb_rl(rd, k), t);
+        for (int k = 0; k < W; k++) t = __builtin_fma(Lr[k], qpb_rl(t, k) * qpb_rl(rd, k), t);
+    }
     if (on) L[O_W + j0 + lane] = rd * t;
 }
 
@@ -415,8 +431,15 @@ static __device__ __forceinline__ void qpb_pbwd(double *__restrict__ L, const in
 #pragma unroll
     for (int i = 0; i < W; i++) Lc[i] = -rd * L[O_LD + ((on && i > lane) ? lpl + i - lane - 1 : LNZ)];
     double v = L[O_W + j0 + (on ? lane : 0)];
+    if constexpr (W <= 16) {
+        qpb_tfor<0, W>([&](auto kc) {
+            constexpr int k = W - 1 - decltype(kc)::value;
+            v = __builtin_fma(Lc[k], qpb_nb<k>(v), v);
+        });
+    } else {
 #pragma unroll
-    for (int k = W - 1; k >= 0; k--) v = __builtin_fma(Lc[k], qpb_rl(v, k), v);
+        for (int k = W - 1; k >= 0; k--) v = __builtin_fma(Lc[k], qpb_rl(v, k), v);
+    }
     if (on) L[O_W + j0 + lane] = v;
 }
 
