@@ -181,7 +181,7 @@ long lds_doubles(const Plan &pl) {
     // panel lists, <= 3 N + 16 ints); P / A / G, c | b | h and the step tables stay in
     // global memory, the z-row work vectors in registers
     (void)npag; (void)n; (void)p;
-    return (pl.lnz + 1) + 4 * N + m + 64 + (3 * N + 16) / 2;
+    return (pl.lnz + 1) + 4 * N + m + 64 + (3 * N + 16) / 2 + (10 * N + 16) / 2;   // + step tables
 }
 
 // position of row i in column k of L (Li ascends within a column), -1 if absent

@@ -59,6 +59,17 @@ struct qpb_args {
 #define O_RED (O_W + NN)               // reduction scratch [NW][8]
 #define LDS_QP (O_RED + 64)
 #define RU ((NN + QPB_WG - 1) / QPB_WG)   // KKT rows per thread (row t + u WG)
+#ifndef QPB_T_MSLDS
+#define QPB_T_MSLDS 1   // 1: the programs' step tables staged in LDS (~1 KB): a step's metadata is one
+                        // LDS read ahead of its descriptor loads instead of a second global round trip
+#endif
+// step tables of the five programs in LDS (ints)
+#define QPB_MS_FAC 0
+#define QPB_MS_FWD (QPB_MS_FAC + 4 * QPB_fac_NSTEPS)
+#define QPB_MS_BWD (QPB_MS_FWD + 4 * QPB_fwd_NSTEPS)
+#define QPB_MS_MV (QPB_MS_BWD + 4 * QPB_bwd_NSTEPS)
+#define QPB_MS_OBJ (QPB_MS_MV + 4 * QPB_mv_NSTEPS)
+#define QPB_MS_TOTAL (QPB_MS_OBJ + 4 * QPB_obj_NSTEPS + 4)
 
 // compile-time loop (the owner-row registers are only ever indexed by constants:
 // a runtime index would put them in scratch memory)
@@ -464,6 +475,9 @@ static __device__ __forceinline__ long qpb_xcd_block() {
 extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double L[LDS_QP];
     __shared__ int SN[QPB_PANEL_INTS > 0 ? QPB_PANEL_INTS : 1];       // supernode records + panel lists
+#if QPB_T_MSLDS
+    __shared__ __attribute__((aligned(16))) int MS[QPB_MS_TOTAL];
+#endif
     const int t = threadIdx.x;
     const long q = qpb_xcd_block();
     if (q >= a.B) return;                        // workgroup-uniform
@@ -521,6 +535,16 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     if (t < 8) qpb_seg[t] = 0.0;
 #endif
     for (int j = t; j < QPB_PANEL_INTS; j += QPB_WG) SN[j] = TI[j];
+#if QPB_T_MSLDS
+    for (int j = t; j < 4 * QPB_fac_NSTEPS; j += QPB_WG) MS[QPB_MS_FAC + j] = TI[QPB_I_fac_steps + j];
+    for (int j = t; j < 4 * QPB_fwd_NSTEPS; j += QPB_WG) MS[QPB_MS_FWD + j] = TI[QPB_I_fwd_steps + j];
+    for (int j = t; j < 4 * QPB_bwd_NSTEPS; j += QPB_WG) MS[QPB_MS_BWD + j] = TI[QPB_I_bwd_steps + j];
+    for (int j = t; j < 4 * QPB_mv_NSTEPS; j += QPB_WG) MS[QPB_MS_MV + j] = TI[QPB_I_mv_steps + j];
+    for (int j = t; j < 4 * QPB_obj_NSTEPS; j += QPB_WG) MS[QPB_MS_OBJ + j] = TI[QPB_I_obj_steps + j];
+#define QPB_STEPS(name, NAME) (MS + QPB_MS_##NAME)
+#else
+#define QPB_STEPS(name, NAME) (TI + QPB_I_##name##_steps)
+#endif
     __syncthreads();
 
     // KKT values into the factor layout (init: z diagonal -1; loop: -s/z)
@@ -538,7 +562,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     };
     auto factor = [&]() {
         QPB_TIC();
-        qpb_run(TI + QPB_I_fac_steps, QPB_fac_NSTEPS, TI + QPB_I_fac_hdr, TD + QPB_D_fac,
+        qpb_run(QPB_STEPS(fac, FAC), QPB_fac_NSTEPS, TI + QPB_I_fac_hdr, TD + QPB_D_fac,
                 [&](double acc, unsigned long long d) {
                     const unsigned lo = (unsigned)d, hi = (unsigned)(d >> 32);
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(lo)) * QPB_AT(O_RD, qpb_lo16(hi)),
@@ -567,7 +591,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     // W (permuted rhs) -> W (permuted solution)
     auto solve = [&]() {
         QPB_TIC();
-        qpb_run(TI + QPB_I_fwd_steps, QPB_fwd_NSTEPS, TI + QPB_I_fwd_hdr, TD32 + QPB_D_fwd,
+        qpb_run(QPB_STEPS(fwd, FWD), QPB_fwd_NSTEPS, TI + QPB_I_fwd_hdr, TD32 + QPB_D_fwd,
                 [&](double acc, unsigned d) {
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(d)), QPB_AT(O_W, qpb_hi16(d)), acc);
                 },
@@ -586,7 +610,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
                         }
                     }
                 });
-        qpb_run(TI + QPB_I_bwd_steps, QPB_bwd_NSTEPS, TI + QPB_I_bwd_hdr, TD32 + QPB_D_bwd,
+        qpb_run(QPB_STEPS(bwd, BWD), QPB_bwd_NSTEPS, TI + QPB_I_bwd_hdr, TD32 + QPB_D_bwd,
                 [&](double acc, unsigned d) {
                     return __builtin_fma(-QPB_AT(O_LD, qpb_lo16(d)), QPB_AT(O_W, qpb_hi16(d)), acc);
                 },
@@ -607,7 +631,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     // R = [P A' G'; A 0 0; G 0 0] V (raw products)
     auto products = [&](const double *__restrict__ vec) {
         QPB_TIC();
-        qpb_run(TI + QPB_I_mv_steps, QPB_mv_NSTEPS, TI + QPB_I_mv_hdr, TD32 + QPB_D_mv,
+        qpb_run(QPB_STEPS(mv, MV), QPB_mv_NSTEPS, TI + QPB_I_mv_hdr, TD32 + QPB_D_mv,
                 [&](double acc, unsigned d) {
                     return __builtin_fma(pag((int)(qpb_lo16(d) >> 3)),
                                          *(const double *)((const char *)vec + qpb_hi16(d)), acc);
@@ -792,7 +816,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         QPB_ROWS(if (r < NX) R[r] = V[r];)
     }
     __syncthreads();
-    qpb_run(TI + QPB_I_obj_steps, QPB_obj_NSTEPS, TI + QPB_I_obj_hdr, TD32 + QPB_D_obj,
+    qpb_run(QPB_STEPS(obj, OBJ), QPB_obj_NSTEPS, TI + QPB_I_obj_hdr, TD32 + QPB_D_obj,
             [&](double acc, unsigned d) {
                 return __builtin_fma(pag((int)(qpb_lo16(d) >> 3)), *(const double *)((const char *)R + qpb_hi16(d)),
                                      acc);
