@@ -70,6 +70,7 @@ static long wave_lds_doubles(const Plan &pl, long nd) {
     const bool mfma = pl.G.nnz() > 48 && pl.n <= 64;
     long t = std::max(nd * (nd - 1) / 2, mfma ? 256 * nt * nt : 0L);
     if (nd > 16) t = std::max(t, 128L);
+    if (nd > 16 && nd <= 32) t = std::max(t, nd * nd);          // two rows per lane (QPB_W_DUP) scratch
     const char *opts = getenv("QPB_WAVE_OPTS");
     if (nd > 32 && opts && strstr(opts, "QPB_W_BLK=1"))
         t = std::max(t, 128L + 2 * 48 * 17 + 16);               // blocked LDL' scratch (QPB_W_BLK)

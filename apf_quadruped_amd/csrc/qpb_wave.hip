@@ -54,6 +54,9 @@ struct qpb_args {
 #ifndef QPB_W_BLK          // 1: blocked LDL' -- 16-column panels, rank-16 trailing updates on MFMA
 #define QPB_W_BLK 0       // 1 measured slower on 30/68/18 AMD (29.1k vs 22.5k cycles per factor), DESIGN.md
 #endif
+#ifndef QPB_W_DUP          // 1: dense blocks of 17..32 rows factored with every lane holding two rows
+#define QPB_W_DUP (QPB_ND > 16 && QPB_ND <= 32)   // (L & 15 and 16 + (L & 15)): all broadcasts DPP
+#endif
 #ifndef QPB_W_H0RE         // 1: the static part of the dense row recomputed per factor (not held live)
 #define QPB_W_H0RE (QPB_ND > 32)
 #endif
@@ -105,8 +108,8 @@ struct qpb_args {
 // (a row per lane: stride 16 would put every lane on one bank)
 #define BLK_RS 17
 #define BLK_SZ (128 + 2 * 48 * BLK_RS + 16)
-#define TSZ (((QPB_TMAX(QPB_TMAX(ND * (ND - 1) / 2, QPB_W_MFMA ? 256 * ((NX + 15) / 16) * ((NX + 15) / 16) : 0), \
-                        QPB_W_BLK ? BLK_SZ : (QPB_W_LDSB ? 128 : 0)) + 1) & ~1) + 2)
+#define TSZ (((QPB_TMAX(QPB_TMAX(QPB_TMAX(ND * (ND - 1) / 2, QPB_W_MFMA ? 256 * ((NX + 15) / 16) * ((NX + 15) / 16) : 0), \
+                                  QPB_W_BLK ? BLK_SZ : (QPB_W_LDSB ? 128 : 0)), QPB_W_DUP ? ND * ND : 0) + 1) & ~1) + 2)
 #define T_SINK (TSZ - 2)
 #define OFF_V (OFF_T + TSZ)
 #define LDS_WAVE (OFF_V + VB_SIZE)
@@ -602,6 +605,58 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         // H'(k+1,k) and H'(k+1,k+1) (values before step k) with exactly the
         // operations lane k+1's own update performs, so the trailing updates
         // of step k are off the chain.
+#if QPB_W_DUP
+        // 17..32 dense rows: lane L holds rows L & 15 (Hlo) and 16 + (L & 15) (Hhi),
+        // the same copy in each of the four 16-lane DPP rows, so H(j, k) of any row j
+        // is one row_newbcast away (no LDS round trip per pivot, no v_readlane).
+        // Every lane updates both of its rows: the same operations, in the same
+        // order, as the one-row-per-lane factor -- the same bits.
+        double Hlo[ND], Hhi[ND];
+        {
+            double *Sd = Tx;                     // ND x ND scratch (TSZ >= ND^2)
+            if (isd) {
+#pragma unroll
+                for (int e = 0; e < ND; e++) Sd[ln * ND + e] = H[e];
+            }
+            qpb_wsync();
+            const int rl = ln & 15, rh = 16 + (ln & 15);
+            const int rhc = rh < ND ? rh : ND - 1;
+#pragma unroll
+            for (int e = 0; e < ND; e++) {
+                Hlo[e] = Sd[rl * ND + e];
+                const double v = Sd[rhc * ND + e];
+                Hhi[e] = rh < ND ? v : 0.0;
+            }
+            qpb_wsync();                         // every read before Tx is reused
+        }
+        double dpiv = qpb_dpp<0x150>(Hlo[0]);    // row 0's H(0,0): lane 0 of every DPP row
+        if constexpr (qpb_dkind[0] == 2) dpiv += kdz[0];
+        const int lr = ln & 15;
+        qpb_for<0, ND>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const double rd = qpb_rcp_reg(dpiv);
+            if constexpr (k + 1 < ND) {
+                constexpr int r1 = k + 1;
+                const double h = qpb_dpp<0x150 + (r1 & 15)>(r1 < 16 ? Hlo[k] : Hhi[k]);
+                const double hkk = qpb_dpp<0x150 + (r1 & 15)>(r1 < 16 ? Hlo[k + 1] : Hhi[k + 1]);
+                dpiv = __builtin_fma(h, h * -rd, hkk);
+                if constexpr (qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
+            }
+            rDd = ln == k ? rd : rDd;
+            const double nlo = Hlo[k] * -rd, nhi = Hhi[k] * -rd;
+            qpb_for<k + 1, ND>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                const double b = qpb_dpp<0x150 + (j & 15)>(j < 16 ? Hlo[k] : Hhi[k]);   // H(j, k)
+                Hlo[j] = __builtin_fma(b, nlo, Hlo[j]);
+                Hhi[j] = __builtin_fma(b, nhi, Hhi[j]);
+            });
+            Hlo[k] = lr > k ? nlo : 0.0;
+            Hhi[k] = 16 + lr > k ? nhi : 0.0;
+        });
+        // back to one row per lane: lane d < 16 owns row d (Hlo), 16 <= d < 32 row d (Hhi)
+#pragma unroll
+        for (int e = 0; e < ND; e++) H[e] = ln < 16 ? Hlo[e] : Hhi[e];
+#else
 #if QPB_W_LDSB
         // broadcasts of the updates through LDS instead of v_readlane pairs: column
         // k (H(j,k) of every row j) is published by its lanes as soon as step k-1
@@ -718,6 +773,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             H[k] = ln > k ? nl : 0.0;       // -L(d,k) below the diagonal, 0 elsewhere
 #endif
         });
+#endif  // QPB_W_DUP
         if (fstamp) QPB_TS(fstamp + 2);
     };
     // transpose -L through LDS: lane e gets column e (0 on and above the
