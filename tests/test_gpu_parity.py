@@ -345,3 +345,26 @@ def test_winner_payload(B):
     none = torch.tensor([np.inf, -1.0], dtype=torch.float64, device="cuda")
     p2 = winner_payload(none, out["x"], 12, B).cpu().numpy()
     assert p2[1] == -1 and np.isnan(p2[2:]).all()
+
+
+@pytest.mark.gpu
+def test_wave_two_rows_per_lane_factor_bit_identical(monkeypatch):
+    """The 17-32-row dense blocks (leaves-first controller QPs: 30 rows) are
+    factored with two rows per lane (QPB_W_DUP, DPP broadcasts); it performs the
+    one-row-per-lane factor's operations in the same order, so every output is
+    bit-identical to the QPB_W_DUP=0 build."""
+    import torch
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan
+    B = 256
+    d = W.controller_qp(0xD06B07 + 33, np.arange(B))
+    res = {}
+    for opt in ("", "QPB_W_DUP=0"):
+        monkeypatch.setenv("QPB_WAVE_OPTS", opt)
+        plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], kernel="wave")
+        assert "#define QPB_ND 30" in plan.wave_source()
+        vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
+        res[opt] = plan.unpack(plan.solve(**vals, B=B), B)
+    for k in ("x", "y", "z", "s", "fval", "iters", "flag"):
+        np.testing.assert_array_equal(res[""][k], res["QPB_W_DUP=0"][k])
+    assert (res[""]["flag"] == 0).all()
