@@ -79,46 +79,78 @@ struct Snode {
     long j0, w, R;
 };
 
-// One level's tasks -> steps.  Tasks are sorted by term count; the lanes-per-task
-// exponent g minimises a rough latency model: per step, one round per term a lane
-// sums, log2 G butterfly stages and a fixed step cost.
+// One level's tasks -> steps.  Tasks are sorted by term count; a level is cut into
+// at most two groups (heavy prefix, light suffix), each with its own lanes-per-task
+// exponent g, minimising a rough latency model: per step, one round per term a lane
+// sums (kRound), log2 G butterfly stages and a fixed step cost.  (One g for a whole
+// level pads every light task to the heaviest one's rounds: MPC's factor levels had
+// 1 504 real terms in 5 106 slots.)  The steps of a level need no barrier between
+// them; the level's last step carries it.
 void pack_level(std::vector<Task> &tasks, int wg, uint64_t dummy, Prog &P) {
     if (tasks.empty()) return;
+    // weight of one round (a term per lane: its descriptor load and LDS reads)
+    // against the fixed cost of a step (30); measured on MPC: 3 -> 10 is -7 % per QP
+    static const double kRound = [] {
+        const char *e = getenv("QPB_TREE_RW");
+        return e ? atof(e) : 10.0;
+    }();
+    static const bool kSplit = !getenv("QPB_TREE_NOSPLIT");
     std::stable_sort(tasks.begin(), tasks.end(),
                      [](const Task &a, const Task &b) { return a.con.size() > b.con.size(); });
-    int best_g = 0;
-    double best_cost = 1e300;
-    for (int g = 0; (1 << g) <= std::min(64, wg); g++) {
+    const size_t n = tasks.size();
+    auto group_cost = [&](size_t b, size_t e, int g) {
         const long G = 1L << g, per = wg >> g;
         double cost = 0;
-        for (size_t s = 0; s < tasks.size(); s += per) {
+        for (size_t s = b; s < e; s += per) {
             const long R = round_bucket(((long)tasks[s].con.size() + G - 1) / G);
-            // per step: one round per term a lane sums, the butterfly, a fixed cost;
             // rounds past the 8 prefetched ones add a memory latency per 24 (qpb_run)
-            cost += 3.0 * R + 3.0 * g + 30.0 + (R > 8 ? 12.0 * (double)((R - 8 + 23) / 24) : 0.0);
+            cost += kRound * R + 3.0 * g + 30.0 + (R > 8 ? 12.0 * (double)((R - 8 + 23) / 24) : 0.0);
         }
-        if (cost < best_cost - 1e-9) { best_cost = cost; best_g = g; }
-    }
-    const int g = best_g;
-    const long G = 1L << g, per = wg >> g;
-    for (size_t s = 0; s < tasks.size(); s += per) {
-        const size_t e = std::min(tasks.size(), s + (size_t)per);
-        const long nt = (long)(e - s), act = nt * G;
-        const long R = round_bucket(((long)tasks[s].con.size() + G - 1) / G);
-        const long doff = (long)P.desc.size(), toff = (long)P.hdr.size();
-        P.desc.resize(P.desc.size() + (size_t)(R * act), dummy);
-        for (size_t t = s; t < e; t++) {
-            P.hdr.push_back(tasks[t].out);
-            const long lt = (long)(t - s);
-            for (size_t ci = 0; ci < tasks[t].con.size(); ci++) {
-                const long r = (long)ci / G, sub = (long)ci % G;
-                P.desc[doff + r * act + lt * G + sub] = tasks[t].con[ci];
+        return cost;
+    };
+    auto best_g = [&](size_t b, size_t e, double *c) {
+        int bg = 0;
+        double bc = 1e300;
+        for (int g = 0; (1 << g) <= std::min(64, wg); g++) {
+            const double cost = group_cost(b, e, g);
+            if (cost < bc - 1e-9) { bc = cost; bg = g; }
+        }
+        *c = bc;
+        return bg;
+    };
+    double best;
+    int g1 = best_g(0, n, &best), g2 = 0;
+    size_t split = n;
+    if (kSplit)
+        for (size_t s = 1; s < n; s++) {
+            if (tasks[s].con.size() == tasks[s - 1].con.size()) continue;   // cut where the count changes
+            double c1, c2;
+            const int a1 = best_g(0, s, &c1), a2 = best_g(s, n, &c2);
+            if (c1 + c2 < best - 1e-9) { best = c1 + c2; g1 = a1; g2 = a2; split = s; }
+        }
+    auto emit = [&](size_t b, size_t e_end, int g, bool last_group) {
+        const long G = 1L << g, per = wg >> g;
+        for (size_t s = b; s < e_end; s += per) {
+            const size_t e = std::min(e_end, s + (size_t)per);
+            const long nt = (long)(e - s), act = nt * G;
+            const long R = round_bucket(((long)tasks[s].con.size() + G - 1) / G);
+            const long doff = (long)P.desc.size(), toff = (long)P.hdr.size();
+            P.desc.resize(P.desc.size() + (size_t)(R * act), dummy);
+            for (size_t t = s; t < e; t++) {
+                P.hdr.push_back(tasks[t].out);
+                const long lt = (long)(t - s);
+                for (size_t ci = 0; ci < tasks[t].con.size(); ci++) {
+                    const long r = (long)ci / G, sub = (long)ci % G;
+                    P.desc[doff + r * act + lt * G + sub] = tasks[t].con[ci];
+                }
             }
+            const bool last = last_group && e == e_end;
+            P.steps.insert(P.steps.end(), {(int32_t)doff, (int32_t)toff, (int32_t)((nt << 4) | g),
+                                           (int32_t)(R | (last ? STEP_BARRIER : 0))});
         }
-        const bool last = e == tasks.size();
-        P.steps.insert(P.steps.end(), {(int32_t)doff, (int32_t)toff, (int32_t)((nt << 4) | g),
-                                       (int32_t)(R | (last ? STEP_BARRIER : 0))});
-    }
+    };
+    emit(0, split, g1, split == n);
+    if (split < n) emit(split, n, g2, true);
 }
 
 // Plan-wide tables of the tree kernel, one device buffer: every program's
