@@ -719,14 +719,16 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     if (plan->tree_ok) {
         plan->tree_wg = qpb::tree_wg_for(plan->pl);
         qpb::generate_tree_kernel(plan->pl, plan->tree_wg, &plan->tree_kname, nullptr, &plan->tree_tables);
-        // 256-thread plans (N > 160): beyond two QPs per CU (512 QPs) the 128-thread
-        // form, whose registers and LDS allow four (MPC 1 024 QPs: 3.04 -> 2.01 ms;
-        // at 512 and below the 256-thread form's shorter step chain wins, 1.58 vs 1.71)
+        // 256-thread plans (N > 160): beyond two QPs per CU (512 QPs) a 192-thread
+        // form, whose registers (<= 168: three waves per SIMD) and LDS allow four
+        // (MPC 1 024 QPs: 3.04 -> 1.65 ms; 128 threads 1.70; at 512 and below the
+        // 256-thread form's shorter step chain wins)
         if (plan->tree_wg == 256 && !getenv("QPB_TREE_WG")) {
             plan->tree_occ_batch = 512;
             if (const char *e = getenv("QPB_TREE_OCC_BATCH")) plan->tree_occ_batch = atol(e);
             if (plan->tree_occ_batch >= 0) {
-                plan->tree2_wg = 128;
+                plan->tree2_wg = 192;
+                if (const char *e = getenv("QPB_TREE2_WG")) plan->tree2_wg = atoi(e) == 128 ? 128 : 192;
                 qpb::generate_tree_kernel(plan->pl, plan->tree2_wg, &plan->tree2_kname, nullptr, &plan->tree2_tables);
             }
         }

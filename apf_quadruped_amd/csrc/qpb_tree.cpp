@@ -227,7 +227,7 @@ long lpos(const Plan &pl, long i, long k) {
 int tree_wg_for(const Plan &pl) {
     if (const char *e = getenv("QPB_TREE_WG")) {
         const int w = atoi(e);
-        if (w == 64 || w == 128 || w == 256 || w == 512) return w;
+        if (w == 64 || w == 128 || w == 192 || w == 256 || w == 512) return w;
     }
     return pl.N <= 64 ? 64 : pl.N <= 160 ? 128 : 256;
 }
@@ -252,6 +252,8 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
     o << "#define QPB_NX " << n << "\n#define QPB_NZ " << m << "\n#define QPB_NY " << p << "\n#define QPB_N " << N
       << "\n#define QPB_LNZ " << lnz << "\n#define QPB_NNZP " << nP << "\n#define QPB_NNZA " << nA
       << "\n#define QPB_NNZG " << nG << "\n#define QPB_WG " << wg << "\n";
+    // four 192-thread workgroups per CU are three waves per SIMD: <= 168 registers
+    if (wg == 192) o << "#define QPB_T_WPE 3\n";
     if (const char *e = getenv("QPB_TREE_OPTS")) {     // experiment knobs (#ifndef blocks of qpb_tree.hip)
         std::istringstream in(e);
         std::string kv;

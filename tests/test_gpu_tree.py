@@ -140,7 +140,7 @@ def test_tree_kernel_sigma_d(oracle):
 
 @pytest.mark.gpu
 def test_tree_large_batch_form_matches_oracle(oracle):
-    """Beyond 512 QPs an N > 160 plan launches its 128-thread tree kernel (four QPs
+    """Beyond 512 QPs an N > 160 plan launches its 192-thread tree kernel (four QPs
     per CU): same algorithm, its own level packing -- checked against the oracle in
     the plan's order, and its kernel name is the one qpb_plan_kernel_name reports."""
     import torch
@@ -150,7 +150,7 @@ def test_tree_large_batch_form_matches_oracle(oracle):
     B = 600
     d = plans.standard_qp("mpc_h10", np.arange(B))
     plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel="tree")
-    assert plan.kernel_name(B) != plan.kernel_name(512) and "_w128_" in plan.kernel_name(B)
+    assert plan.kernel_name(B) != plan.kernel_name(512) and "_w192_" in plan.kernel_name(B)
     vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
     r = plan.unpack(plan.solve(**vals, B=B), B)
     assert (r["flag"] == 0).all()
