@@ -379,10 +379,48 @@ template <int J> static __device__ __forceinline__ double qpb_nb(double v) {
 // regularisation (ldl.c:273-274, 319-320), then A(r,c) -= A(r,k) A(c,k) / D_k for
 // k < c <= r.  LD keeps the unscaled column (A(r,k) at pivot k), as the gather
 // programs do.  Lanes above a column's diagonal compute values never stored.
+//
+// Panels with W <= 16 and R <= W + 4 (16 - W) rows (every MPC panel: 12 x 24) are
+// factored with the top W rows copied into every 16-lane DPP row (QPB_T_PDUP):
+// lane L holds panel row L & 15 if that is < W (the same row, the same operations,
+// the same bits in all four DPP rows), else row W + (L >> 4)(16 - W) + (L & 15) - W.
+// A(c, k) for c < W is then lane c of the lane's own DPP row: one row_newbcast
+// instead of two v_readlane through SGPRs per update, and the pivot chain has no
+// VALU -> SGPR -> VALU round trip.  Only DPP row 0 stores the top rows.
+#ifndef QPB_T_PDUP
+#define QPB_T_PDUP 1
+#endif
 template <int W>
 static __device__ __forceinline__ void qpb_pfac(double *__restrict__ L, const int *__restrict__ rec, int lane) {
     const int j0 = rec[0], R = rec[2];
     const int *lp = rec + 3;
+    if constexpr (QPB_T_PDUP && W <= 16) {
+        if (R <= W + 4 * (16 - W)) {                   // uniform
+            const int c16 = lane & 15, dr = lane >> 4;
+            const int pr = c16 < W ? c16 : W + dr * (16 - W) + (c16 - W);
+            const bool on = pr < R, st = on && (pr >= W || dr == 0);
+            double P[W];
+#pragma unroll
+            for (int c = 0; c < W; c++)
+                P[c] = L[pr == c ? O_RD + j0 + c : O_LD + ((on && pr > c) ? lp[c] + pr - c - 1 : LNZ)];
+            double myr = 0.0;
+            qpb_tfor<0, W>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                const double rk = qpb_rcp_reg(qpb_nb<k>(P[k]));
+                myr = pr == k ? rk : myr;
+                const double f = -P[k] * rk;
+                qpb_tfor<k + 1, W>([&](auto cc) {
+                    constexpr int c = decltype(cc)::value;
+                    P[c] = __builtin_fma(f, qpb_nb<c>(P[k]), P[c]);
+                });
+            });
+#pragma unroll
+            for (int c = 0; c < W; c++)
+                if (st && pr > c) L[O_LD + lp[c] + pr - c - 1] = P[c];
+            if (lane < W) L[O_RD + j0 + lane] = myr;
+            return;
+        }
+    }
     const bool on = lane < R;
     double P[W];
 #pragma unroll
