@@ -387,8 +387,11 @@ template <int J> static __device__ __forceinline__ double qpb_nb(double v) {
 // A(c, k) for c < W is then lane c of the lane's own DPP row: one row_newbcast
 // instead of two v_readlane through SGPRs per update, and the pivot chain has no
 // VALU -> SGPR -> VALU round trip.  Only DPP row 0 stores the top rows.
+// Off in the 192-thread form (168 registers for three waves per SIMD): there it
+// spills more (148 vs 108 B of scratch per lane) for the same time, and the spill
+// traffic of 1 024 MPC QPs grows from 93 to 166 MB written per launch.
 #ifndef QPB_T_PDUP
-#define QPB_T_PDUP 1
+#define QPB_T_PDUP (QPB_WG != 192)
 #endif
 template <int W>
 static __device__ __forceinline__ void qpb_pfac(double *__restrict__ L, const int *__restrict__ rec, int lane) {

@@ -1,8 +1,10 @@
 """Summarise the SQ / GRBM counter passes of scripts/gpu_sq.sh into
 profiles/<name>.json: what bounds the row kernel (the headline kernel) at the
-headline batch (1 024 C1 QPs) and at 2^20 QPs.
+headline batch (1 024 C1 QPs) and at 2^20 QPs -- or, with `tree`, the passes of
+scripts/gpu_sq_tree.sh (the tree kernel on MPC QPs, one QP per workgroup).
 
     python scripts/sq_summary.py gpurun_out/sq profiles/r02_sq_row.json
+    python scripts/sq_summary.py gpurun_out/sqt profiles/r02_sq_tree.json tree
 
 Units (MI355X_MICROARCH.md, rocprofv3 PMC): SQ_WAVE_CYCLES / SQ_WAIT_* /
 SQ_ACTIVE_INST_* count quad-cycles summed over waves; SQ_INSTS_* count wave
@@ -20,26 +22,33 @@ SIMDS = 256 * 4
 FP64_PEAK_FLOP_PER_CYC_SIMD = 32      # 78.6 TF / (1 024 SIMDs x 2.4 GHz)
 
 
-def load(d):
+def load(d, prefix="qpb_row"):
     vals = defaultdict(list)
     dur = defaultdict(list)
+    wgs = {}
     for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if not r["Kernel_Name"].startswith("qpb_row"):
+            if not r["Kernel_Name"].startswith(prefix):
                 continue
             key = int(r["Grid_Size"])
+            wgs[key] = int(r["Workgroup_Size"])
             vals[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
             dur[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-    return vals, dur
+    return vals, dur, wgs
 
 
 def main():
     src, out = sys.argv[1], sys.argv[2]
-    vals, dur = load(src)
+    tree = len(sys.argv) > 3 and sys.argv[3] == "tree"
+    vals, dur, wgs = load(src, "qpb_tree" if tree else "qpb_row")
     res = {}
     for grid in sorted({g for g, _ in vals}):
         c = {n: sum(v) / len(v) for (g, n), v in vals.items() if g == grid}
-        B = grid // 64 * QPS_PER_WAVE
+        if tree:
+            B = grid // wgs[grid]
+            B = 1 if B == 8 else B          # one QP: the grid is padded to 8 blocks (one per XCD)
+        else:
+            B = grid // 64 * QPS_PER_WAVE
         t = sorted(dur[grid])[len(dur[grid]) // 2]
         wc = 4 * c["SQ_WAVE_CYCLES"]                      # cycles summed over waves
         clock = c["GRBM_GUI_ACTIVE"] / 8 / t
@@ -48,8 +57,12 @@ def main():
         fma_lane = c["SQ_INSTS_VALU_FMA_F64"] * 64 / B
         flops_issued = (2 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"]) * 64
         wps = wc / (SIMDS * cyc)
+        if tree:
+            kind = (f"one QP's step chain: {wps:.2f} waves per SIMD on average over the launch, SIMD VALU busy "
+                    f"{c['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * cyc):.0%}, a wave waits {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.0%} "
+                    f"of its cycles (LDS / descriptor loads / barriers)")
         simd_valu = c["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cyc)       # VALU-issue cycles per SIMD cycle
-        kind = (f"VALU issue at {wps:.1f} waves per SIMD (SIMD VALU busy {simd_valu:.0%}; neither HBM nor FP64 peak)"
+        kind = kind if tree else (f"VALU issue at {wps:.1f} waves per SIMD (SIMD VALU busy {simd_valu:.0%}; neither HBM nor FP64 peak)"
                 if wps > 1.5 else
                 f"latency: one wave on {wps:.0%} of the SIMDs, VALU issue + LDS/memory waits (neither HBM nor FP64 peak)")
         res[f"B={B}"] = {
@@ -68,12 +81,20 @@ def main():
             "fp64_issue_frac_of_peak": flops_issued / (FP64_PEAK_FLOP_PER_CYC_SIMD * SIMDS * cyc),
             "counters": c,
         }
-    res["reading"] = ("1 024 QPs: 256 waves, one on a quarter of the SIMDs -- the per-wave dependency chain "
+    res["reading"] = ("MPC (N = 380): one QP alone runs 6 passes of ~118 gather / panel steps each (~1 us per "
+                      "step: descriptor wait, LDS terms, butterfly, epilogue, barrier); at 1 024 QPs (4 per CU) the "
+                      "average wave lives ~0.98 ms of the 1.65 ms launch -- the launch is as long as the slowest QP "
+                      "(10-11 iterations vs a mean of 5.7), which runs alone at the end: latency, not throughput"
+                      ) if tree else ("1 024 QPs: 256 waves, one on a quarter of the SIMDs -- the per-wave dependency chain "
                       "(VALU issue ~50 %, LDS / memory waits ~40 % of its cycles) is the bound.  2^20 QPs: the "
                       "two-wave form (<= 256 registers, 3.6 KB LDS per QP) keeps ~1.9 waves per SIMD and the "
                       "SIMD's VALU busy most cycles: issue-bound, not HBM- (6-7 % of 8 TB/s) or FP64-bound; FP64 "
                       "lane-FMAs per QP are ~3.8x the algorithmic count (16 lanes per QP, sparse G rows and the "
                       "dense-row LDL' update every lane)")
+    if tree:
+        for k, v in res.items():
+            if isinstance(v, dict):
+                v.pop("fp64_issue_frac_of_peak", None)
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
         if isinstance(v, dict):
