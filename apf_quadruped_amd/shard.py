@@ -94,11 +94,17 @@ class ArgminGather:
         from ._lib import check, lib
         self._C, self._check, self._lib = C, check, lib
         idb = C.create_string_buffer(128)
+        err = None
         if rank == 0:
-            check(lib().qpb_comm_get_unique_id(idb), "qpb_comm_get_unique_id")
-        obj = [idb.raw if rank == 0 else None]
+            try:
+                check(lib().qpb_comm_get_unique_id(idb), "qpb_comm_get_unique_id")
+            except RuntimeError as e:      # still broadcast, so no rank waits forever
+                err = str(e)
+        obj = [idb.raw if err is None else None, err]
         if world > 1:
             dist.broadcast_object_list(obj, src=0)
+        if obj[1] is not None:
+            raise RuntimeError(f"rank 0: {obj[1]}")
         idb = C.create_string_buffer(obj[0], 128)
         h = C.c_void_p()
         check(lib().qpb_comm_init(C.byref(h), int(world), idb, int(rank)), "qpb_comm_init")

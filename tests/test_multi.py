@@ -98,3 +98,37 @@ def test_shard_helpers():
     g = [[1.0, 5], [1.0, 0], [np.inf, -1]]
     assert global_winner(g, [0, 100, 200]) == (1.0, 5, 0)
     assert global_winner([[np.inf, -1]], [0]) == (np.inf, -1, -1)
+
+
+def _comm_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from apf_quadruped_amd.shard import ArgminGather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ArgminGather(rank, world)
+        q.put((rank, "ok"))
+    except RuntimeError as e:
+        q.put((rank, f"raised: {e}"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_comm_setup_fails_on_every_rank_without_a_gpu():
+    """ArgminGather's bootstrap (rank 0 makes the RCCL unique id, every rank gets it
+    by broadcast, then every rank joins the communicator) must fail on every rank
+    alike without a GPU -- whether rank 0 cannot make the id (the error travels in
+    the broadcast) or the communicator cannot be made -- so bench.py's fallback is
+    collective and no rank waits forever."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(v.startswith("raised") for v in res.values()), res
