@@ -153,7 +153,7 @@ def cpu_baseline(seed, sample, passes, tol, gen=None, label="C1"):
                 mean_iters=float(iters.mean()), optimal_frac=float((flags == 0).mean()))
 
 
-def shape_leg(name, gen, B, tol, dev, steps=20, warmup=2, cpu=None):
+def shape_leg(name, gen, B, tol, dev, steps=50, warmup=5, cpu=None):
     """One non-headline workload on one GPU: B QPs of `gen`'s shape per launch
     (solve + argmin per step), kernel duration from HIP events, algorithmic-byte
     roofline, and (cpu = (sample, passes)) the reference on the host cores."""
