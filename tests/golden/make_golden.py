@@ -87,6 +87,9 @@ def main(only=None):
     if only == "c30_swing":
         c30_swing_cases(ref)
         return
+    if only == "edge_infeasible":
+        infeasible_case(ref)
+        return
     # C1: 12-var / 20-ineq / 6-eq contact-force QP (configs 1, 2, 5).
     ids = np.arange(64)
     d = W.contact_force_qp(SEED_BASE + 1, ids)
@@ -121,6 +124,20 @@ def main(only=None):
     sparse_cases(ref)
     c30_cases(ref)
     c30_swing_cases(ref)
+    infeasible_case(ref)
+
+
+def infeasible_case(ref):
+    """Edge: primal-infeasible contact-force QPs -- a lateral force of 3 kN against
+    a friction cone that allows ~100 N -- which qpSWIFT runs to maxit = 100
+    (QP_MAXIT) with diverging iterates; plus a maxit-truncated copy (tol 1e-6)."""
+    ids8 = np.arange(8)
+    r, Wr = W.contact_inputs(SEED_BASE + 7, ids8)
+    Wr = Wr.copy()
+    Wr[:, 0] += 3000.0
+    d = W.contact_qp_from_terms(r, Wr)
+    save("edge_infeasible", seed=SEED_BASE + 7, **dense_case(ref, d, ids8, 1e-6))
+    save("edge_infeasible_maxit8", seed=SEED_BASE + 7, **dense_case(ref, d, ids8, 1e-6, maxit=8))
 
 
 def to_csc(M):

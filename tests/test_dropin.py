@@ -176,7 +176,8 @@ def test_dropin_fast_default_with_reference_permutation(name):
             assert np.abs(r[k] - g[k][q]).max() <= 1e-6 * scale, (name, q, k)
 
 DENSE = ["c1_tol1e-6", "c1_tol1e-2", "c1_rowmajor", "c1_noeq", "edge_zero_g_row", "mixed_stance4",
-         "mixed_trot_blfr", "mixed_crawl_blflfr", "c1_maxit0", "c1_maxit2", "c1_maxit5"]
+         "mixed_trot_blfr", "mixed_crawl_blflfr", "c1_maxit0", "c1_maxit2", "c1_maxit5", "edge_infeasible",
+         "edge_infeasible_maxit8"]
 
 
 @pytest.fixture
@@ -262,3 +263,20 @@ def test_dropin_reuses_qp_and_plan_cache(exact_mode):
     assert f1 == f2 == 0 and np.array_equal(x1, x2) and np.array_equal(x1, g["x"][3])
     t = [dropin.solve_dense(*_golden_dense_args(g, q), perm=g["perm"][q])["tsetup"] for q in range(8)]
     assert max(t[1:]) < 0.05   # cached plan: no ordering / JIT after the first setup
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["edge_infeasible", "edge_infeasible_maxit8"])
+def test_dropin_infeasible_qp(name):
+    """A primal-infeasible QP through the controller's call (Permut = NULL): QP_SOLVE
+    returns QP_MAXIT after maxit iterations, as qpSWIFT does (golden flag and
+    iteration count), with finite iterates."""
+    g = golden(name)
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    for q in range(g["x"].shape[0]):
+        r = dropin.solve_dense(*_golden_dense_args(g, q), ordering=int(g["ordering"]), reltol=tol, abstol=tol,
+                               maxit=maxit)
+        assert r["flag"] == int(g["flag"][q]), r["error"]
+        assert r["iters"] == int(g["iters"][q]), (name, q)
+        assert all(np.isfinite(r[k]).all() for k in ("x", "y", "z", "s")), (name, q)
+

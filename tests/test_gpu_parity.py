@@ -16,8 +16,13 @@ from conftest import golden
 
 TOL = 1e-6
 DENSE_CASES = ["c1_tol1e-6", "c1_tol1e-2", "c1_rowmajor", "c1_noeq", "edge_zero_g_row",
-               "mixed_stance4", "mixed_trot_blfr", "mixed_trot_brfl", "mixed_crawl_blflfr"] + \
+               "mixed_stance4", "mixed_trot_blfr", "mixed_trot_brfl", "mixed_crawl_blflfr",
+               "edge_infeasible"] + \
               [f"c1_maxit{k}" for k in range(7)]
+# primal-infeasible QPs cut at 8 iterations: the iterates diverge, so only the exact
+# kernel (same operations, same bits) is held to them; the fast kernels are checked
+# on flag / iteration count (test_infeasible_runs_to_maxit)
+EXACT_ONLY_CASES = ["edge_infeasible_maxit8"]
 
 
 def _dense(g):
@@ -46,7 +51,7 @@ def _solve(g, perm, exact, p_upper=False, kernel="lane"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", DENSE_CASES)
+@pytest.mark.parametrize("name", DENSE_CASES + EXACT_ONLY_CASES)
 def test_exact_kernel_bit_identical_to_reference(name):
     g = golden(name)
     _, r = _solve(g, perm=g["perm"][0], exact=True, p_upper=False)
@@ -368,3 +373,21 @@ def test_wave_two_rows_per_lane_factor_bit_identical(monkeypatch):
     for k in ("x", "y", "z", "s", "fval", "iters", "flag"):
         np.testing.assert_array_equal(res[""][k], res["QPB_W_DUP=0"][k])
     assert (res[""]["flag"] == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["edge_infeasible", "edge_infeasible_maxit8"])
+@pytest.mark.parametrize("own_order,kernel", [(False, "lane"), (True, "lane"), (False, "wave"), (True, "wave"),
+                                              (True, "wave1"), (False, "tree"), (True, "tree")])
+def test_infeasible_runs_to_maxit(name, own_order, kernel):
+    """Primal-infeasible contact-force QPs (a 3 kN lateral force against ~100 N of
+    friction): qpSWIFT stops at maxit with QP_MAXIT (golden flags / iterations);
+    every fast kernel, in either KKT order, must report the same flag and iteration
+    count and keep its iterates finite."""
+    g = golden(name)
+    _, r = _solve(g, perm=None if own_order else g["perm"][0], exact=False, p_upper=True, kernel=kernel)
+    np.testing.assert_array_equal(r["flag"], g["flag"])
+    np.testing.assert_array_equal(r["iters"], g["iters"])
+    for k in ("x", "y", "z", "s"):
+        assert np.isfinite(r[k]).all(), (name, kernel, k)
+
