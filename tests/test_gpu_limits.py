@@ -22,6 +22,9 @@ LIMIT_CASES = [
     (48, 96, 24, "wave"),
     (64, 128, 8, "wave"),    # the one-QP-per-wavefront form at its variable limit
     (65, 40, 10, "other"),   # past it: lane or tree kernel
+    (12, 256, 6, "wave"),    # four z rows per lane: the inequality limit
+    (12, 257, 6, "other"),   # one inequality past it
+    (40, 64, 40, "wave"),    # as many equalities as variables
 ]
 
 
