@@ -216,11 +216,21 @@ static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, doub
     asm volatile("" ::: "memory");
     double v = __builtin_huge_val();
     long i = -1;
-    for (unsigned k = lane; k < nw; k += 64) {
-        const double pv = __builtin_bit_cast(double, __hip_atomic_load(&a.part[2 * k], __ATOMIC_RELAXED,
-                                                                       __HIP_MEMORY_SCOPE_AGENT));
-        const long pi = (long)__hip_atomic_load(&a.part[2 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (qpb_better(pv, pi, v, i)) { v = pv; i = pi; }
+    // four partials per lane per round, all loads issued before the first compare
+    // (one memory latency per 256 waves instead of one per 64)
+    for (unsigned k0 = lane; k0 < nw; k0 += 256) {
+        double pv[4];
+        long pi[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const unsigned k = k0 + 64u * u < nw ? k0 + 64u * u : nw - 1;
+            pv[u] = __builtin_bit_cast(double, __hip_atomic_load(&a.part[2 * k], __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_AGENT));
+            pi[u] = (long)__hip_atomic_load(&a.part[2 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (k0 + 64u * u < nw && qpb_better(pv[u], pi[u], v, i)) { v = pv[u]; i = pi[u]; }
     }
     for (int o = 1; o < 64; o <<= 1) {
         const double ov = __shfl_xor(v, o, 64);
@@ -633,6 +643,20 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     }
     double fr[1] = {fv};
     qpb_rsum<1>(fr);
+    // fused argmin first: the arrival's store -> s_waitcnt vmcnt(0) -> atomic round
+    // trip then waits for the wave's partial only, not for its output stores
+    if (a.best) {
+        // this wave's best: rows are QPs (fval / flag uniform within a row)
+        double bv = __builtin_huge_val();
+        long bi = -1;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const double v = qpb_rl64(fr[0], 16 * r);
+            const int f = __builtin_amdgcn_readlane(valid && flag == 0 ? 0 : 1, 16 * r);
+            if (f == 0 && qpb_better(v, qoff + q0 + r, bv, bi)) { bv = v; bi = qoff + q0 + r; }
+        }
+        qpb_argmin_arrive(a, bv, bi);
+    }
     // ---- outputs (tiled SoA)
     if (valid) {
         if (isx) a.x[tile * (NX * 64) + c * 64 + ql] = x;
@@ -675,18 +699,6 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #endif
 #endif  // QPB_R_TIMING == 3
         }
-    }
-    if (a.best) {
-        // this wave's best: rows are QPs (fval / flag uniform within a row)
-        double bv = __builtin_huge_val();
-        long bi = -1;
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const double v = qpb_rl64(fr[0], 16 * r);
-            const int f = __builtin_amdgcn_readlane(valid && flag == 0 ? 0 : 1, 16 * r);
-            if (f == 0 && qpb_better(v, qoff + q0 + r, bv, bi)) { bv = v; bi = qoff + q0 + r; }
-        }
-        qpb_argmin_arrive(a, bv, bi);
     }
 }
 
