@@ -78,6 +78,7 @@ def lib() -> C.CDLL:
     L.qpb_comm_get_unique_id.argtypes = [vp]
     L.qpb_comm_init.argtypes = [C.POINTER(vp), C.c_int, vp, C.c_int]
     L.qpb_comm_destroy.argtypes = [vp]
+    L.qpb_comm_count.argtypes = [vp, C.POINTER(C.c_int)]
     L.qpb_comm_destroy.restype = None
     L.qpb_argmin_allgather.argtypes = [vp, vp, C.c_long, C.c_long, C.c_long, vp, vp, vp]
     L.qpb_argmin_reduce.argtypes = [vp, C.c_long, C.c_long, vp, vp]

@@ -134,6 +134,15 @@ int qpb_comm_init(void **comm, int nranks, const void *id, int rank) {
     return QPB_OK;
 }
 
+int qpb_comm_count(void *comm, int *nranks) {
+    if (!comm || !nranks) return qpb::set_error(QPB_EINVAL, "NULL comm / nranks");
+    const Rccl &r = rccl();
+    if (!r.err.empty()) return qpb::set_error(QPB_EHIP, r.err.c_str());
+    ncclResult_t rc = r.commCount((ncclComm_t)comm, nranks);
+    if (rc != ncclSuccess) return rccl_fail(rc, "ncclCommCount");
+    return QPB_OK;
+}
+
 void qpb_comm_destroy(void *comm) {
     if (!comm) return;
     {

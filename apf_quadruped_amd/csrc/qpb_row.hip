@@ -41,14 +41,12 @@ struct qpb_args {
 };
 
 // Staging / H0 knobs.  Round 1 saw an illegal-address fault with ZF128, AADPP and
-// LATEFAC all on; it does not reproduce with the pinned compiler and its pre-RA
-// workaround, and both are on since: parity green, 1 024 QPs 31.9 ->
-// 31.2 us, 2^20 QPs 4.01 -> 3.69 ms (interleaved A/B, scripts/gpu_ab.sh).
+// LATEFAC all on.  Until its cause is named ZF128 and AADPP ship off.
 #ifndef QPB_R_ZF128
-#define QPB_R_ZF128 1     // zero-fill the staging area with 16-byte LDS stores
+#define QPB_R_ZF128 0     // zero-fill the staging area with 16-byte LDS stores
 #endif
 #ifndef QPB_R_AADPP
-#define QPB_R_AADPP 1     // 1e7 A'A of H0 by DPP broadcasts (1) or LDS reads (0)
+#define QPB_R_AADPP 0     // 1e7 A'A of H0 by DPP broadcasts (1) or LDS reads (0)
 #endif
 #ifndef QPB_R_LATEFAC
 #define QPB_R_LATEFAC 1   // factor after the exit test (0: before it, overlapping the reductions)

@@ -110,6 +110,13 @@ class ArgminGather:
         check(lib().qpb_comm_init(C.byref(h), int(world), idb, int(rank)), "qpb_comm_init")
         self.comm, self.rank, self.world = h, rank, world
 
+    def count(self) -> int:
+        """Ranks in the communicator as RCCL reports them (ncclCommCount)."""
+        C = self._C
+        k = C.c_int(0)
+        self._check(self._lib().qpb_comm_count(self.comm, C.byref(k)), "qpb_comm_count")
+        return int(k.value)
+
     def gather(self, best, x, n: int, B: int, base: int, out, stream):
         C = self._C
         self._check(self._lib().qpb_argmin_allgather(
@@ -118,6 +125,57 @@ class ArgminGather:
         return out
 
     def close(self):
-        if self.comm is not None and self.comm.value:
+        if getattr(self, "comm", None) is not None and self.comm.value:
             self._lib().qpb_comm_destroy(self.comm)
         self.comm = None
+
+
+def make_argmin_gather(rank: int, world: int, device):
+    """ArgminGather on every rank, or the torch fallback on every rank: the ranks
+    agree on the outcome of qpb_comm_init (an all_reduce of a success flag over the
+    default process group) so no rank is left waiting in the RCCL gather while
+    another has fallen back.  Returns (gather object, info dict for the bench line:
+    path, ranks RCCL reports, and the init error if any)."""
+    import torch
+    import torch.distributed as dist
+    ag, err = None, None
+    try:
+        ag = ArgminGather(rank, world)
+    except Exception as e:      # noqa: BLE001 -- reported in the info dict
+        err = str(e)
+    ok = torch.tensor([0 if ag is None else 1], dtype=torch.int32, device=device)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 1:
+        return ag, {"gather": "qpb_argmin_allgather", "rccl_ranks": ag.count(), "init_error": None}
+    if ag is not None:
+        ag.close()
+    return TorchGather(world), {"gather": "torch_fallback", "rccl_ranks": None,
+                                "init_error": err or "qpb_comm_init failed on another rank"}
+
+
+class TorchGather:
+    """Fallback for ArgminGather when the library's RCCL communicator cannot be
+    made on every rank: payload (qpb_winner, global index) + torch's
+    all_gather_into_tensor (also RCCL) + qpb_argmin_reduce, on the same stream."""
+
+    def __init__(self, world):
+        self.world = world
+        self.comm = None
+
+    def gather(self, best, x, n, B, base, out, stream):
+        import ctypes as C
+        import torch
+        import torch.distributed as dist
+        from ._lib import check, lib
+        with torch.cuda.stream(stream):
+            pay = winner_payload(best, x, n, B, stream=stream)
+            pay[1] = torch.where(pay[1] >= 0, pay[1] + base, pay[1])
+            g = torch.empty((2 + n) * self.world, dtype=torch.float64, device=pay.device)
+            dist.all_gather_into_tensor(g, pay)
+            check(lib().qpb_argmin_reduce(C.c_void_p(g.data_ptr()), self.world, n, C.c_void_p(out.data_ptr()),
+                                          C.c_void_p(stream.cuda_stream)), "qpb_argmin_reduce")
+        return out
+
+    def close(self):
+        pass

@@ -177,13 +177,13 @@ def shape_leg(name, gen, B, tol, dev, steps=50, warmup=5, cpu=None):
     return res
 
 
-def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, gen=None):
+def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, gen=None, info=None):
     """Timed loop of `steps` steps (solve + argmin [+ all_gather]) on resident
     inputs.  Returns (wall seconds max over ranks, mean kernel ms max over
-    ranks, outputs, gathered winners)."""
+    ranks, outputs, gathered winners); `info` (a dict) receives the gather path."""
     import torch
     import torch.distributed as dist
-    from apf_quadruped_amd.shard import ArgminGather, shard_range
+    from apf_quadruped_amd.shard import make_argmin_gather, shard_range
     base = shard_range(rank, world, B)[0]
     host = make_shard(plan, seed, base, B, chunk=65536 if gen is None else 1024, gen=gen)
     vals = {k: torch.from_numpy(v).to(dev) for k, v in host.items()}
@@ -205,11 +205,13 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
         # the argmin gather through the C ABI: qpb_argmin_allgather =
         # payload kernel + ncclAllGather of 16 + 8n B per rank (RCCL, xGMI) + device
         # reduce, on its own stream so it overlaps the next step's solve
-        try:
-            ag = ArgminGather(rank, world)
-        except Exception as e:       # keep the scaling run alive: same RCCL, through torch
-            print(f"[rank {rank}] qpb_comm_init failed ({e}); torch all_gather fallback", file=sys.stderr)
-            ag = _TorchGather(world)
+        # (every rank takes the same path: the ranks agree on qpb_comm_init's outcome)
+        ag, ginfo = make_argmin_gather(rank, world, dev)
+        if ginfo["init_error"]:
+            print(f"[rank {rank}] qpb_comm_init failed ({ginfo['init_error']}); torch all_gather fallback",
+                  file=sys.stderr)
+        if info is not None:
+            info.update(ginfo)
         gs = torch.cuda.Stream(dev)
         winners = [torch.zeros(2 + n, dtype=torch.float64, device=dev) for _ in range(nbuf)]
         solved = [torch.cuda.Event() for _ in range(nbuf)]
@@ -269,34 +271,6 @@ def run_leg(plan, B, steps, warmup, tol, dev, rank, world, seed, gather=True, ge
     else:
         result = bests[last].clone()
     return elapsed, kern_ms, outs[last], result
-
-
-class _TorchGather:
-    """Fallback for ArgminGather when the library's RCCL communicator cannot be
-    made: payload (qpb_winner, global index) + torch's all_gather_into_tensor (also
-    RCCL) + qpb_argmin_reduce, on the same stream."""
-
-    def __init__(self, world):
-        self.world = world
-        self.comm = None
-
-    def gather(self, best, x, n, B, base, out, stream):
-        import ctypes as C
-        import torch
-        import torch.distributed as dist
-        from apf_quadruped_amd import _lib
-        from apf_quadruped_amd.shard import winner_payload
-        with torch.cuda.stream(stream):
-            pay = winner_payload(best, x, n, B, stream=stream)
-            pay[1] = torch.where(pay[1] >= 0, pay[1] + base, pay[1])
-            g = torch.empty((2 + n) * self.world, dtype=torch.float64, device=pay.device)
-            dist.all_gather_into_tensor(g, pay)
-            _lib.check(_lib.lib().qpb_argmin_reduce(C.c_void_p(g.data_ptr()), self.world, n, C.c_void_p(out.data_ptr()),
-                                                    C.c_void_p(stream.cuda_stream)), "qpb_argmin_reduce")
-        return out
-
-    def close(self):
-        pass
 
 
 def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
@@ -544,7 +518,9 @@ def main():
     plan = Plan.from_dense(12, 20, 6, d0["P"][0], d0["A"][0], d0["G"][0], exact=args.exact, kernel=args.kernel)
     plan.compile()
     B = args.batch
-    elapsed, kern_ms, out, gathered = run_leg(plan, B, args.steps, args.warmup, args.tol, dev, rank, world, seed)
+    ginfo = {}
+    elapsed, kern_ms, out, gathered = run_leg(plan, B, args.steps, args.warmup, args.tol, dev, rank, world, seed,
+                                              info=ginfo)
     kname = plan.kernel_name(B)
     flags = out["flag"].cpu().numpy()
     iters = out["iters"].cpu().numpy()
@@ -643,7 +619,11 @@ def main():
             gi = int(g[1])
             line["argmin"] = {"fval": float(g[0]), "index": gi, "rank": gi // B if gi >= 0 else -1,
                               "x": g[2:].tolist() if gi >= 0 else None,
-                              "collective": "qpb_argmin_allgather (RCCL ncclAllGather, 16 + 8n B per rank)"}
+                              "gather": ginfo.get("gather"), "rccl_ranks": ginfo.get("rccl_ranks"),
+                              "init_error": ginfo.get("init_error"),
+                              "collective": ("qpb_argmin_allgather (RCCL ncclAllGather, 16 + 8n B per rank)"
+                                             if ginfo.get("gather") == "qpb_argmin_allgather" else
+                                             "torch all_gather_into_tensor (RCCL) + qpb_argmin_reduce")}
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

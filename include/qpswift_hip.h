@@ -222,6 +222,8 @@ int  qpb_apf_wrench(long K, const qpb_apf_state *st, const double *targets, doub
 int  qpb_comm_get_unique_id(void *id /* QPB_COMM_ID_BYTES */);
 int  qpb_comm_init(void **comm, int nranks, const void *id, int rank);   /* on the current HIP device */
 void qpb_comm_destroy(void *comm);
+/* Ranks RCCL reports for the communicator (ncclCommCount). */
+int  qpb_comm_count(void *comm, int *nranks);
 /* Every rank calls this after qpb_solve_best on its shard: best = that shard's
  * {fval, index} (DEVICE), x = its tiled x (nv = n, B QPs), base = global index of
  * its QP 0.  Builds the rank's payload {fval, base + index, x*[n]} on the device,

@@ -14,6 +14,9 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(config, items):
+    # the per-config GPU parity tests run first (tests/test_gpu_configs.py)
+    items.sort(key=lambda it: 0 if it.nodeid.startswith("tests/test_gpu_configs.py") or
+               os.path.basename(str(it.fspath)) == "test_gpu_configs.py" else 1)
     have_gpu = False
     try:
         import torch

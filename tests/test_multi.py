@@ -132,3 +132,32 @@ def test_two_rank_comm_setup_fails_on_every_rank_without_a_gpu():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(v.startswith("raised") for v in res.values()), res
+
+
+def _agree_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from apf_quadruped_amd.shard import TorchGather, make_argmin_gather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ag, info = make_argmin_gather(rank, world, "cpu")
+    q.put((rank, (isinstance(ag, TorchGather), info["gather"], info["rccl_ranks"], bool(info["init_error"]))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gather_path_is_agreed_on_every_rank():
+    """bench.py's gather path (make_argmin_gather): when the RCCL communicator cannot
+    be made, EVERY rank falls back to the torch gather (the ranks all_reduce the init
+    outcome), and the bench line records which path ran."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1] == (True, "torch_fallback", None, True), res
