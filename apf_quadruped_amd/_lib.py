@@ -84,6 +84,7 @@ def lib() -> C.CDLL:
     L.qpb_argmin_reduce.argtypes = [vp, C.c_long, C.c_long, vp, vp]
     L.qpb_assemble_controller.argtypes = [vp, C.c_long, vp, C.c_int, vp, C.c_double] + [vp] * 8
     L.qpb_apf_wrench.argtypes = [C.c_long, C.POINTER(QpbApfState), vp, vp, vp, vp]
+    L.qpb_apf_update.argtypes = [C.POINTER(QpbApfState), dp, C.c_double, dp]
     L.qpb_amd_order.restype = C.c_int
     L.qpb_amd_order.argtypes = [C.c_long, lp, lp, lp]
     L.qpb_plan_source.restype = C.c_long
@@ -99,6 +100,8 @@ def lib() -> C.CDLL:
     L.qpb_plan_compile.argtypes = [vp]
     L.qpb_solve.restype = C.c_int
     L.qpb_solve.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp]
+    L.qpb_solve_warm.restype = C.c_int
+    L.qpb_solve_warm.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp, vp]
     L.qpb_solve_best.restype = C.c_int
     L.qpb_solve_best.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp, vp]
     L.qpb_assemble_contact.restype = C.c_int

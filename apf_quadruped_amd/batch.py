@@ -331,6 +331,39 @@ class Plan:
         return out
 
 
+    def solve_warm(self, P, G, c, h, A=None, b=None, B=None, reltol=1e-6, abstol=1e-6, maxit=100,
+                   sigma_d=0.0, out=None, sigma=None, stream=None):
+        """Warm solve (qpb_solve_warm): continue every QP from out's x, y, z, s,
+        iters and flag and from sigma (float64 device tensor [B], in/out), as a
+        second QP_SOLVE on the same QP object does (qpSWIFT.c:502-596).  Inputs as
+        solve(); `out` must hold the previous state."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+        def t(a):
+            if a is None:
+                return None
+            if isinstance(a, np.ndarray):
+                a = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
+            return a
+
+        P, G, c, h, A, b = map(t, (P, G, c, h, A, b))
+        if B is None:
+            B = c.numel() // self.n
+        if out is None or sigma is None:
+            raise ValueError("solve_warm needs the previous outputs and sigma")
+        st = QpbSettings(int(maxit), float(reltol), float(abstol), float(sigma_d))
+        if stream is None:
+            stream = torch.cuda.current_stream(dev)
+        ptr = lambda a: None if a is None else C.c_void_p(a.data_ptr())
+        check(_lib.lib().qpb_solve_warm(self._h, int(B), ptr(P), ptr(A) if self.p else None, ptr(G), ptr(c), ptr(h),
+                                        ptr(b) if self.p else None, C.byref(st), ptr(out["x"]),
+                                        ptr(out["y"]) if self.p else None, ptr(out["z"]), ptr(out["s"]),
+                                        ptr(out["flag"]), ptr(out["iters"]), ptr(out["fval"]),
+                                        ptr(out.get("stats")), ptr(sigma), C.c_void_p(stream.cuda_stream)),
+              "qpb_solve_warm")
+        return out
+
     def launcher(self, vals, out, B, reltol=1e-6, abstol=1e-6, maxit=100, sigma_d=0.0, stream=None, best=None):
         """A zero-argument callable that launches qpb_solve on fixed device buffers
         with every C argument pre-built: one ctypes call per launch, so a Python
@@ -507,6 +540,16 @@ def apf_state(**kw) -> QpbApfState:
                 for i, x in enumerate(flat):
                     arr[i] = x
     return st
+
+
+def apf_update(state: QpbApfState, h_prev, period_st: float) -> float:
+    """qpb_apf_update: one gait step's robustness smoothing and fake_crawl
+    (main.cpp:1273-1321), in place; returns robf_to_mean."""
+    h = np.ascontiguousarray(h_prev, dtype=np.float64).reshape(4)
+    mean = C.c_double(0.0)
+    check(_lib.lib().qpb_apf_update(C.byref(state), h.ctypes.data_as(C.POINTER(C.c_double)), float(period_st),
+                                    C.byref(mean)), "qpb_apf_update")
+    return float(mean.value)
 
 
 def apf_wrench(state: QpbApfState, targets, K=None, wrench=None, com_des=None, stream=None):

@@ -449,6 +449,18 @@ extern "C" int qpb_assemble_controller(const qpb_plan *plan_c, long B, const dou
     return QPB_OK;
 }
 
+// main.cpp:1273-1276 (the smoothing, per foot, in BR BL FL FR order of the state)
+// and :1307-1321 (robf_to_mean = (bl + fr + br + fl) / 4, fake_crawl below 0.34)
+extern "C" int qpb_apf_update(qpb_apf_state *st, const double h_prev[4], double period_st, double *robf_mean) {
+    if (!st || !h_prev) return qpb::set_error(QPB_EINVAL, "bad APF update arguments");
+    for (int i = 0; i < 4; i++) st->rob_foot[i] = 0.35 * st->rob_foot[i] + 0.65 * h_prev[i] / period_st;
+    const double *rf = st->rob_foot;        // 0 BR, 1 BL, 2 FL, 3 FR
+    const double mean = (rf[1] + rf[3] + rf[0] + rf[2]) / 4.0;
+    st->fake_crawl = mean < 0.34 ? 1 : 0;
+    if (robf_mean) *robf_mean = mean;
+    return QPB_OK;
+}
+
 extern "C" int qpb_apf_wrench(long K, const qpb_apf_state *st, const double *targets, double *wrench,
                               double *com_des, void *stream) {
     if (K < 0 || !st) return qpb::set_error(QPB_EINVAL, "bad APF arguments");

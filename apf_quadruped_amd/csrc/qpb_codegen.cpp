@@ -417,6 +417,9 @@ struct Gen {
              "  long B;\n"
              "  double tol, abstol, sigma_d;\n"
              "  long maxit;\n"
+             "  const void *tab; double *best; unsigned long long *part; unsigned *ctr;\n"
+             "  double *sig;   // per-QP sigma: in (warm) / out (NULL: not tracked)\n"
+             "  long warm;     // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)\n"
              "};\n";
         o << "static __device__ __forceinline__ double qpb_rcp(double v) {\n"
              "  double r = __builtin_amdgcn_rcp(v);\n"
@@ -474,7 +477,22 @@ struct Gen {
         if (!park.count("s")) decl_vec("s", m);
         if (!park.count("z")) decl_vec("z", m);
 
-        // ---- kkt_initialize (Auxilary.c:992-1089)
+        // ---- kkt_initialize (Auxilary.c:992-1089); a warm solve (QP_SOLVE called
+        // again, qpSWIFT.c:502-596) instead continues from the output arrays
+        ln("long it0 = 0; int flag0 = 3; double sigma = 100.0;");
+        open("if (a.warm) {");
+        begin_phase(false, false);
+        auto warm_load = [&](const char *arr, long nv) {
+            for (long i = 0; i < nv; i++)
+                wr(arr, i, std::string("a.") + arr + "[tile * " + S(nv * 64) + " + " + S(i * 64) + " + lane]");
+        };
+        warm_load("x", n);
+        warm_load("y", p);
+        warm_load("s", m);
+        warm_load("z", m);
+        ln("it0 = a.iters[q]; flag0 = a.flag[q]; sigma = a.sig[q];");
+        close();
+        open("else {");
         ln("// setup: factor the KKT holding -I, solve for rhs [-c; b; h]");
         begin_phase();
         factor(pl.K_init);
@@ -504,13 +522,14 @@ struct Gen {
         for (long i = 0; i < m; i++) wr("s", i, "sh < 0 ? " + V("zi", i) + " : " + V("zi", i) + " + (1 + sh)");
         for (long i = 0; i < m; i++) wr("z", i, "hi < 0 ? -" + V("zi", i) + " : -" + V("zi", i) + " + (1 + hi)");
         close();
+        close();   // else (cold)
 
-        // ---- QP_SOLVE loop (qpSWIFT.c:502-602)
-        ln("long it = 0; int flag = 3;");
+        // ---- QP_SOLVE loop (qpSWIFT.c:502-602); QP_MAXIT only when IterationCount
+        // == maxit (qpSWIFT.c:598-601), IterationCount = it0 + it
+        ln("long it = 0; int flag = flag0;");
         ln("double fval = 0.0, st_rx = 0.0, st_ry = 0.0, st_rz = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;");
-        ln("double sigma = 100.0;");
         open("for (;;) {");
-        ln("if (it >= a.maxit) { flag = 2; break; }");
+        ln("if (it >= a.maxit) { flag = it0 + it == a.maxit ? 2 : flag0; break; }");
         begin_phase();
         // residuals (Auxilary.c:745-786) and objective (Auxilary.c:1133-1141)
         if (opt.exact) {
@@ -602,7 +621,7 @@ struct Gen {
         dot("sz", m, "s", "z");
         ln("st_mu = sz / " + S(m) + ".0;");
         ln(std::string("if (st_rx < a.tol && st_rz < a.tol") + (p ? " && st_ry < a.tol" : "") +
-           " && st_mu < a.abstol) { flag = 0; break; }");
+           " && st_mu < a.abstol) { flag = it0 + it == a.maxit ? 2 : 0; break; }");
         // lambda, mu (qpSWIFT.c:537-538)
         // lambda = sqrt(s.*z) (Auxilary.c:638-646) only ever enters squared, so the
         // fast kernel uses lambda^2 = s.*z directly (no sqrt).
@@ -728,7 +747,8 @@ struct Gen {
         if (p) store("y", p, "y");
         store("z", m, "z");
         store("s", m, "s");
-        ln("a.flag[q] = flag; a.iters[q] = (int)it; a.fval[q] = fval;");
+        ln("a.flag[q] = flag; a.iters[q] = (int)(it0 + it); a.fval[q] = fval;");
+        ln("if (a.sig) a.sig[q] = sigma;");
         ln("if (a.stats) { double *o = a.stats + tile * 384 + lane; o[0] = st_rx; o[64] = st_ry; o[128] = st_rz;"
            " o[192] = st_mu; o[256] = ap; o[320] = ad; }");
         o << "}\n";

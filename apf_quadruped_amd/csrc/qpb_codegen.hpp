@@ -37,6 +37,13 @@ struct KernelArgs {
     double *best = nullptr;                 // row kernel: fused argmin output {fval, index}
     unsigned long long *part = nullptr;     //   per-wave partials
     unsigned *ctr = nullptr;                //   arrival counter (zero between launches)
+    // warm solve (qpb_solve_warm; QP_SOLVE called again on the same QP object,
+    // qpSWIFT.c:502-596): warm = 0 is cold (kkt_initialize first); warm = 1
+    // continues every QP from x, y, z, s, iters, flag as they are in the output
+    // arrays and from sigma = sig[q] (options->sigma).  sig (when not NULL)
+    // receives the last sigma.
+    double *sig = nullptr;
+    long warm = 0;
 };
 
 std::string kernel_name(const Plan &pl, const GenOptions &opt);

@@ -38,6 +38,8 @@ struct qpb_args {
     double *best;             // fused argmin (qpb_solve_best): {fval, index}, or NULL
     unsigned long long *part; // per-wave partials {fval bits, index}
     unsigned *ctr;            // arrival counter (zero between launches)
+    double *sig;              // per-QP sigma: in (warm) / out (NULL: not tracked)
+    long warm;                // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
 };
 
 // Staging / H0 knobs.  Round 1 saw an illegal-address fault with ZF128, AADPP and
@@ -494,15 +496,33 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     // QP_SOLVE loop (qpSWIFT.c:502-602); the wave runs until all four rows stop
     double x = 0.0, y = 0.0, s0 = 1.0, s1 = 1.0, z0 = 1.0, z1 = 1.0;
     bool act = valid;
-    int flag = 3;
-    long itq = 0;
+    long itq = 0, it0 = 0;     // it0: IterationCount the QP enters with (warm solve)
+    int flag0 = 3;             // stats->Flag it enters with (QP_FATAL after setup)
     double st_rx2 = 0.0, st_ry2 = 0.0, st_rz2 = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0, fv = 0.0;
     const double tol2 = a.tol > 0.0 ? a.tol * a.tol : -1.0;
-    double sigma = 100.0;
+    double sigma = 100.0;      // options->sigma (SIGMA, GlobalOptions.h:49)
     long it = -1;
+    if (a.warm) {
+        // warm: QP_SOLVE continues from the object's iterate, IterationCount and
+        // options->sigma (qpSWIFT.c:502-596 never re-initialises); no setup pass
+        if (isx) x = a.x[tile * (NX * 64) + c * 64 + ql];
+#if NY > 0
+        if (isy) y = a.y[tile * (NY * 64) + c * 64 + ql];
+#endif
+        if (isz0) { z0 = a.z[tile * (NZ * 64) + c * 64 + ql]; s0 = a.s[tile * (NZ * 64) + c * 64 + ql]; }
+        if (isz1) { z1 = a.z[tile * (NZ * 64) + (16 + c) * 64 + ql]; s1 = a.s[tile * (NZ * 64) + (16 + c) * 64 + ql]; }
+        it0 = a.iters[qc];
+        flag0 = a.flag[qc];
+        sigma = a.sig[qc];
+        it = 0;
+    }
+    int flag = flag0;
+    double sigf = sigma;       // options->sigma when this row's loop ends (a frozen row's own
+                               // sigma keeps being recomputed while the rest of the wave runs)
     for (;;) {
         if (it >= 0 && it >= a.maxit) {
-            if (act) { flag = 2; itq = it; }
+            // qpSWIFT.c:598-601: QP_MAXIT only when IterationCount == maxit
+            if (act) { itq = it0 + it; flag = itq == a.maxit ? 2 : flag0; sigf = sigma; }
             break;
         }
         // updatekktmatrix (Auxilary.c:211-215): z diagonal -s/z (-I at setup, s = z = 1)
@@ -556,8 +576,9 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 st_rz2 = red[2];
                 st_mu = mu_it;
                 if (red[0] < tol2 && red[2] < tol2 && (NY == 0 || red[1] < tol2) && mu_it < a.abstol) {
-                    flag = 0;
-                    itq = it;
+                    itq = it0 + it;
+                    flag = itq == a.maxit ? 2 : 0;
+                    sigf = sigma;
                     act = false;
                 }
             }
@@ -674,6 +695,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             a.flag[q] = flag;
             a.iters[q] = (int)itq;
             a.fval[q] = fr[0];
+            if (a.sig) a.sig[q] = sigf;
 #if QPB_R_TIMING == 3
             QPB_TM(4);
             if (a.stats) {

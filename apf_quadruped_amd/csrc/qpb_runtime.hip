@@ -641,6 +641,7 @@ int set_error(int code, const char *msg) { return fail(code, msg); }
 
 int strided_copy(const CopySegs &t, void *stream) {
     if (t.nseg <= 0) return QPB_OK;
+    if (t.nseg > CopySegs::kMax) return fail(QPB_EINVAL, "strided copy: too many segments");
     long mx = 1;
     for (int i = 0; i < t.nseg; i++) mx = std::max(mx, t.seg[i].n);
     const unsigned gx = (unsigned)std::min<long>(64, (mx + 255) / 256);
@@ -868,10 +869,13 @@ int qpb_plan_compile(qpb_plan *plan) {
     return rc;
 }
 
-static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
+}  // extern "C"
+
+int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
                       const double *c, const double *h, const double *b, const qpb_settings *st,
                       double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
-                      double *stats, double *best, void *stream) {
+                      double *stats, double *best, void *stream, double *sig, bool warm) {
+    if (warm && !sig) return fail(QPB_EINVAL, "a warm solve needs sigma");
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     if (B < 0) return fail(QPB_EINVAL, "need B >= 0");
     if (B == 0) return QPB_OK;
@@ -909,6 +913,8 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     a.abstol = st->abstol;
     a.sigma_d = st->sigma_d;
     a.maxit = st->maxit;
+    a.sig = sig;
+    a.warm = warm ? 1 : 0;
     if (tree && (rc = qpb::tree_tables_on_device(plan, &a.tab, tree2))) return rc;
     // qpb_solve_best on the row kernel: the argmin runs inside the solve launch
     // (its last wave reduces the per-wave partials), saving the separate launch
@@ -935,11 +941,14 @@ static int solve_impl(qpb_plan *plan, long B, const double *P, const double *A, 
     return QPB_OK;
 }
 
+extern "C" {
+
 int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
               const double *c, const double *h, const double *b, const qpb_settings *st,
               double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
               double *stats, void *stream) {
-    return solve_impl(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, nullptr, stream);
+    return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, nullptr, stream,
+                         nullptr, false);
 }
 
 int qpb_solve_best(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
@@ -947,7 +956,17 @@ int qpb_solve_best(qpb_plan *plan, long B, const double *P, const double *A, con
                    double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
                    double *stats, double *best, void *stream) {
     if (!best) return fail(QPB_EINVAL, "qpb_solve_best: best is NULL");
-    return solve_impl(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, best, stream);
+    return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, best, stream,
+                         nullptr, false);
+}
+
+int qpb_solve_warm(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
+                   const double *c, const double *h, const double *b, const qpb_settings *st,
+                   double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
+                   double *stats, double *sigma, void *stream) {
+    if (!sigma) return fail(QPB_EINVAL, "qpb_solve_warm: sigma is NULL");
+    return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, nullptr, stream, sigma,
+                         true);
 }
 
 /* ---- plan groups: one launch for a mixed-pattern batch (qpb_group_*) ---- */

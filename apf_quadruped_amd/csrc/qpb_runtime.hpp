@@ -53,7 +53,8 @@ struct CopySeg {
     long n, ss, ds;   // element count, source stride, destination stride
 };
 struct CopySegs {
-    CopySeg seg[8];
+    static constexpr int kMax = 16;
+    CopySeg seg[kMax];
     int nseg;
 };
 // Device-side strided copies on `stream` (one launch for all segments).
@@ -65,4 +66,9 @@ int compile_tree2(qpb_plan *plan);
 int compile_tree(qpb_plan *plan);
 std::string wave_source_of(const qpb_plan *plan);   // wave or row form, as the plan chose
 int set_error(int code, const char *msg);
+// qpb_solve / qpb_solve_best / qpb_solve_warm in one: best != NULL fuses the
+// argmin; sig != NULL receives every QP's last sigma (and, warm, supplies it)
+int solve_ex(qpb_plan *plan, long B, const double *P, const double *A, const double *G, const double *c,
+             const double *h, const double *b, const qpb_settings *st, double *x, double *y, double *z, double *s,
+             int *flag, int *iters, double *fval, double *stats, double *best, void *stream, double *sig, bool warm);
 }  // namespace qpb

@@ -32,6 +32,8 @@ struct qpb_args {
     double *best;           // (row kernel's fused argmin; unused here)
     unsigned long long *part;
     unsigned *ctr;
+    double *sig;            // per-QP sigma: in (warm) / out (NULL: not tracked)
+    long warm;              // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
 };
 
 #define NX QPB_NX
@@ -694,8 +696,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
 #endif
     double sigma = 100.0, alpha_p = 0.0, alpha_d = 0.0;
     double n_rx = 0.0, n_ry = 0.0, n_rz = 0.0, n_mu = 0.0, mu = 0.0;
-    long it = 0;
-    int flag = 2;
+    long it = 0, it0 = 0;       // it0: IterationCount the QP enters with (warm solve)
+    int flag0 = 3;              // stats->Flag it enters with (QP_FATAL after setup)
+    bool conv = false;
     const double invm = 1.0 / (double)NZ;
     // rhs b = [rx; ry; rz - ds/z] (updatekktmatrix_b, Auxilary.c:274-295)
     auto rhs = [&]() {
@@ -722,6 +725,25 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     // (sigma <= sigma_d: refactor, qpSWIFT.c:572-579)
     enum { ST_INIT, ST_INITZ, ST_TOP, ST_PRED, ST_CORR, ST_CENT };
     int stage = ST_INIT;
+    if (a.warm) {
+        // warm: QP_SOLVE continues from the object's iterate, IterationCount and
+        // options->sigma (qpSWIFT.c:502-596 never re-initialises); no setup solve
+        for (int j = t; j < NX; j += QPB_WG) V[j] = a.x[tile * (NX * 64) + j * 64 + ql];
+#if NY > 0
+        for (int j = t; j < NY; j += QPB_WG) V[NX + j] = a.y[tile * (NY * 64) + j * 64 + ql];
+#endif
+        for (int j = t; j < NZ; j += QPB_WG) {
+            V[NX + NY + j] = a.z[tile * (NZ * 64) + j * 64 + ql];
+            S[j] = a.s[tile * (NZ * 64) + j * 64 + ql];
+        }
+        it0 = a.iters[q];
+        flag0 = a.flag[q];
+        sigma = a.sig[q];
+        __syncthreads();
+        QPB_ROWS(if (r < NX) xp[u] = V[r];)
+        stage = ST_TOP;
+    }
+    int flag = flag0;
     for (;;) {
         if (stage == ST_INITZ || stage == ST_TOP) {
             if (stage == ST_TOP && it >= a.maxit) break;
@@ -767,7 +789,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
                 n_rz = __builtin_sqrt(acc[2]);
                 n_mu = acc[3] * invm;
             }
-            if (n_rx < a.tol && n_rz < a.tol && (NY == 0 || n_ry < a.tol) && n_mu < a.abstol) { flag = 0; break; }
+            if (n_rx < a.tol && n_rz < a.tol && (NY == 0 || n_ry < a.tol) && n_mu < a.abstol) {
+                flag = 0;
+                conv = true;
+                break;
+            }
             {
                 double acc[1] = {0.0};
                 QPB_ROWS(if (r >= NX + NY) {
@@ -847,11 +873,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         it++;
         stage = ST_TOP;
     }
-    if (it == a.maxit) flag = 2;
+    if (it0 + it == a.maxit) flag = 2;     // qpSWIFT.c:598-601: IterationCount == maxit
 
     // ---- objective of the x the last residuals were computed at (qpSWIFT.c:515):
     // V itself after convergence, else the iteration's starting x (owner registers)
-    if (flag != 0) {
+    if (!conv) {
         QPB_ROWS(if (r < NX) R[r] = xp[u];)     // R is free here: the objective's x
     } else {
         QPB_ROWS(if (r < NX) R[r] = V[r];)
@@ -880,8 +906,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     }
     if (t == 0) {
         a.flag[q] = flag;
-        a.iters[q] = (int)it;
+        a.iters[q] = (int)(it0 + it);
         a.fval[q] = fv[0];
+        if (a.sig) a.sig[q] = sigma;
         if (a.stats) {
             double *st = a.stats + tile * (6 * 64) + ql;
 #if QPB_T_TIMING == 2

@@ -80,6 +80,10 @@ struct Priv {
     long nP = 0, nA = 0, nG = 0, nin = 0, nout = 0;
     long oP = 0, oA = 0, oG = 0, oc = 0, oh = 0, ob = 0, ox = 0, oy = 0, oz = 0, os = 0, ost = 0, ofv = 0,
          oin = 0, oout = 0, ototal = 0;
+    // kkt_initialize's point is in x, y, z, s (QP_SETUP ran it on the device):
+    // QP_SOLVE then continues from the object's state (a warm solve), as the
+    // reference's QP_SOLVE always does; otherwise its first QP_SOLVE is cold
+    bool inited = false;
 };
 
 // Public struct first so that a QP* is also a Handle*.
@@ -366,7 +370,7 @@ int ensure_device(Priv &v, const QP &q) {
         v.nin = v.nP + v.nA + v.nG + q.n + q.m + q.p;
         v.nout = q.n + q.p + 2 * q.m + 6 + 1;   // x y z s stats fval
         v.oin = take(v.nin);
-        v.oout = take(v.nout + 1);              // + flag, iters (two ints in one double slot)
+        v.oout = take(v.nout + 2);              // + flag, iters (two ints in one double slot), sigma
         v.ofv = v.oout + v.nout - 1;
         v.ototal = o;
     }
@@ -384,7 +388,7 @@ int ensure_device(Priv &v, const QP &q) {
         }
         w.dcap = v.ototal;
     }
-    const long hneed = v.nin + v.nout + 1;
+    const long hneed = v.nin + v.nout + 2;
     if (!zero_copy(v) && w.hcap < hneed) {
         if (w.hmem) (void)hipHostFree(w.hmem);
         w.hcap = 0;
@@ -418,10 +422,50 @@ int ensure_device(Priv &v, const QP &q) {
     return QPB_OK;
 }
 
-// Zero-copy solve: inputs written straight into the tiled slot of QP 0 (stride
-// 64) of the mapped pinned slab, one launch reads them over the host link and
-// writes x, y, z, s, stats, flag, iterations and fval back into it.
-int solve_zero_copy(Priv &v, QP &q) {
+// The state a warm solve continues from / a solve leaves (the QP object's
+// public fields), and the settings of this call.
+struct CallState {
+    bool warm;
+    qpb_settings st;
+};
+
+CallState call_state(const Priv &v, const QP &q, long maxit) {
+    CallState cs;
+    cs.warm = v.inited;
+    cs.st.maxit = maxit;
+    cs.st.reltol = q.options->reltol;
+    cs.st.abstol = q.options->abstol;
+    cs.st.sigma_d = q.sigma_d;
+    return cs;
+}
+
+// Results of one launch back into the QP object.  `setup_init`: the launch was
+// QP_SETUP's kkt_initialize (maxit = 0): only x, y, z, s change.
+void take_results(Priv &v, QP &q, const double *x, const double *y, const double *z, const double *s,
+                  const double *stv, double fval, const int *fl_it, double sigma, long maxit, bool setup_init) {
+    const long n = q.n, m = q.m, p = q.p;
+    std::memcpy(q.x, x, sizeof(double) * (size_t)n);
+    if (p > 0) std::memcpy(q.y, y, sizeof(double) * (size_t)p);
+    std::memcpy(q.z, z, sizeof(double) * (size_t)m);
+    std::memcpy(q.s, s, sizeof(double) * (size_t)m);
+    if (setup_init) return;
+    const long before = v.st.IterationCount;
+    v.st.Flag = fl_it[0];
+    v.st.IterationCount = fl_it[1];
+    q.options->sigma = sigma;
+    // the loop body never ran (maxit <= 0): the reference touches no statistic;
+    // no iteration ran: its step lengths stay as they were (qpSWIFT.c:506-596)
+    if (maxit <= 0) return;
+    v.st.fval = fval;
+    v.st.n_rx = stv[0]; v.st.n_ry = stv[1]; v.st.n_rz = stv[2]; v.st.n_mu = stv[3];
+    if (v.st.IterationCount != before) { v.st.alpha_p = stv[4]; v.st.alpha_d = stv[5]; }
+}
+
+// Zero-copy solve: inputs (and, warm, the QP's state) written straight into the
+// tiled slot of QP 0 (stride 64) of the mapped pinned slab, one launch reads
+// them over the host link and writes x, y, z, s, stats, flag, iterations, fval
+// and sigma back into it.
+int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     const long n = q.n, m = q.m, p = q.p;
     double *h = v.zmem, *d = v.zdev;
     auto put = [h](long off, const double *src, long k) {
@@ -433,34 +477,36 @@ int solve_zero_copy(Priv &v, QP &q) {
     put(v.oc, q.c, n);
     put(v.oh, q.h, m);
     if (p > 0) put(v.ob, q.b, p);
-    qpb_settings st;
-    st.maxit = q.options->maxit;
-    st.reltol = q.options->reltol;
-    st.abstol = q.options->abstol;
-    st.sigma_d = q.sigma_d;
-    const long ofl = v.oout;               // flag, iterations: two ints in one double slot
-    int rc = qpb_solve(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
-                       p > 0 ? d + v.ob : nullptr, &st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz, d + v.os,
-                       reinterpret_cast<int *>(d + ofl), reinterpret_cast<int *>(d + ofl) + 1, d + v.ofv, d + v.ost,
-                       v.stream);
+    const long ofl = v.oout + v.nout;       // flag, iterations: two ints in one double slot
+    const long osg = ofl + 1;               // sigma (options->sigma)
+    if (cs.warm) {
+        put(v.ox, q.x, n);
+        if (p > 0) put(v.oy, q.y, p);
+        put(v.oz, q.z, m);
+        put(v.os, q.s, m);
+        const int iv[2] = {(int)v.st.Flag, (int)v.st.IterationCount};
+        std::memcpy(h + ofl, iv, sizeof(iv));
+        h[osg] = q.options->sigma;
+    }
+    int *dfl = reinterpret_cast<int *>(d + ofl);
+    int rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
+                           p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz,
+                           d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, nullptr, v.stream, d + osg, cs.warm);
     if (hipStreamSynchronize(v.stream) != hipSuccess && !rc) rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: kernel failed");
     if (rc) return rc;
+    std::vector<double> tmp((size_t)(n + p + 2 * m + 6));
+    double *tx = tmp.data(), *ty = tx + n, *tz = ty + p, *ts = tz + m, *tst = ts + m;
     auto get = [h](double *dst, long off, long k) {
         for (long i = 0; i < k; i++) dst[i] = h[off + 64 * i];
     };
-    get(q.x, v.ox, n);
-    if (p > 0) get(q.y, v.oy, p);
-    get(q.z, v.oz, m);
-    get(q.s, v.os, m);
-    double r[6];
-    get(r, v.ost, 6);
-    v.st.n_rx = r[0]; v.st.n_ry = r[1]; v.st.n_rz = r[2]; v.st.n_mu = r[3];
-    v.st.alpha_p = r[4]; v.st.alpha_d = r[5];
-    v.st.fval = h[v.ofv];
+    get(tx, v.ox, n);
+    if (p > 0) get(ty, v.oy, p);
+    get(tz, v.oz, m);
+    get(ts, v.os, m);
+    get(tst, v.ost, 6);
     int iv[2];
     std::memcpy(iv, h + ofl, sizeof(iv));
-    v.st.Flag = iv[0];
-    v.st.IterationCount = iv[1];
+    take_results(v, q, tx, ty, tz, ts, tst, h[v.ofv], iv, h[osg], cs.st.maxit, setup_init);
     return QPB_OK;
 }
 
@@ -475,19 +521,15 @@ void mirror_kkt(Priv &v, QP &q) {
             v.Kpr[k] = kkt_slot_value(pl.K_loop[k], q.P->pr, Av, q.G->pr, q.s, q.z);
 }
 
-int solve_on_device(Priv &v, QP &q) {
-    int rc = ensure_device(v, q);
-    if (rc) return rc;
-    int cur = -1;
-    (void)hipGetDevice(&cur);
-    if (cur != v.dev) (void)hipSetDevice(v.dev);
+// Staged solve (QPSWIFT_HIP_STAGED=1, and always for the exact lane kernel,
+// which re-reads its inputs every iteration -- over the host link that costs more
+// than the copies).  The pinned host slab mirrors the device region [oin, oout +
+// nout + 2): packed inputs | packed x y z s stats fval | flag, iterations | sigma,
+// so ONE host-to-device copy carries the inputs and (warm) the QP's state, a
+// scatter kernel spreads them to the tiled slots, the solve runs, a gather kernel
+// packs the results and ONE device-to-host copy brings them back.
+int solve_staged(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     const long n = q.n, m = q.m, p = q.p;
-    if (zero_copy(v)) {
-        rc = solve_zero_copy(v, q);
-        if (cur != v.dev && cur >= 0) (void)hipSetDevice(cur);
-        if (!rc) mirror_kkt(v, q);
-        return rc;
-    }
     double *hin = v.hmem, *hout = v.hmem + v.nin;
     double *w = hin;
     auto put = [&w](const double *src, long k) {
@@ -500,12 +542,26 @@ int solve_on_device(Priv &v, QP &q) {
     put(q.c, n);
     put(q.h, m);
     if (p > 0) put(q.b, p);
+    long up = v.nin;                         // doubles to upload
+    if (cs.warm) {                           // the QP's state into the packed output region
+        w = hout;
+        put(q.x, n);
+        if (p > 0) put(q.y, p);
+        put(q.z, m);
+        put(q.s, m);
+        const int iv[2] = {(int)v.st.Flag, (int)v.st.IterationCount};
+        std::memcpy(hout + v.nout, iv, sizeof(iv));
+        hout[v.nout + 1] = q.options->sigma;
+        up = v.nin + v.nout + 2;
+    }
     double *d = v.dmem;
-    hipError_t e = hipMemcpyAsync(d + v.oin, hin, sizeof(double) * (size_t)v.nin, hipMemcpyHostToDevice, v.stream);
+    hipError_t e = hipMemcpyAsync(d + v.oin, hin, sizeof(double) * (size_t)up, hipMemcpyHostToDevice, v.stream);
+    int rc = e == hipSuccess ? QPB_OK : qpb::set_error(QPB_EHIP, "QP_SOLVE: upload failed");
     qpb::CopySegs sc{};
     long po = v.oin;
     auto scatter = [&](long dst, long k) {
         if (k <= 0) return;
+        if (sc.nseg >= qpb::CopySegs::kMax) { sc.nseg = qpb::CopySegs::kMax + 1; return; }   // refused below
         sc.seg[sc.nseg++] = {d + po, d + dst, k, 1, 64};
         po += k;
     };
@@ -515,22 +571,25 @@ int solve_on_device(Priv &v, QP &q) {
     scatter(v.oc, n);
     scatter(v.oh, m);
     scatter(v.ob, p);
-    if (e == hipSuccess) rc = qpb::strided_copy(sc, v.stream);
-    else rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: upload failed");
-    qpb_settings st;
-    st.maxit = q.options->maxit;
-    st.reltol = q.options->reltol;
-    st.abstol = q.options->abstol;
-    st.sigma_d = q.sigma_d;
+    if (cs.warm) {
+        po = v.oout;
+        scatter(v.ox, n);
+        scatter(v.oy, p);
+        scatter(v.oz, m);
+        scatter(v.os, m);
+    }
+    if (!rc) rc = qpb::strided_copy(sc, v.stream);
     int *fl = reinterpret_cast<int *>(d + v.oout + v.nout);
+    double *sg = d + v.oout + v.nout + 1;
     if (!rc)
-        rc = qpb_solve(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
-                       p > 0 ? d + v.ob : nullptr, &st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz, d + v.os,
-                       fl, fl + 1, d + v.ofv, d + v.ost, v.stream);
+        rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
+                           p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz,
+                           d + v.os, fl, fl + 1, d + v.ofv, d + v.ost, nullptr, v.stream, sg, cs.warm);
     qpb::CopySegs gc{};
     long qo = v.oout;
     auto gather = [&](long src, long k, long ss) {
         if (k <= 0) return;
+        if (gc.nseg >= qpb::CopySegs::kMax) { gc.nseg = qpb::CopySegs::kMax + 1; return; }   // refused below
         gc.seg[gc.nseg++] = {d + src, d + qo, k, ss, 1};
         qo += k;
     };
@@ -540,27 +599,54 @@ int solve_on_device(Priv &v, QP &q) {
     gather(v.os, m, 64);
     gather(v.ost, 6, 64);
     if (!rc) rc = qpb::strided_copy(gc, v.stream);
-    if (!rc && hipMemcpyAsync(hout, d + v.oout, sizeof(double) * (size_t)(v.nout + 1), hipMemcpyDeviceToHost,
+    if (!rc && hipMemcpyAsync(hout, d + v.oout, sizeof(double) * (size_t)(v.nout + 2), hipMemcpyDeviceToHost,
                               v.stream) != hipSuccess)
         rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: download failed");
     if (hipStreamSynchronize(v.stream) != hipSuccess && !rc) rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: kernel failed");
-    if (cur != v.dev && cur >= 0) (void)hipSetDevice(cur);
     if (rc) return rc;
     const double *r = hout;
-    std::memcpy(q.x, r, sizeof(double) * (size_t)n); r += n;
-    if (p > 0) { std::memcpy(q.y, r, sizeof(double) * (size_t)p); r += p; }
-    std::memcpy(q.z, r, sizeof(double) * (size_t)m); r += m;
-    std::memcpy(q.s, r, sizeof(double) * (size_t)m); r += m;
-    v.st.n_rx = r[0]; v.st.n_ry = r[1]; v.st.n_rz = r[2]; v.st.n_mu = r[3];
-    v.st.alpha_p = r[4]; v.st.alpha_d = r[5];
-    r += 6;
-    v.st.fval = r[0];
     int iv[2];
     std::memcpy(iv, hout + v.nout, sizeof(iv));
-    v.st.Flag = iv[0];
-    v.st.IterationCount = iv[1];
-    mirror_kkt(v, q);
+    take_results(v, q, r, r + n, r + n + p, r + n + p + m, r + n + p + 2 * m, hout[v.nout - 1], iv, hout[v.nout + 1],
+                 cs.st.maxit, setup_init);
     return QPB_OK;
+}
+
+// One launch for this QP: QP_SETUP's kkt_initialize (setup_init: maxit = 0,
+// cold) or a QP_SOLVE (warm once the initial point is in the object).
+int solve_on_device(Priv &v, QP &q, bool setup_init) {
+    int rc = ensure_device(v, q);
+    if (rc) return rc;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (cur != v.dev) (void)hipSetDevice(v.dev);
+    CallState cs = call_state(v, q, setup_init ? 0 : q.options->maxit);
+    if (setup_init) cs.warm = false;
+    rc = zero_copy(v) ? solve_zero_copy(v, q, cs, setup_init) : solve_staged(v, q, cs, setup_init);
+    if (cur != v.dev && cur >= 0) (void)hipSetDevice(cur);
+    if (rc) return rc;
+    if (setup_init) v.inited = true;
+    else {
+        v.inited = true;            // the object now holds an iterate to continue from
+        mirror_kkt(v, q);
+    }
+    return QPB_OK;
+}
+
+// QP_SETUP's kkt_initialize (qpSWIFT.c:447): the initial point in x, y, z, s
+// when setup returns, computed on the device (maxit = 0 launch).  Skipped without
+// a GPU or with QPSWIFT_HIP_SETUP_INIT=0 (the first QP_SOLVE is then a cold solve,
+// one launch per tick instead of two; x, y, z, s stay zero until it).
+QP *setup_init(QP *q, clk::time_point t0) {
+    if (!q) return q;
+    Priv &v = *handle_of(q)->priv;
+    const char *e = std::getenv("QPSWIFT_HIP_SETUP_INIT");
+    int ndev = 0;
+    if (v.plan && !(e && e[0] == '0') && hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) {
+        if (solve_on_device(v, *q, true) != QPB_OK) v.err = qpb_last_error();
+    }
+    v.st.tsetup = seconds_since(t0);
+    return q;
 }
 
 void release(QP *q) {
@@ -596,7 +682,7 @@ QP *QP_SETUP(qp_int n, qp_int m, qp_int p, qp_int *Pjc, qp_int *Pir, qp_real *Pp
     q.c = c;
     q.h = h;
     q.sigma_d = sigma_d;
-    return finish_setup(hd, Permut, t0);
+    return setup_init(finish_setup(hd, Permut, t0), t0);
 }
 
 QP *QP_SETUP_dense(qp_int n, qp_int m, qp_int p, qp_real *Ppr, qp_real *Apr, qp_real *Gpr, qp_real *c,
@@ -624,7 +710,7 @@ QP *QP_SETUP_dense(qp_int n, qp_int m, qp_int p, qp_real *Ppr, qp_real *Apr, qp_
     q.c = c;
     q.h = h;
     q.sigma_d = 0.0;   // qpSWIFT.c:334
-    return finish_setup(hd, Permut, t0);
+    return setup_init(finish_setup(hd, Permut, t0), t0);
 }
 
 qp_int QP_SOLVE(QP *myQP) {
@@ -635,7 +721,7 @@ qp_int QP_SOLVE(QP *myQP) {
     if (!v.plan) {
         rc = qpb::set_error(QPB_ECOMPILE, ("QP_SOLVE: no kernel for this QP: " + v.err).c_str());
     } else {
-        rc = solve_on_device(v, *myQP);
+        rc = solve_on_device(v, *myQP, false);
     }
     if (rc) v.st.Flag = QP_FATAL;
     v.st.tsolve = seconds_since(t0);

@@ -83,3 +83,43 @@ def setup_dense(n, m, p, P, A, G, c, h, b, perm=None, ordering=COLUMN_MAJOR_ORDE
     P, A, G, c, h, b, perm = keep
     qp = L.QP_SETUP_dense(n, m, p, dptr(P), dptr(A), dptr(G), dptr(c), dptr(h), dptr(b), lptr(perm), ordering)
     return qp, keep
+
+
+def state(qp, n, m):
+    """The QP object's state as the caller sees it: x, y, z, s, stats and
+    options->sigma (what a further QP_SOLVE continues from, qpSWIFT.c:502-596)."""
+    L = _lib.lib()
+    q = qp.contents
+    st, o = q.stats.contents, q.options.contents
+    return dict(x=np.ctypeslib.as_array(q.x, (n,)).copy(),
+                y=np.ctypeslib.as_array(q.y, (q.p,)).copy() if q.p else np.zeros(0),
+                z=np.ctypeslib.as_array(q.z, (m,)).copy(), s=np.ctypeslib.as_array(q.s, (m,)).copy(),
+                flag=int(st.Flag), iters=int(st.IterationCount), fval=float(st.fval), sigma=float(o.sigma),
+                n_rx=st.n_rx, n_ry=st.n_ry, n_rz=st.n_rz, n_mu=st.n_mu,
+                error=L.qpb_last_error().decode(errors="replace") if st.Flag == 3 else "")
+
+
+def solve_again(qp, n, m, reltol=None, abstol=None, maxit=None):
+    """Options override -> QP_SOLVE on an existing QP object -> its state."""
+    o = qp.contents.options.contents
+    if reltol is not None:
+        o.reltol = reltol
+    if abstol is not None:
+        o.abstol = abstol
+    if maxit is not None:
+        o.maxit = maxit
+    rc = int(_lib.lib().QP_SOLVE(qp))
+    out = state(qp, n, m)
+    out["rc"] = rc
+    return out
+
+
+def setup_csc(n, m, p, Pjc, Pir, Ppr, Ajc, Air, Apr, Gjc, Gir, Gpr, c, h, b, sigma_d=0.0, perm=None):
+    """QP_SETUP only; returns (QP pointer, keep-alive arrays: CSC and c, h, b are
+    borrowed by the QP, qpSWIFT.c:60-234)."""
+    L = _lib.lib()
+    keep = [_i64(a) for a in (Pjc, Pir, Ajc, Air, Gjc, Gir, perm)] + [_f64(a) for a in (Ppr, Apr, Gpr, c, h, b)]
+    Pjc, Pir, Ajc, Air, Gjc, Gir, perm, Ppr, Apr, Gpr, c, h, b = keep
+    qp = L.QP_SETUP(n, m, p, lptr(Pjc), lptr(Pir), dptr(Ppr), lptr(Ajc), lptr(Air), dptr(Apr),
+                    lptr(Gjc), lptr(Gir), dptr(Gpr), dptr(c), dptr(h), dptr(b), sigma_d, lptr(perm))
+    return qp, keep

@@ -149,6 +149,24 @@ int  qpb_solve_best(qpb_plan *plan, long B,
                     int *flag, int *iters, double *fval, double *stats,
                     double *best, void *stream);
 
+/* Warm solve: QP_SOLVE called again on the same QP objects.  The reference's
+ * QP_SOLVE (qpSWIFT.c:473-644) never re-initialises: it continues from the
+ * object's x, y, z, s, stats->IterationCount and options->sigma, runs at most
+ * maxit further iterations, and sets QP_MAXIT only when IterationCount reaches
+ * exactly maxit (:598-601), otherwise leaving stats->Flag as it was.  Here every
+ * QP q continues from x, y, z, s, iters[q] and flag[q] as they are in the (in/out)
+ * arrays and from sigma[q] (DEVICE, [B]; in/out: receives the last sigma).  A cold
+ * qpb_solve with maxit = 0 leaves kkt_initialize's point in x, y, z, s (what
+ * QP_SETUP leaves in the QP, qpSWIFT.c:447); warm solves from there with
+ * iters = 0, flag = QP_FATAL and sigma = 100 reproduce a cold solve. */
+int  qpb_solve_warm(qpb_plan *plan, long B,
+                    const double *P, const double *A, const double *G,
+                    const double *c, const double *h, const double *b,
+                    const qpb_settings *st,
+                    double *x, double *y, double *z, double *s,
+                    int *flag, int *iters, double *fval, double *stats,
+                    double *sigma, void *stream);
+
 /* Lowest-fval optimal QP of a batch (device-side reduction): writes
  * {fval, index} of the minimum over q with flag[q] == 0 (ties -> lowest index;
  * none -> {+inf, -1}) to out2 (device, 2 doubles; the index as a double). */
@@ -212,6 +230,13 @@ typedef struct qpb_apf_state {
 } qpb_apf_state;
 int  qpb_apf_wrench(long K, const qpb_apf_state *st, const double *targets, double *wrench,
                     double *com_des, void *stream);
+/* The robustness state of one gait step, as the controller derives it before the
+ * fields (main.cpp:1273-1321): every foot's index is smoothed,
+ * rob_foot = 0.35 rob_foot + 0.65 h_prev / period_st (h_prev: the step's
+ * accumulated 1 / foot height of BR, BL, FL, FR; period_st: the step's duration),
+ * and fake_crawl = (mean of the four < 0.34).  Updates st in place (host, no GPU);
+ * the mean (robf_to_mean) goes to *robf_mean when not NULL. */
+int  qpb_apf_update(qpb_apf_state *st, const double h_prev[4], double period_st, double *robf_mean);
 
 /* ---- the multi-GPU argmin gather: RCCL over xGMI ----
  * One process per GPU, each solving its own shard (no data-path collective).

@@ -17,6 +17,17 @@ def _fr(v):
     return 0.0 if abs(v) < 0.07 else abs(v)
 
 
+def apf_update(s: dict, h_prev, period_st: float) -> float:
+    """main.cpp:1273-1276 (rob_foot = 0.35 rob_foot + 0.65 h_prev / period_st per
+    foot) and :1307-1321 (robf_to_mean = (bl + fr + br + fl) / 4; fake_crawl when it
+    is below 0.34), on s in place (order BR, BL, FL, FR).  Returns robf_to_mean."""
+    rf = [0.35 * float(s["rob_foot"][i]) + 0.65 * float(h_prev[i]) / period_st for i in range(4)]
+    s["rob_foot"] = np.asarray(rf)
+    mean = (rf[1] + rf[3] + rf[0] + rf[2]) / 4.0
+    s["fake_crawl"] = bool(mean < 0.34)
+    return mean
+
+
 def apf_wrench(s: dict, targets: np.ndarray):
     """s: the fields of qpb_apf_state (numpy); targets [K, 2] -> wrench [K, 6], com_des [K, 6]."""
     K = targets.shape[0]
@@ -62,7 +73,22 @@ def apf_wrench(s: dict, targets: np.ndarray):
 
 def sample_state(seed: int = 7, rep_field=True, min_exit=False, fake_crawl=False):
     """A plausible tick: nominal stance feet around the CoM with jitter, small CoM
-    motion, robustness indices, the controller's nominal versors (main.cpp:440-458)."""
+    motion, the controller's nominal versors (main.cpp:440-458), and robustness
+    indices as the controller derives them (apf_update: the previous step's smoothed
+    indices and this step's accumulated 1/h over a 0.4 s step), so that fake_crawl
+    is what main.cpp:1320 sets -- the state is drawn until it matches the requested
+    fake_crawl."""
+    for k in range(1000):
+        s = _sample_state(seed + 7919 * k, rep_field, min_exit)
+        prev = np.random.default_rng(seed + 7919 * k + 1)
+        s["rob_foot"] = prev.uniform(0.0, 0.6, 4)
+        apf_update(s, prev.uniform(0.0, 0.25, 4), 0.4)
+        if s["fake_crawl"] == bool(fake_crawl):
+            return s
+    raise RuntimeError("no state with the requested fake_crawl")
+
+
+def _sample_state(seed, rep_field, min_exit):
     rng = np.random.default_rng(seed)
     com = np.array([0.1, -0.05, 0.39, 0.01, -0.02, 0.03]) + rng.uniform(-0.01, 0.01, 6)
     ee = com[None, :2] + FOOT_OFF + rng.uniform(-0.03, 0.03, (4, 2))
@@ -77,4 +103,4 @@ def sample_state(seed: int = 7, rep_field=True, min_exit=False, fake_crawl=False
     return dict(ee=ee, com=com, com_vel=rng.uniform(-0.1, 0.1, 6), acc_des=rng.uniform(-0.5, 0.5, 6),
                 des_orient=np.array([0.0, 0.0]), rob_foot=rng.uniform(0.0, 0.5, 4), versor=versor,
                 lat_versor=np.array([1.0, 0.0]), R_wb=R, Mcom=M, mass=21.261, rep_field=rep_field,
-                min_exit=min_exit, fake_crawl=fake_crawl)
+                min_exit=min_exit, fake_crawl=False)

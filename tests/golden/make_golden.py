@@ -90,6 +90,9 @@ def main(only=None):
     if only == "edge_infeasible":
         infeasible_case(ref)
         return
+    if only == "resolve":
+        resolve_cases(ref)
+        return
     # C1: 12-var / 20-ineq / 6-eq contact-force QP (configs 1, 2, 5).
     ids = np.arange(64)
     d = W.contact_force_qp(SEED_BASE + 1, ids)
@@ -125,6 +128,97 @@ def main(only=None):
     c30_cases(ref)
     c30_swing_cases(ref)
     infeasible_case(ref)
+    resolve_cases(ref)
+
+
+def _state(lib, qp, n, m):
+    """The QP object's state as a caller sees it: x, y, z, s, stats, options->sigma."""
+    q = qp.contents
+    st, o = q.stats.contents, q.options.contents
+    return dict(x=np.ctypeslib.as_array(q.x, (n,)).copy(),
+                y=np.ctypeslib.as_array(q.y, (q.p,)).copy() if q.p else np.zeros(0),
+                z=np.ctypeslib.as_array(q.z, (m,)).copy(), s=np.ctypeslib.as_array(q.s, (m,)).copy(),
+                flag=int(st.Flag), iters=int(st.IterationCount), fval=float(st.fval), sigma=float(o.sigma),
+                n_rx=st.n_rx, n_ry=st.n_ry, n_rz=st.n_rz, n_mu=st.n_mu)
+
+
+def resolve_sequence(ref, setup, n, m, calls, dense=True):
+    """One QP object: setup, then QP_SOLVE once per (reltol = abstol, maxit) in
+    `calls`, the options changed in between -- qpSWIFT's QP_SOLVE continues from
+    the object's iterate, IterationCount and options->sigma (qpSWIFT.c:502-596).
+    Returns the state after setup and after every call."""
+    L = ref.lib
+    qp = setup()
+    states = [_state(L, qp, n, m)]
+    for tol, maxit in calls:
+        o = qp.contents.options.contents
+        o.reltol = tol
+        o.abstol = tol
+        o.maxit = maxit
+        rc = int(L.QP_SOLVE(qp))
+        stt = _state(L, qp, n, m)
+        assert rc == stt["flag"]
+        states.append(stt)
+    N = n + m + qp.contents.p
+    perm = np.ctypeslib.as_array(qp.contents.kkt.contents.P, (N,)).copy()
+    (L.QP_CLEANUP_dense if dense else L.QP_CLEANUP)(qp)
+    return states, perm
+
+
+def resolve_cases(ref):
+    """QP_SOLVE called repeatedly on one QP object (qpSWIFT.c:502-596 never
+    re-initialises; QP_SETUP leaves kkt_initialize's point in x, s, z, :447):
+    state after setup and after each call of a sequence of (tol, maxit) calls --
+    the controller's tol 1e-2 solve then tightened to 1e-6, the same tol again (no
+    iteration), maxit-truncated calls whose IterationCount passes maxit (the
+    :598-601 QP_MAXIT rule), and sigma_d = 0.05 (QP_SETUP, options->sigma carried)."""
+    from apf_quadruped_amd.qpswift_abi import dptr, lptr
+
+    def dense_seq(name, d, ids, calls, seed):
+        n, m, p = d["n"], d["m"], d["p"]
+        P, A, G = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+        per = []
+        for q in range(len(ids)):
+            keep = [np.ascontiguousarray(a, dtype=np.float64) for a in (P[q], A[q], G[q], d["c"][q], d["h"][q],
+                                                                        d["b"][q])]
+            setup = lambda k=keep: ref.lib.QP_SETUP_dense(n, m, p, *[dptr(a) for a in k], lptr(None), 30)
+            per.append(resolve_sequence(ref, setup, n, m, calls))
+        out = dict(n=n, m=m, p=p, ordering=30, calls=np.asarray(calls, dtype=np.float64), qp_ids=np.asarray(ids),
+                   P=P, A=A, G=G, c=d["c"], h=d["h"], b=d["b"], perm=np.asarray([pp for _, pp in per]))
+        for k in per[0][0][0]:
+            out["st_" + k] = np.asarray([[stt[k] for stt in sts] for sts, _ in per])
+        save(name, seed=seed, **out)
+
+    ids = np.arange(16)
+    d = W.contact_force_qp(SEED_BASE + 1, ids)
+    dense_seq("resolve_c1", d, ids, [(1e-2, 100), (1e-6, 100), (1e-6, 100)], SEED_BASE + 1)
+    dense_seq("resolve_c1_maxit", {k: (v[:8] if hasattr(v, "shape") else v) for k, v in d.items()}, ids[:8],
+              [(1e-6, 0), (1e-6, 2), (1e-6, 2), (1e-6, 3), (1e-6, 100)], SEED_BASE + 1)
+    ids4 = np.arange(4)
+    dc = W.controller_qp(SEED_BASE + 30, ids4)
+    dense_seq("resolve_c30", dc, ids4, [(1e-2, 100), (1e-6, 100)], SEED_BASE + 30)
+    # QP_SETUP (CSC) with sigma_d = 0.05: the options->sigma carried between calls
+    # decides the sigma > sigma_d branch (qpSWIFT.c:540) of the next call
+    ids8 = np.arange(8)
+    d7 = W.contact_force_qp(SEED_BASE + 7, ids8)
+    per, rows = [], []
+    for q in range(8):
+        Pjc, Pir, Ppr = to_csc(d7["P"][q]); Ajc, Air, Apr = to_csc(d7["A"][q]); Gjc, Gir, Gpr = to_csc(d7["G"][q])
+        keep = [Pjc, Pir, Ppr, Ajc, Air, Apr, Gjc, Gir, Gpr] + \
+            [np.ascontiguousarray(d7[k][q], dtype=np.float64) for k in ("c", "h", "b")]
+        setup = lambda k=keep: ref.lib.QP_SETUP(12, 20, 6, lptr(k[0]), lptr(k[1]), dptr(k[2]), lptr(k[3]),
+                                                lptr(k[4]), dptr(k[5]), lptr(k[6]), lptr(k[7]), dptr(k[8]),
+                                                dptr(k[9]), dptr(k[10]), dptr(k[11]), 0.05, lptr(None))
+        per.append(resolve_sequence(ref, setup, 12, 20, [(1e-2, 100), (1e-6, 100), (1e-8, 100)], dense=False))
+        rows.append(keep)
+    out = dict(n=12, m=20, p=6, sigma_d=0.05, calls=np.asarray([(1e-2, 100), (1e-6, 100), (1e-8, 100)]),
+               Pjc=rows[0][0], Pir=rows[0][1], Ajc=rows[0][3], Air=rows[0][4], Gjc=rows[0][6], Gir=rows[0][7],
+               Ppr=np.stack([r[2] for r in rows]), Apr=np.stack([r[5] for r in rows]),
+               Gpr=np.stack([r[8] for r in rows]), c=d7["c"], h=d7["h"], b=d7["b"],
+               perm=np.asarray([pp for _, pp in per]))
+    for k in per[0][0][0]:
+        out["st_" + k] = np.asarray([[stt[k] for stt in sts] for sts, _ in per])
+    save("resolve_csc_sigma0.05", seed=SEED_BASE + 7, **out)
 
 
 def infeasible_case(ref):

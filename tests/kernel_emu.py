@@ -47,7 +47,8 @@ class QpbArgs(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("P", "A", "G", "c", "h", "b", "x", "y", "z", "s", "flag", "iters",
                                           "fval", "stats")] + \
                [("B", C.c_long), ("tol", C.c_double), ("abstol", C.c_double), ("sigma_d", C.c_double),
-                ("maxit", C.c_long)]
+                ("maxit", C.c_long)] + [(n, C.c_void_p) for n in ("tab", "best", "part", "ctr", "sig")] + \
+               [("warm", C.c_long)]
 
 
 def build_emulator(src: str, exact: bool, cache_dir=None):
@@ -71,20 +72,26 @@ def build_emulator(src: str, exact: bool, cache_dir=None):
     return lib, wg
 
 
-def emulate(plan, vals, B, reltol=1e-6, abstol=1e-6, maxit=100, sigma_d=0.0):
-    """Run plan's generated kernel on the CPU for B QPs (tiled numpy inputs)."""
+def emulate(plan, vals, B, reltol=1e-6, abstol=1e-6, maxit=100, sigma_d=0.0, warm=None):
+    """Run plan's generated kernel on the CPU for B QPs (tiled numpy inputs).
+    warm = the `out` dict of a previous call plus "sigma" ([B]): a warm solve
+    (qpb_solve_warm) continuing from it, updated in place and returned."""
     from apf_quadruped_amd.batch import TILE, ntiles
     lib, wg = build_emulator(plan.source(), plan.exact)
     T = ntiles(B) * TILE
     keep = {k: np.ascontiguousarray(v, dtype=np.float64) for k, v in vals.items()}
-    out = dict(x=np.zeros(plan.n * T), y=np.zeros(max(plan.p, 1) * T), z=np.zeros(plan.m * T),
-               s=np.zeros(plan.m * T), flag=np.zeros(B, np.int32), iters=np.zeros(B, np.int32),
-               fval=np.zeros(B), stats=np.zeros(6 * T))
+    out = warm if warm is not None else \
+        dict(x=np.zeros(plan.n * T), y=np.zeros(max(plan.p, 1) * T), z=np.zeros(plan.m * T),
+             s=np.zeros(plan.m * T), flag=np.zeros(B, np.int32), iters=np.zeros(B, np.int32),
+             fval=np.zeros(B), stats=np.zeros(6 * T))
     a = QpbArgs()
     for k in ("P", "A", "G", "c", "h", "b"):
         setattr(a, k, keep[k].ctypes.data if k in keep else None)
-    for k in out:
+    for k in ("x", "y", "z", "s", "flag", "iters", "fval", "stats"):
         setattr(a, k, out[k].ctypes.data)
+    if warm is not None:
+        a.sig = warm["sigma"].ctypes.data
+        a.warm = 1
     a.B, a.tol, a.abstol, a.sigma_d, a.maxit = B, reltol / np.sqrt(3.0), abstol, sigma_d, maxit
     lib.qpb_emu_run(a, wg, B)
     return out

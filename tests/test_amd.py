@@ -28,7 +28,7 @@ from apf_quadruped_amd.batch import Plan
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libqpswift_ref.so")
 LP = C.POINTER(C.c_long)
 DENSE = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, "*.npz"))
-               if not os.path.basename(f).startswith("csc_"))
+               if "csc_" not in os.path.basename(f))
 
 
 def amd(n, jc, ir):

@@ -156,3 +156,29 @@ def test_apf_candidates_end_to_end(oracle):
     # the winner is the oracle's (up to rounding-level near-ties between candidates)
     assert abs(fv[int(b[1])] - fv.min()) <= 1e-9 * max(1.0, abs(fv.min()))
     assert abs(b[0] - fv.min()) <= 1e-9 * max(1.0, abs(fv.min()))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5])
+def test_apf_update_matches_restatement(seed):
+    """qpb_apf_update (host C, no GPU): the step's robustness smoothing and the
+    fake_crawl decision (main.cpp:1273-1276, 1307-1321) equal the restatement in
+    tests/apf_ref.py bit for bit, over successive steps of one robot; both sides of
+    the 0.34 threshold occur."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import apf_ref
+    from apf_quadruped_amd.batch import apf_state, apf_update
+    rng = np.random.default_rng(seed)
+    s = apf_ref.sample_state(seed)
+    st = apf_state(**s)
+    seen = set()
+    for step in range(40):
+        h = rng.uniform(0.0, 0.3, 4)
+        period = rng.uniform(0.2, 0.6)
+        m_ref = apf_ref.apf_update(s, h, period)
+        m = apf_update(st, h, period)
+        assert m == m_ref
+        assert list(st.rob_foot) == list(s["rob_foot"])
+        assert bool(st.fake_crawl) == s["fake_crawl"]
+        seen.add(s["fake_crawl"])
+    assert seen == {True, False}

@@ -249,20 +249,89 @@ def test_dropin_controller_call_null_permut(name):
             assert np.abs(r[k] - g[k][q]).max() <= 1e-6 * scale, (name, q, k)
 
 
+RESOLVE = ["resolve_c1", "resolve_c1_maxit", "resolve_csc_sigma0.05"]
+
+
+def _resolve_setup(g, q, perm):
+    n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
+    if "Pjc" in g:
+        return dropin.setup_csc(n, m, p, g["Pjc"], g["Pir"], g["Ppr"][q], g["Ajc"], g["Air"], g["Apr"][q], g["Gjc"],
+                                g["Gir"], g["Gpr"][q], g["c"][q], g["h"][q], g["b"][q], sigma_d=float(g["sigma_d"]),
+                                perm=perm)
+    return dropin.setup_dense(n, m, p, g["P"][q], g["A"][q], g["G"][q], g["c"][q], g["h"][q], g["b"][q], perm=perm,
+                              ordering=int(g["ordering"]))
+
+
+def _check_state(got, g, q, k, exact, what):
+    """State after call k (0 = after setup) vs the reference's."""
+    assert got["flag"] == int(g["st_flag"][q, k]), (what, got["flag"], got.get("error"))
+    assert got["iters"] == int(g["st_iters"][q, k]), (what, got["iters"])
+    keys = ("x", "y", "z", "s") if int(g["p"]) else ("x", "z", "s")
+    if exact:
+        for key in keys:
+            np.testing.assert_array_equal(got[key], g["st_" + key][q, k], err_msg=f"{what}.{key}")
+        assert got["sigma"] == float(g["st_sigma"][q, k]), what
+        if k > 0 and g["calls"][k - 1][1] > 0:
+            assert got["fval"] == float(g["st_fval"][q, k]), what
+    else:
+        for key in keys:
+            ref = g["st_" + key][q, k]
+            assert np.abs(got[key] - ref).max() <= 1e-6 * max(1.0, float(np.abs(ref).max())), (what, key)
+
+
 @pytest.mark.gpu
-def test_dropin_reuses_qp_and_plan_cache(exact_mode):
-    """Solving the same QP object twice and many QPs of one pattern (plan cache)."""
+@pytest.mark.parametrize("name", RESOLVE)
+@pytest.mark.parametrize("null_perm", [False, True])
+@pytest.mark.parametrize("exact", [True, False])
+def test_dropin_resolve_sequence_matches_reference(name, null_perm, exact, monkeypatch):
+    """QP_SOLVE called again on one QP object continues from its x, y, z, s,
+    IterationCount and options->sigma (qpSWIFT.c:502-596), after QP_SETUP left
+    kkt_initialize's point in x, y, z, s (:447): the state after setup and after
+    every call of the reference's own sequences (tol 1e-2 then 1e-6 then 1e-6
+    again; maxit 0 / 2 / 2 / 3 / 100 -- QP_MAXIT only when IterationCount ==
+    maxit, :598-601; sigma_d = 0.05 with sigma carried) -- bit-identical under
+    QPSWIFT_HIP_EXACT=1, within 1e-6 with equal flags / counts otherwise."""
+    if exact:
+        monkeypatch.setenv("QPSWIFT_HIP_EXACT", "1")
+    g = golden(name)
+    n, m = int(g["n"]), int(g["m"])
+    for q in range(0, g["st_x"].shape[0], 3):
+        qp, keep = _resolve_setup(g, q, None if null_perm else g["perm"][q])
+        try:
+            st = dropin.state(qp, n, m)
+            _check_state(st, g, q, 0, exact, f"{name}[{q}] setup")
+            for k, (tol, maxit) in enumerate(g["calls"], start=1):
+                st = dropin.solve_again(qp, n, m, reltol=float(tol), abstol=float(tol), maxit=int(maxit))
+                assert st["rc"] == st["flag"]
+                _check_state(st, g, q, k, exact, f"{name}[{q}] call {k}")
+        finally:
+            (_lib.lib().QP_CLEANUP if "Pjc" in g else _lib.lib().QP_CLEANUP_dense)(qp)
+
+
+@pytest.mark.gpu
+def test_dropin_resolve_controller_shape():
+    """The controller's 30/68/18 QP (Permut = NULL): tol 1e-2 then tightened to
+    1e-6 on the same object -- flags and the cumulative IterationCount equal the
+    reference's, x, y, z, s within 1e-6 after each call."""
+    g = golden("resolve_c30")
+    n, m = int(g["n"]), int(g["m"])
+    for q in range(g["st_x"].shape[0]):
+        qp, keep = _resolve_setup(g, q, None)
+        try:
+            _check_state(dropin.state(qp, n, m), g, q, 0, False, f"c30[{q}] setup")
+            for k, (tol, maxit) in enumerate(g["calls"], start=1):
+                st = dropin.solve_again(qp, n, m, reltol=float(tol), abstol=float(tol), maxit=int(maxit))
+                _check_state(st, g, q, k, False, f"c30[{q}] call {k}")
+        finally:
+            _lib.lib().QP_CLEANUP_dense(qp)
+
+
+@pytest.mark.gpu
+def test_dropin_plan_cache_makes_setup_a_lookup(exact_mode):
+    """Many QPs of one pattern: after the first setup no ordering / JIT runs."""
     g = golden("c1_tol1e-6")
-    L = _lib.lib()
-    qp, keep = dropin.setup_dense(*_golden_dense_args(g, 3), perm=g["perm"][3])
-    f1 = L.QP_SOLVE(qp)
-    x1 = np.ctypeslib.as_array(qp.contents.x, (12,)).copy()
-    f2 = L.QP_SOLVE(qp)
-    x2 = np.ctypeslib.as_array(qp.contents.x, (12,)).copy()
-    L.QP_CLEANUP_dense(qp)
-    assert f1 == f2 == 0 and np.array_equal(x1, x2) and np.array_equal(x1, g["x"][3])
     t = [dropin.solve_dense(*_golden_dense_args(g, q), perm=g["perm"][q])["tsetup"] for q in range(8)]
-    assert max(t[1:]) < 0.05   # cached plan: no ordering / JIT after the first setup
+    assert max(t[1:]) < 0.05
 
 
 @pytest.mark.gpu

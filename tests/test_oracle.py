@@ -12,8 +12,10 @@ import pytest
 
 from conftest import GOLDEN, golden
 
+# resolve_*: QP_SOLVE sequences on one QP object (tests/test_dropin.py,
+# tests/test_codegen_emu.py); the oracle solves one call per QP
 DENSE = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-               if not os.path.basename(p).startswith("csc_"))
+               if not os.path.basename(p).startswith(("csc_", "resolve_")))
 SPARSE = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "csc_*.npz")))
 
 
