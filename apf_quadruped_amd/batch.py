@@ -187,8 +187,13 @@ class Plan:
         L.qpb_plan_tree_tables(self._h, buf, size)
         return buf.raw[:size]
 
-    def compile(self) -> None:
-        check(_lib.lib().qpb_plan_compile(self._h), "qpb_plan_compile")
+    def compile(self, warm: bool = False, B: int = 1) -> None:
+        """Compile (or fetch from the code-object cache) the plan's kernels; warm:
+        the warm-solve variant qpb_solve_warm launches for a batch of B."""
+        if warm:
+            check(_lib.lib().qpb_plan_compile_warm(self._h, int(B)), "qpb_plan_compile_warm")
+        else:
+            check(_lib.lib().qpb_plan_compile(self._h), "qpb_plan_compile")
 
     @property
     def nnz(self):

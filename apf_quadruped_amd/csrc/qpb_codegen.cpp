@@ -408,6 +408,7 @@ struct Gen {
           << ": n=" << n << " m=" << m << " p=" << p << " N=" << N << " nnz(L)=" << pl.lnz
           << (opt.exact ? " [exact]" : " [fast]") << "\n";
         o << "#pragma clang fp contract(" << (opt.exact ? "off" : "fast") << ")\n";
+        o << "#ifndef QPB_WARM\n#define QPB_WARM 0   // 1: the warm-solve variant (qpb_solve_warm)\n#endif\n";
         o << "struct qpb_args {\n"
              "  const double *P, *A, *G, *c, *h, *b;\n"
              "  double *x, *y, *z, *s;\n"
@@ -480,7 +481,7 @@ struct Gen {
         // ---- kkt_initialize (Auxilary.c:992-1089); a warm solve (QP_SOLVE called
         // again, qpSWIFT.c:502-596) instead continues from the output arrays
         ln("long it0 = 0; int flag0 = 3; double sigma = 100.0;");
-        open("if (a.warm) {");
+        open("if (QPB_WARM) {   // the warm-solve variant (qpb_solve_warm)");
         begin_phase(false, false);
         auto warm_load = [&](const char *arr, long nv) {
             for (long i = 0; i < nv; i++)
@@ -748,7 +749,7 @@ struct Gen {
         store("z", m, "z");
         store("s", m, "s");
         ln("a.flag[q] = flag; a.iters[q] = (int)(it0 + it); a.fval[q] = fval;");
-        ln("if (a.sig) a.sig[q] = sigma;");
+        ln("if (QPB_WARM) a.sig[q] = sigma;");
         ln("if (a.stats) { double *o = a.stats + tile * 384 + lane; o[0] = st_rx; o[64] = st_ry; o[128] = st_rz;"
            " o[192] = st_mu; o[256] = ap; o[320] = ad; }");
         o << "}\n";

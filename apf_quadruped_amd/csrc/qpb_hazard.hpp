@@ -1,0 +1,14 @@
+// qpb_hazard.hpp -- wait states for DPP inline asm (qpb_hazard.cpp).
+#pragma once
+
+#include <string>
+
+namespace qpb {
+// Pad every DPP instruction inside an inline-asm region of the assembly text s
+// (clang -S output) with the s_nop its VGPR / EXEC producers require on every
+// path into it.  Returns the number of padded sites; *report summarises.
+int asm_fixup(std::string &s, std::string *report);
+// Check a disassembled code object (llvm-objdump -d): 1 clean, 0 hazard found
+// (*report says where), -1 could not audit.
+int audit_disassembly(const std::string &dis, std::string *report);
+}  // namespace qpb

@@ -56,6 +56,9 @@ struct qpb_args {
 #ifndef QPB_R_ALIAS
 #define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
 #endif
+#ifndef QPB_WARM
+#define QPB_WARM 0        // 1: the warm-solve variant (qpb_solve_warm), compiled on demand
+#endif
 #ifndef QPB_R_TIMING
 #define QPB_R_TIMING 0    // 2: per-QP start / end (realtime, cycles), iterations, hardware ids into stats;
                           // 3: cycles per phase (H0 + setup solve, residuals, factor, predictor,
@@ -496,33 +499,37 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     // QP_SOLVE loop (qpSWIFT.c:502-602); the wave runs until all four rows stop
     double x = 0.0, y = 0.0, s0 = 1.0, s1 = 1.0, z0 = 1.0, z1 = 1.0;
     bool act = valid;
-    long itq = 0, it0 = 0;     // it0: IterationCount the QP enters with (warm solve)
-    int flag0 = 3;             // stats->Flag it enters with (QP_FATAL after setup)
+    long itq = 0;
     double st_rx2 = 0.0, st_ry2 = 0.0, st_rz2 = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0, fv = 0.0;
     const double tol2 = a.tol > 0.0 ? a.tol * a.tol : -1.0;
     double sigma = 100.0;      // options->sigma (SIGMA, GlobalOptions.h:49)
     long it = -1;
-    if (a.warm) {
-        // warm: QP_SOLVE continues from the object's iterate, IterationCount and
-        // options->sigma (qpSWIFT.c:502-596 never re-initialises); no setup pass
-        if (isx) x = a.x[tile * (NX * 64) + c * 64 + ql];
+#if QPB_WARM
+    // warm variant (qpb_solve_warm): QP_SOLVE continues from the object's iterate,
+    // IterationCount and options->sigma (qpSWIFT.c:502-596 never re-initialises)
+    if (isx) x = a.x[tile * (NX * 64) + c * 64 + ql];
 #if NY > 0
-        if (isy) y = a.y[tile * (NY * 64) + c * 64 + ql];
+    if (isy) y = a.y[tile * (NY * 64) + c * 64 + ql];
 #endif
-        if (isz0) { z0 = a.z[tile * (NZ * 64) + c * 64 + ql]; s0 = a.s[tile * (NZ * 64) + c * 64 + ql]; }
-        if (isz1) { z1 = a.z[tile * (NZ * 64) + (16 + c) * 64 + ql]; s1 = a.s[tile * (NZ * 64) + (16 + c) * 64 + ql]; }
-        it0 = a.iters[qc];
-        flag0 = a.flag[qc];
-        sigma = a.sig[qc];
-        it = 0;
-    }
-    int flag = flag0;
+    if (isz0) { z0 = a.z[tile * (NZ * 64) + c * 64 + ql]; s0 = a.s[tile * (NZ * 64) + c * 64 + ql]; }
+    if (isz1) { z1 = a.z[tile * (NZ * 64) + (16 + c) * 64 + ql]; s1 = a.s[tile * (NZ * 64) + (16 + c) * 64 + ql]; }
+    const long it0 = a.iters[qc];   // IterationCount the QP enters with
+    const int flag0 = a.flag[qc];   // stats->Flag it enters with (QP_FATAL after setup)
+    sigma = a.sig[qc];
+    it = 0;
     double sigf = sigma;       // options->sigma when this row's loop ends (a frozen row's own
                                // sigma keeps being recomputed while the rest of the wave runs)
+#define QPB_SIGF sigf = sigma
+#else
+    constexpr long it0 = 0;
+    constexpr int flag0 = 3;
+#define QPB_SIGF (void)0
+#endif
+    int flag = flag0;
     for (;;) {
         if (it >= 0 && it >= a.maxit) {
             // qpSWIFT.c:598-601: QP_MAXIT only when IterationCount == maxit
-            if (act) { itq = it0 + it; flag = itq == a.maxit ? 2 : flag0; sigf = sigma; }
+            if (act) { itq = it0 + it; flag = (!QPB_WARM || itq == a.maxit) ? 2 : flag0; QPB_SIGF; }
             break;
         }
         // updatekktmatrix (Auxilary.c:211-215): z diagonal -s/z (-I at setup, s = z = 1)
@@ -577,8 +584,8 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 st_mu = mu_it;
                 if (red[0] < tol2 && red[2] < tol2 && (NY == 0 || red[1] < tol2) && mu_it < a.abstol) {
                     itq = it0 + it;
-                    flag = itq == a.maxit ? 2 : 0;
-                    sigf = sigma;
+                    flag = (QPB_WARM && itq == a.maxit) ? 2 : 0;
+                    QPB_SIGF;
                     act = false;
                 }
             }
@@ -695,7 +702,9 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             a.flag[q] = flag;
             a.iters[q] = (int)itq;
             a.fval[q] = fr[0];
-            if (a.sig) a.sig[q] = sigf;
+#if QPB_WARM
+            a.sig[q] = sigf;
+#endif
 #if QPB_R_TIMING == 3
             QPB_TM(4);
             if (a.stats) {
@@ -733,4 +742,5 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_R_WPE) QPB_KERNEL_NAME(
 }
 #endif
 #undef QPB_TM
+#undef QPB_SIGF
 #endif  // QPB_ROW_COMMON_ONLY

@@ -26,6 +26,7 @@
 #include "../../include/qpswift_hip.h"
 #include "qpb_codegen.hpp"
 #include "qpb_plan.hpp"
+#include "qpb_hazard.hpp"
 #include "qpb_runtime.hpp"
 #include "qpb_tree.hpp"
 #include "qpb_wave.hpp"
@@ -282,27 +283,51 @@ static std::vector<std::string> compile_options(bool exact) {
     return o;
 }
 
+// Kernels with DPP inline asm are compiled through assembly: clang -S, then
+// qpb_hazard's asm_fixup pads every DPP instruction of an asm region with the
+// wait states its operands' producers require (qpb_hazard.cpp), then the text is
+// assembled and linked into the code object.  Others compile straight to it.
 static int compile_with_clang(const std::string &clang, const std::string &kname, const std::string &src,
-                              bool exact, std::vector<char> &code) {
+                              bool exact, std::vector<char> &code, std::string *fixup_report = nullptr) {
     std::string dir = getenv("TMPDIR") && *getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp";
     const std::string base = dir + "/qpb_" + kname + "_" + std::to_string((long)getpid()) + "_" +
                              std::to_string((unsigned long)std::hash<std::thread::id>()(std::this_thread::get_id()));
-    const std::string sp = base + ".hip", op = base + ".co";
+    const std::string sp = base + ".hip", op = base + ".co", ap = base + ".s", obp = base + ".o";
     {
         std::ofstream f(sp, std::ios::binary);
         if (!f) return fail(QPB_ECOMPILE, "cannot write " + sp);
         f << src;
     }
+    // QPB_NO_ASM_FIXUP=1: experiments only (A/B of the padding's cost); part of the cache key
+    const bool via_asm = src.find("_dpp ") != std::string::npos && !getenv("QPB_NO_ASM_FIXUP");
+    const std::string bindir = clang.substr(0, clang.rfind('/'));
     std::vector<std::string> argv = {clang, "-x", "hip", "--cuda-device-only", "--no-gpu-bundle-output",
                                      "-I" + clang.substr(0, clang.rfind("/lib/llvm/bin/")) + "/include",
                                      "-include", "hip/hip_runtime.h"};
     for (auto &o : compile_options(exact)) argv.push_back(o);
+    if (via_asm) argv.push_back("-S");
     argv.push_back("-o");
-    argv.push_back(op);
+    argv.push_back(via_asm ? ap : op);
     argv.push_back(sp);
     std::string log;
-    const int st = run_child(argv, &log);
+    int st = run_child(argv, &log);
     unlink(sp.c_str());
+    if (st == 0 && via_asm) {
+        std::vector<char> txt;
+        if (!read_file(ap, txt)) st = -1;
+        else {
+            std::string as(txt.begin(), txt.end());
+            std::string rep;
+            asm_fixup(as, &rep);
+            if (fixup_report) *fixup_report = rep;
+            write_file(ap, std::vector<char>(as.begin(), as.end()));
+            st = run_child({bindir + "/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
+                            ap, "-o", obp}, &log);
+            if (st == 0) st = run_child({bindir + "/ld.lld", "-shared", obp, "-o", op}, &log);
+        }
+        unlink(ap.c_str());
+        unlink(obp.c_str());
+    }
     if (st != 0 || !read_file(op, code)) {
         unlink(op.c_str());
         return fail(QPB_ECOMPILE, "clang (" + clang + ") exit " + std::to_string(st) + ": " + log.substr(0, 4000));
@@ -338,43 +363,10 @@ static int compile_with_hiprtc(const std::string &kname, const std::string &src,
 std::string compiler_ident() { return compiler().ident; }
 
 // ---- DPP hazard audit of a compiled code object ----------------------------
-// The row / wave kernels issue v_fmac_f64_dpp from inline asm, where the
-// compiler's hazard recognizer cannot insert the wait states a DPP instruction
-// needs: 2 after a write of its DPP-permuted source VGPR (src0; the cross-lane
-// read happens early in the pipeline), 5 after a VALU write of EXEC.  (The
-// compiler applies the 2-state rule to every VGPR operand of its own DPP code;
-// the production row kernel has writes of src1 right before its DPP FMAs and is
-// equal to the oracle to 1e-9, so src1 / the accumulator are not checked.)  The
-// audit disassembles the code object (llvm-objdump) and checks every DPP
-// instruction against every path into it, branches included.  Returns 1 clean,
-// 0 hazard found (report says where), -1 could not audit.
-struct AsmInsn {
-    uint64_t addr = 0;
-    std::string mn;
-    std::vector<std::pair<int, int>> vregs;   // every v register operand, [lo, hi]
-    bool vdef0 = false;                       // first operand is a VGPR the instruction writes
-    bool exec_valu_def = false;               // v_cmpx*: VALU write of EXEC
-    bool dpp = false, uncond = false;
-    int ws = 1;                               // wait states the instruction itself provides
-    long long target = -1;                    // branch target address
-};
-
-static bool parse_vreg(const std::string &t, std::pair<int, int> &r) {
-    size_t i = 0;
-    while (i < t.size() && (t[i] == ' ' || t[i] == '-' || t[i] == '|')) i++;
-    if (i + 1 >= t.size() || t[i] != 'v') return false;
-    if (t[i + 1] == '[') {
-        int a = 0, b = 0;
-        if (sscanf(t.c_str() + i + 2, "%d:%d]", &a, &b) != 2) return false;
-        r = {a, b};
-        return true;
-    }
-    if (!isdigit((unsigned char)t[i + 1])) return false;
-    int a = atoi(t.c_str() + i + 1);
-    r = {a, a};
-    return true;
-}
-
+// llvm-objdump the code object and check every DPP instruction on every path into
+// it (qpb_hazard.cpp: 2 wait states after a VALU write of any VGPR it reads, 5
+// after a VALU write of EXEC).  Returns 1 clean, 0 hazard found (report says
+// where), -1 could not audit.
 int dpp_audit(const std::vector<char> &code, std::string *report) {
     const Compiler &cc = compiler();
     std::string objdump;
@@ -392,104 +384,7 @@ int dpp_audit(const std::vector<char> &code, std::string *report) {
     const int st = run_child({objdump, "-d", "--mcpu=gfx950", path}, &dis);
     unlink(path.c_str());
     if (st != 0) { *report = "llvm-objdump failed"; return -1; }
-    std::vector<AsmInsn> ins;
-    std::map<uint64_t, size_t> at;
-    uint64_t fbase = 0;
-    std::istringstream in(dis);
-    std::string line;
-    while (std::getline(in, line)) {
-        if (!line.empty() && isxdigit((unsigned char)line[0]) && line.find(">:") != std::string::npos) {
-            fbase = strtoull(line.c_str(), nullptr, 16);          // "0000000000001d00 <name>:"
-            continue;
-        }
-        if (line.empty() || line[0] != '\t') continue;
-        const size_t cm = line.find("// ");
-        if (cm == std::string::npos) continue;
-        AsmInsn a;
-        a.addr = strtoull(line.c_str() + cm + 3, nullptr, 16);
-        std::string text = line.substr(1, cm - 1);
-        std::istringstream ts(text);
-        ts >> a.mn;
-        std::string rest;
-        std::getline(ts, rest);
-        std::vector<std::string> ops;
-        {
-            std::string cur;
-            for (char ch : rest) {
-                if (ch == ',') { ops.push_back(cur); cur.clear(); }
-                else cur += ch;
-            }
-            if (!cur.empty()) {     // the last operand may carry modifiers after a space
-                std::istringstream ls(cur);
-                std::string first;
-                ls >> first;
-                ops.push_back(first);
-            }
-        }
-        for (auto &o : ops) {
-            std::pair<int, int> r;
-            if (parse_vreg(o, r)) a.vregs.push_back(r);
-        }
-        const std::string &m = a.mn;
-        a.dpp = m.find("_dpp") != std::string::npos;
-        const bool no_vdst = m.rfind("s_", 0) == 0 || m.find("store") != std::string::npos ||
-                             m.rfind("ds_write", 0) == 0 || m.rfind("v_cmp", 0) == 0 ||
-                             m.rfind("v_readlane", 0) == 0 || m.rfind("v_readfirstlane", 0) == 0;
-        std::pair<int, int> r0;
-        a.vdef0 = !no_vdst && !ops.empty() && parse_vreg(ops[0], r0);
-        a.exec_valu_def = m.rfind("v_cmpx", 0) == 0;
-        if (m == "s_nop") a.ws = 1 + (int)strtol(rest.c_str(), nullptr, 0);
-        a.uncond = m == "s_branch" || m == "s_endpgm" || m.rfind("s_setpc", 0) == 0;
-        if (m == "s_branch" || m.rfind("s_cbranch", 0) == 0) {
-            const size_t lt = line.find('<', cm);
-            if (lt != std::string::npos) {
-                const size_t plus = line.find("+0x", lt);
-                a.target = (long long)(fbase + (plus != std::string::npos ? strtoull(line.c_str() + plus + 3, nullptr, 16) : 0));
-            }
-        }
-        at[a.addr] = ins.size();
-        ins.push_back(std::move(a));
-    }
-    if (ins.empty()) { *report = "empty disassembly"; return -1; }
-    std::map<uint64_t, std::vector<size_t>> preds_by_target;
-    for (size_t i = 0; i < ins.size(); i++)
-        if (ins[i].target >= 0) preds_by_target[(uint64_t)ins[i].target].push_back(i);
-    auto overlap = [](const std::pair<int, int> &a, const std::pair<int, int> &b) {
-        return a.first <= b.second && b.first <= a.second;
-    };
-    int hazards = 0;
-    std::ostringstream rep;
-    for (size_t d = 0; d < ins.size(); d++) {
-        if (!ins[d].dpp) continue;
-        // backward DFS over predecessors; ws = wait states between the visited
-        // instruction and the DPP instruction
-        std::vector<std::pair<size_t, int>> stack;
-        auto push_preds = [&](size_t i, int ws) {
-            if (i > 0 && !ins[i - 1].uncond) stack.push_back({i - 1, ws});
-            auto it = preds_by_target.find(ins[i].addr);
-            if (it != preds_by_target.end())
-                for (size_t p : it->second) stack.push_back({p, ws});
-        };
-        push_preds(d, 0);
-        int guard = 0;
-        while (!stack.empty() && guard++ < 4096) {
-            auto [p, ws] = stack.back();
-            stack.pop_back();
-            const AsmInsn &P = ins[p];
-            bool bad = false;
-            if (ws < 2 && P.vdef0 && ins[d].vregs.size() >= 2 && overlap(P.vregs[0], ins[d].vregs[1])) bad = true;
-            if (ws < 5 && P.exec_valu_def) bad = true;
-            if (bad) {
-                if (hazards++ < 8)
-                    rep << std::hex << "0x" << ins[d].addr << " " << ins[d].mn << " after 0x" << P.addr << " " << P.mn
-                        << std::dec << " (" << ws << " wait states); ";
-                break;
-            }
-            if (ws + P.ws < 5) push_preds(p, ws + P.ws);
-        }
-    }
-    *report = hazards ? std::to_string(hazards) + " DPP hazard(s): " + rep.str() : "clean";
-    return hazards ? 0 : 1;
+    return audit_disassembly(dis, report);
 }
 
 
@@ -503,6 +398,7 @@ int compile_kernel(const std::string &kname, const std::function<std::string()> 
     const Compiler &cc = compiler();
     std::string id = cc.ident;
     for (auto &o : compile_options(exact)) id += " " + o;
+    id += getenv("QPB_NO_ASM_FIXUP") ? " no-dpp-fixup" : " dpp-wait-states-v1";   // qpb_hazard.cpp's rules
     char tag[17];
     snprintf(tag, sizeof tag, "%016llx", (unsigned long long)fnv1a(id));
     const std::string dir = cache_dir();
@@ -514,19 +410,22 @@ int compile_kernel(const std::string &kname, const std::function<std::string()> 
         return QPB_OK;
     }
     std::string src = gen_src();
+    std::string fix;
     int rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
-                              : compile_with_clang(cc.clang, kname, src, exact, *code);
+                              : compile_with_clang(cc.clang, kname, src, exact, *code, &fix);
     if (rc) return rc;
     std::string audit = "no DPP asm";
     if (src.find("v_fmac_f64_dpp") != std::string::npos) {
-        // DPP from inline asm: verify the wait states in the code object; on a
-        // hazard (or no way to check) rebuild with wait states inside every
-        // DPP asm (QPB_DPP_NOP = 2), which is hazard-free by construction
+        // DPP from inline asm: the clang path padded it (asm_fixup); verify the
+        // wait states in the code object either way; on a hazard (or no way to
+        // check) rebuild with wait states inside every DPP asm (QPB_DPP_NOP = 2),
+        // which is hazard-free by construction
         const int ok = dpp_audit(*code, &audit);
+        if (!fix.empty()) audit = fix + "; audit: " + audit;
         if (ok != 1) {
             src = "#define QPB_DPP_NOP 2\n" + src;
             rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
-                                  : compile_with_clang(cc.clang, kname, src, exact, *code);
+                                  : compile_with_clang(cc.clang, kname, src, exact, *code, &fix);
             if (rc) return rc;
             audit += " -> rebuilt with QPB_DPP_NOP=2";
         }
@@ -617,6 +516,25 @@ int compile_tree2(qpb_plan *plan) {
     if (plan->tree_occ_batch < 0) return fail(QPB_EINVAL, "plan has no large-batch tree kernel");
     return compile_kernel(plan->tree2_kname, [plan] { return generate_tree_kernel(plan->pl, plan->tree2_wg, nullptr); },
                           false, &plan->tree2_code);
+}
+
+// The warm-solve variant of a plan's kernel: its source with QPB_WARM = 1 under
+// the name <kname>_w (a separate code object, so the cold kernels -- the batched
+// hot path -- keep their register allocation).
+static std::mutex g_warm_mu;
+int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
+                 std::shared_ptr<std::vector<char>> **slot) {
+    {
+        std::lock_guard<std::mutex> lk(g_warm_mu);
+        *slot = &plan->warm_code[kname];     // std::map nodes are stable
+    }
+    const std::string wname = kname + "_w";
+    return compile_kernel(wname, [&] {
+        std::string src = gen_src();
+        for (size_t pos = 0; (pos = src.find(kname, pos)) != std::string::npos; pos += wname.size())
+            src.replace(pos, kname.size(), wname);
+        return "#define QPB_WARM 1\n" + src;
+    }, exact, *slot);
 }
 
 int load_function(const std::string &kname, const std::shared_ptr<std::vector<char>> &code, hipFunction_t *fn) {
@@ -856,6 +774,26 @@ long qpb_plan_kernel_name(const qpb_plan *plan, long B, char *buf, long cap) {
     return (long)s.size();
 }
 
+int qpb_plan_compile_warm(qpb_plan *plan, long B) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    if (B < 1) B = 1;
+    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
+                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
+    const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
+    const bool row2 = wave && plan->row_occ_batch >= 0 && B > plan->row_occ_batch;
+    const bool tree2 = tree && plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch;
+    const std::string &kn = row2 ? plan->row2_kname : wave ? plan->wave_kname : tree2 ? plan->tree2_kname
+                          : tree ? plan->tree_kname : plan->kname;
+    std::function<std::string()> gen =
+        row2 ? std::function<std::string()>([plan] { return qpb::generate_row_kernel(plan->pl, nullptr, 2); })
+        : wave ? std::function<std::string()>([plan] { return qpb::wave_source_of(plan); })
+        : tree2 ? std::function<std::string()>([plan] { return qpb::generate_tree_kernel(plan->pl, plan->tree2_wg, nullptr); })
+        : tree ? std::function<std::string()>([plan] { return qpb::generate_tree_kernel(plan->pl, plan->tree_wg, nullptr); })
+               : std::function<std::string()>([plan] { return qpb::generate_kernel(plan->pl, plan->gen); });
+    std::shared_ptr<std::vector<char>> *slot = nullptr;
+    return qpb::compile_warm(plan, kn, gen, !wave && !tree && plan->gen.exact, &slot);
+}
+
 int qpb_plan_compile(qpb_plan *plan) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     const int k = plan->kernel_pref;
@@ -893,13 +831,30 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
     hipFunction_t fn;
     const bool row2 = wave && plan->row_occ_batch >= 0 && B > plan->row_occ_batch;
     const bool tree2 = tree && plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch;
-    int rc = row2 ? qpb::compile_row2(plan) : wave ? qpb::compile_wave(plan)
+    int rc;
+    if (!warm) {
+        rc = row2 ? qpb::compile_row2(plan) : wave ? qpb::compile_wave(plan)
            : tree2 ? qpb::compile_tree2(plan) : tree ? qpb::compile_tree(plan) : qpb::compile_plan(plan);
-    if (!rc) rc = row2 ? qpb::load_function(plan->row2_kname, plan->row2_code, &fn)
-                : wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
-                : tree2 ? qpb::load_function(plan->tree2_kname, plan->tree2_code, &fn)
-                : tree ? qpb::load_function(plan->tree_kname, plan->tree_code, &fn)
-                       : qpb::load_function(plan->kname, plan->code, &fn);
+        if (!rc) rc = row2 ? qpb::load_function(plan->row2_kname, plan->row2_code, &fn)
+                    : wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
+                    : tree2 ? qpb::load_function(plan->tree2_kname, plan->tree2_code, &fn)
+                    : tree ? qpb::load_function(plan->tree_kname, plan->tree_code, &fn)
+                           : qpb::load_function(plan->kname, plan->code, &fn);
+    } else {
+        if (wave && !plan->wave_ok) return fail(QPB_EINVAL, "plan is not eligible for the wave kernel");
+        if (tree && !plan->tree_ok) return fail(QPB_EINVAL, "plan is not eligible for the tree kernel");
+        const std::string &kn = row2 ? plan->row2_kname : wave ? plan->wave_kname : tree2 ? plan->tree2_kname
+                              : tree ? plan->tree_kname : plan->kname;
+        std::function<std::string()> gen =
+            row2 ? std::function<std::string()>([plan] { return qpb::generate_row_kernel(plan->pl, nullptr, 2); })
+            : wave ? std::function<std::string()>([plan] { return qpb::wave_source_of(plan); })
+            : tree2 ? std::function<std::string()>([plan] { return qpb::generate_tree_kernel(plan->pl, plan->tree2_wg, nullptr); })
+            : tree ? std::function<std::string()>([plan] { return qpb::generate_tree_kernel(plan->pl, plan->tree_wg, nullptr); })
+                   : std::function<std::string()>([plan] { return qpb::generate_kernel(plan->pl, plan->gen); });
+        std::shared_ptr<std::vector<char>> *slot = nullptr;
+        rc = qpb::compile_warm(plan, kn, gen, !wave && !tree && plan->gen.exact, &slot);
+        if (!rc) rc = qpb::load_function(kn + "_w", *slot, &fn);
+    }
     if (rc) return rc;
     qpb_settings def;
     qpb_default_settings(&def);

@@ -1,6 +1,7 @@
 // qpb_runtime.hpp -- internals shared by the batched C ABI and the qpSWIFT drop-in.
 #pragma once
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -41,6 +42,9 @@ struct qpb_plan {
     std::shared_ptr<std::vector<char>> tree2_code;
     std::vector<char> tree2_tables;
     std::map<int, void *> tree2_dev;
+    // warm-solve variants (qpb_solve_warm; QPB_WARM = 1), compiled on first use:
+    // cold kernel name -> code of "<name>_w"
+    std::map<std::string, std::shared_ptr<std::vector<char>>> warm_code;
     std::vector<int> ctl_table;                 // controller-QP assembly entries (qpb_assemble_controller)
     std::map<int, void *> ctl_dev;              // device -> uploaded entries
     ~qpb_plan();
@@ -64,6 +68,8 @@ int compile_wave(qpb_plan *plan);
 int compile_row2(qpb_plan *plan);
 int compile_tree2(qpb_plan *plan);
 int compile_tree(qpb_plan *plan);
+int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
+                 std::shared_ptr<std::vector<char>> **slot);
 std::string wave_source_of(const qpb_plan *plan);   // wave or row form, as the plan chose
 int set_error(int code, const char *msg);
 // qpb_solve / qpb_solve_best / qpb_solve_warm in one: best != NULL fuses the

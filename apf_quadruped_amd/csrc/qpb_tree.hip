@@ -36,6 +36,10 @@ struct qpb_args {
     long warm;              // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
 };
 
+#ifndef QPB_WARM
+#define QPB_WARM 0              // 1: the warm-solve variant (qpb_solve_warm), compiled on demand
+#endif
+
 #define NX QPB_NX
 #define NY QPB_NY
 #define NZ QPB_NZ
@@ -696,8 +700,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
 #endif
     double sigma = 100.0, alpha_p = 0.0, alpha_d = 0.0;
     double n_rx = 0.0, n_ry = 0.0, n_rz = 0.0, n_mu = 0.0, mu = 0.0;
-    long it = 0, it0 = 0;       // it0: IterationCount the QP enters with (warm solve)
-    int flag0 = 3;              // stats->Flag it enters with (QP_FATAL after setup)
+    long it = 0;
     bool conv = false;
     const double invm = 1.0 / (double)NZ;
     // rhs b = [rx; ry; rz - ds/z] (updatekktmatrix_b, Auxilary.c:274-295)
@@ -725,24 +728,27 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     // (sigma <= sigma_d: refactor, qpSWIFT.c:572-579)
     enum { ST_INIT, ST_INITZ, ST_TOP, ST_PRED, ST_CORR, ST_CENT };
     int stage = ST_INIT;
-    if (a.warm) {
-        // warm: QP_SOLVE continues from the object's iterate, IterationCount and
-        // options->sigma (qpSWIFT.c:502-596 never re-initialises); no setup solve
-        for (int j = t; j < NX; j += QPB_WG) V[j] = a.x[tile * (NX * 64) + j * 64 + ql];
+#if QPB_WARM
+    // warm variant (qpb_solve_warm): QP_SOLVE continues from the object's iterate,
+    // IterationCount and options->sigma (qpSWIFT.c:502-596 never re-initialises)
+    for (int j = t; j < NX; j += QPB_WG) V[j] = a.x[tile * (NX * 64) + j * 64 + ql];
 #if NY > 0
-        for (int j = t; j < NY; j += QPB_WG) V[NX + j] = a.y[tile * (NY * 64) + j * 64 + ql];
+    for (int j = t; j < NY; j += QPB_WG) V[NX + j] = a.y[tile * (NY * 64) + j * 64 + ql];
 #endif
-        for (int j = t; j < NZ; j += QPB_WG) {
-            V[NX + NY + j] = a.z[tile * (NZ * 64) + j * 64 + ql];
-            S[j] = a.s[tile * (NZ * 64) + j * 64 + ql];
-        }
-        it0 = a.iters[q];
-        flag0 = a.flag[q];
-        sigma = a.sig[q];
-        __syncthreads();
-        QPB_ROWS(if (r < NX) xp[u] = V[r];)
-        stage = ST_TOP;
+    for (int j = t; j < NZ; j += QPB_WG) {
+        V[NX + NY + j] = a.z[tile * (NZ * 64) + j * 64 + ql];
+        S[j] = a.s[tile * (NZ * 64) + j * 64 + ql];
     }
+    const long it0 = a.iters[q];    // IterationCount the QP enters with
+    const int flag0 = a.flag[q];    // stats->Flag it enters with (QP_FATAL after setup)
+    sigma = a.sig[q];
+    __syncthreads();
+    QPB_ROWS(if (r < NX) xp[u] = V[r];)
+    stage = ST_TOP;
+#else
+    constexpr long it0 = 0;
+    constexpr int flag0 = 3;
+#endif
     int flag = flag0;
     for (;;) {
         if (stage == ST_INITZ || stage == ST_TOP) {
@@ -908,7 +914,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         a.flag[q] = flag;
         a.iters[q] = (int)(it0 + it);
         a.fval[q] = fv[0];
-        if (a.sig) a.sig[q] = sigma;
+#if QPB_WARM
+        a.sig[q] = sigma;
+#endif
         if (a.stats) {
             double *st = a.stats + tile * (6 * 64) + ql;
 #if QPB_T_TIMING == 2

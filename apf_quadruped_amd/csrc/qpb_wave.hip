@@ -41,6 +41,10 @@ struct qpb_args {
     long warm;                    // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
 };
 
+#ifndef QPB_WARM
+#define QPB_WARM 0                // 1: the warm-solve variant (qpb_solve_warm), compiled on demand
+#endif
+
 // tuning knobs (defaults = measured best; scripts/sweep.py "wave:KNOB=V,...")
 #ifndef QPB_W_GG           // 1: G(r,i)G(r,j) products in registers; 0: recompute from LDS
 #define QPB_W_GG (QPB_NNZG <= 48)
@@ -928,36 +932,38 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     double x = 0.0, y = 0.0, s[ZC], z[ZC];
 #pragma unroll
     for (int t = 0; t < ZC; t++) { s[t] = 1.0; z[t] = 1.0; }
-    long it = -1, it0 = 0;     // it0: IterationCount the QP enters with (warm solve)
-    int flag0 = 3;             // stats->Flag it enters with (QP_FATAL after setup)
+    long it = -1;
     // squared residual norms; the exit test compares them with tol^2 (sqrt is
     // monotone), the norms themselves are taken once, for the statistics
     double st_rx2 = 0.0, st_ry2 = 0.0, st_rz2 = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;
     double fv = 0.0;    // this lane's objective term at the last residual evaluation
     const double tol2 = a.tol > 0.0 ? a.tol * a.tol : -1.0;
     double sigma = 100.0;      // options->sigma (SIGMA, GlobalOptions.h:49)
-    if (a.warm) {
-        // warm: QP_SOLVE continues from the object's iterate, IterationCount and
-        // options->sigma (qpSWIFT.c:502-596 never re-initialises); no setup pass
-        if (isx) x = a.x[tile * (NX * 64) + lane * 64 + ql];
+#if QPB_WARM
+    // warm variant (qpb_solve_warm): QP_SOLVE continues from the object's iterate,
+    // IterationCount and options->sigma (qpSWIFT.c:502-596 never re-initialises)
+    if (isx) x = a.x[tile * (NX * 64) + lane * 64 + ql];
 #if NY > 0
-        if (isy) y = a.y[tile * (NY * 64) + lane * 64 + ql];
+    if (isy) y = a.y[tile * (NY * 64) + lane * 64 + ql];
 #endif
 #pragma unroll
-        for (int t = 0; t < ZC; t++)
-            if (isz[t]) {
-                z[t] = a.z[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql];
-                s[t] = a.s[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql];
-            }
-        it0 = a.iters[q];
-        flag0 = a.flag[q];
-        sigma = a.sig[q];
-        it = 0;
-    }
+    for (int t = 0; t < ZC; t++)
+        if (isz[t]) {
+            z[t] = a.z[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql];
+            s[t] = a.s[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql];
+        }
+    const long it0 = a.iters[q];   // IterationCount the QP enters with
+    const int flag0 = a.flag[q];   // stats->Flag it enters with (QP_FATAL after setup)
+    sigma = a.sig[q];
+    it = 0;
+#else
+    constexpr long it0 = 0;
+    constexpr int flag0 = 3;
+#endif
     int flag = flag0;
     for (;;) {
         // qpSWIFT.c:598-601: QP_MAXIT only when IterationCount == maxit
-        if (it >= 0 && it >= a.maxit) { flag = it0 + it == a.maxit ? 2 : flag0; break; }
+        if (it >= 0 && it >= a.maxit) { flag = (!QPB_WARM || it0 + it == a.maxit) ? 2 : flag0; break; }
         QPB_TS(it >= 0 ? 8 + 8 * it : 2);
         // updatekktmatrix (Auxilary.c:211-215): z diagonal -s/z.  The setup
         // system has -I there, which is this with s = z = 1 (iteration -1).
@@ -1036,7 +1042,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         bool pc = true;
         if (it >= 0) {
             if (st_rx2 < tol2 && st_rz2 < tol2 && (NY == 0 || st_ry2 < tol2) && st_mu < a.abstol) {
-                flag = it0 + it == a.maxit ? 2 : 0;
+                flag = (QPB_WARM && it0 + it == a.maxit) ? 2 : 0;
                 break;
             }
             mu = st_mu;
@@ -1160,7 +1166,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         a.flag[q] = flag;
         a.iters[q] = (int)(it0 + it);
         a.fval[q] = fval;
-        if (a.sig) a.sig[q] = sigma;
+#if QPB_WARM
+        a.sig[q] = sigma;
+#endif
         if (a.stats && !QPB_W_TIMING) {
             double *o = a.stats + tile * 384 + ql;
             o[0] = __builtin_sqrt(st_rx2); o[64] = __builtin_sqrt(st_ry2); o[128] = __builtin_sqrt(st_rz2); o[192] = st_mu; o[256] = ap; o[320] = ad;

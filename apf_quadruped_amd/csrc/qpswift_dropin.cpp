@@ -183,7 +183,11 @@ PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const
     // no GPU QP_SOLVE fails anyway (QP_FATAL), so setup does not JIT at all.
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) rc = 0;
-    else rc = raw->wave_ok && raw->kernel_pref != 1 ? qpb::compile_wave(raw) : qpb::compile_plan(raw);
+    else {
+        rc = raw->wave_ok && raw->kernel_pref != 1 ? qpb::compile_wave(raw) : qpb::compile_plan(raw);
+        // QP_SOLVE continues from the QP's state: the warm-solve variant
+        if (!rc) rc = qpb_plan_compile_warm(raw, 1);
+    }
     if (rc != 0) {
         err = qpb_last_error();
         return nullptr;

@@ -130,6 +130,9 @@ long qpb_plan_tree_tables(const qpb_plan *plan, void *buf, long cap);
 /* Compile the plan's kernels for gfx950 (hiprtc) or fetch them from the
  * code-object cache; needs no GPU.  qpb_solve calls this implicitly. */
 int  qpb_plan_compile(qpb_plan *plan);
+/* The same for the warm-solve variant qpb_solve_warm launches for a batch of B
+ * (compiled on first use otherwise). */
+int  qpb_plan_compile_warm(qpb_plan *plan, long B);
 
 int  qpb_solve(qpb_plan *plan, long B,
                const double *P, const double *A, const double *G,

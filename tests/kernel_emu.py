@@ -77,7 +77,8 @@ def emulate(plan, vals, B, reltol=1e-6, abstol=1e-6, maxit=100, sigma_d=0.0, war
     warm = the `out` dict of a previous call plus "sigma" ([B]): a warm solve
     (qpb_solve_warm) continuing from it, updated in place and returned."""
     from apf_quadruped_amd.batch import TILE, ntiles
-    lib, wg = build_emulator(plan.source(), plan.exact)
+    # the warm variant is the same source with QPB_WARM = 1 (qpb_solve_warm)
+    lib, wg = build_emulator(("#define QPB_WARM 1\n" if warm is not None else "") + plan.source(), plan.exact)
     T = ntiles(B) * TILE
     keep = {k: np.ascontiguousarray(v, dtype=np.float64) for k, v in vals.items()}
     out = warm if warm is not None else \

@@ -1,9 +1,12 @@
 """The DPP hazard audit every generated kernel with inline-asm DPP passes before
-it is cached (qpb_audit_dpp, csrc/qpb_runtime.hip): a DPP instruction must not
-read, as its permuted source, a VGPR written within 2 wait states, nor follow a
-VALU EXEC write within 5.  The compiler's hazard recognizer cannot see into
-inline asm, so this check is what makes the hand-written v_fmac_f64_dpp safe.
-CPU only (clang + llvm-objdump cross-compile and disassemble gfx950)."""
+it is cached (qpb_audit_dpp, csrc/qpb_hazard.cpp): a DPP instruction must not
+read ANY VGPR -- the permuted source, the other source or the tied accumulator
+(the rule LLVM's checkDPPHazards applies to its own DPP code) -- written by a
+VALU within 2 wait states, nor follow a VALU EXEC write within 5.  The compiler's
+hazard recognizer cannot see into inline asm; the runtime compiles such kernels
+through assembly and pads every DPP asm site exactly (asm_fixup), and this audit
+checks the result.  CPU only (clang + llvm-objdump cross-compile and disassemble
+gfx950)."""
 import ctypes as C
 import glob
 import os
@@ -46,15 +49,42 @@ def test_audit_flags_dpp_source_written_too_recently(tmp_path, pad, expect):
     assert r == expect, rep
 
 
+SNIPPET_SRC1 = r"""
+#include <hip/hip_runtime.h>
+extern "C" __global__ void k(double *p) {
+    double a = p[threadIdx.x], b = p[threadIdx.x + 64], c = p[threadIdx.x + 128];
+    asm volatile("v_add_f64 %2, %2, %2\n\t" PAD "v_fmac_f64_dpp %1, %0, %2 row_newbcast:3 row_mask:0xf "
+                 "bank_mask:0xf bound_ctrl:1" : "+v"(a), "+v"(c), "+v"(b));
+    p[threadIdx.x] = c + a + b;
+}
+"""
+SNIPPET_ACC = SNIPPET_SRC1.replace('"v_add_f64 %2, %2, %2', '"v_add_f64 %1, %1, %1')
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="ROCm clang not present")
+@pytest.mark.parametrize("snippet", ["src1", "acc"])
+@pytest.mark.parametrize("pad,expect", [("", 0), ("s_nop 0\\n\\t", 0), ("s_nop 1\\n\\t", 1)])
+def test_audit_flags_other_operands_written_too_recently(tmp_path, snippet, pad, expect):
+    """The non-permuted source and the tied accumulator count too."""
+    src = tmp_path / "k.hip"
+    src.write_text((SNIPPET_SRC1 if snippet == "src1" else SNIPPET_ACC).replace("PAD", f'"{pad}"'))
+    co = tmp_path / "k.co"
+    subprocess.run([CLANG, "-x", "hip", "--cuda-device-only", "--no-gpu-bundle-output", "--offload-arch=gfx950",
+                    "-O3", "-o", str(co), str(src)], check=True)
+    r, rep = _audit(co.read_bytes())
+    assert r == expect, rep
+
+
 def test_cached_dpp_kernels_were_audited():
-    """Every cached row / wave code object carries its audit record: clean, or
-    rebuilt with wait states in every DPP asm."""
+    """Every cached row / wave code object carries its audit record: clean (after
+    the assembly-level padding of its DPP asm sites), or rebuilt with wait states
+    in every DPP asm -- and audits clean now."""
     cache = os.path.join(ROOT, "apf_quadruped_amd", "kcache")
     objs = [f for f in glob.glob(os.path.join(cache, "qpb_row*.hsaco")) + glob.glob(os.path.join(cache, "qpb_wave*.hsaco"))]
     if not objs:
         pytest.skip("no cached kernels (run __graft_entry__.build())")
     for f in objs:
         rec = open(f + ".audit").read()
-        assert rec == "clean" or "rebuilt with QPB_DPP_NOP=2" in rec, (f, rec)
+        assert rec.endswith("clean") or "rebuilt with QPB_DPP_NOP=2" in rec, (f, rec)
         r, rep = _audit(open(f, "rb").read())
         assert r == 1 or "rebuilt" in rec, (f, rep)
