@@ -33,6 +33,17 @@ VARIANTS = {
     "no_prealloc_spill": {"QPB_CLANG_FLAGS": "-mllvm -amdgpu-prealloc-sgpr-spill-vgprs=0"},
     # the row kernel's parked fault (illegal address with all three knobs on)
     "row_knobs": {"QPB_WAVE_OPTS": "QPB_R_ZF128=1 QPB_R_AADPP=1 QPB_R_LATEFAC=1", "QPB_DIAG_PHASES": "c1row"},
+    # round 3: the workaround off, with / without the DPP wait-state padding (qpb_hazard.cpp)
+    "prera_on": {},
+    "prera_on_unpadded": {"QPB_NO_ASM_FIXUP": "1"},
+    "prera_on_opq0": {"QPB_WAVE_OPTS": "QPB_W_OPQ=0"},
+    "prera_on_opq0_h0re0": {"QPB_WAVE_OPTS": "QPB_W_OPQ=0 QPB_W_H0RE=0"},
+    "prera_off_opq0": {"QPB_PRERA_OFF": "1", "QPB_WAVE_OPTS": "QPB_W_OPQ=0"},
+    "prera_on_dup0": {"QPB_WAVE_OPTS": "QPB_W_DUP=0"},
+    "prera_on_dup0_opq0": {"QPB_WAVE_OPTS": "QPB_W_DUP=0 QPB_W_OPQ=0"},
+    "prera_off_dup0_opq0": {"QPB_PRERA_OFF": "1", "QPB_WAVE_OPTS": "QPB_W_DUP=0 QPB_W_OPQ=0"},
+    "padded": {"QPB_PRERA_OFF": "1"},
+    "unpadded": {"QPB_PRERA_OFF": "1", "QPB_NO_ASM_FIXUP": "1"},
     "maxit0": {"QPB_DIAG_MAXIT": "0"},
     "maxit1": {"QPB_DIAG_MAXIT": "1"},
     "maxit2": {"QPB_DIAG_MAXIT": "2"},
