@@ -421,6 +421,7 @@ struct Gen {
              "  const void *tab; double *best; unsigned long long *part; unsigned *ctr;\n"
              "  double *sig;   // per-QP sigma: in (warm) / out (NULL: not tracked)\n"
              "  long warm;     // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)\n"
+             "  double *trace; // warm variant: per-QP timers + per-iteration statistics (or NULL)\n"
              "};\n";
         o << "static __device__ __forceinline__ double qpb_rcp(double v) {\n"
              "  double r = __builtin_amdgcn_rcp(v);\n"
@@ -529,6 +530,9 @@ struct Gen {
         // == maxit (qpSWIFT.c:598-601), IterationCount = it0 + it
         ln("long it = 0; int flag = flag0;");
         ln("double fval = 0.0, st_rx = 0.0, st_ry = 0.0, st_rz = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;");
+        // the drop-in's timers and verbose trace (KernelArgs::trace): warm variant only
+        ln("double *const trc = (QPB_WARM && a.trace) ? a.trace + q * " + S(QPB_TRACE_STRIDE) + " : nullptr;");
+        ln("long t_fac = 0, t_kkt = 0, n_top = 0, n_it = 0, tk0 = 0;");
         open("for (;;) {");
         ln("if (it >= a.maxit) { flag = it0 + it == a.maxit ? 2 : flag0; break; }");
         begin_phase();
@@ -621,6 +625,8 @@ struct Gen {
         }
         dot("sz", m, "s", "z");
         ln("st_mu = sz / " + S(m) + ".0;");
+        ln("if (trc && it < " + S(QPB_TRACE_MAX) + ") { double *e = trc + 4 + 7 * it; e[0] = fval; e[1] = st_rx; "
+           "e[2] = st_ry; e[3] = st_rz; e[4] = st_mu; n_top = it + 1; }");
         ln(std::string("if (st_rx < a.tol && st_rz < a.tol") + (p ? " && st_ry < a.tol" : "") +
            " && st_mu < a.abstol) { flag = it0 + it == a.maxit ? 2 : 0; break; }");
         // lambda, mu (qpSWIFT.c:537-538)
@@ -649,7 +655,9 @@ struct Gen {
             else ln("const double " + V("kd", i) + " = -" + rd("s", i) + " * " + rd("rzi", i) + ";");
         }
         begin_phase();
+        ln("if (trc) tk0 = (long)__builtin_amdgcn_s_memrealtime();");
         factor(pl.K_loop);
+        ln("if (trc) { const long d_ = (long)__builtin_amdgcn_s_memrealtime() - tk0; t_fac += d_; t_kkt += d_; }");
         // form_ds: predictor (pure Newton) or pure centering (qpSWIFT.c:542, 574-575);
         // ds does not enter the factorisation, so it is formed after it.
         //
@@ -700,10 +708,12 @@ struct Gen {
         if (!opt.exact)
             for (long i = 0; i < m; i++) ln(V("cc", i) + " = sigma * mu;");   // centering (!pc) default
         open("if (pc) {");
+        ln("if (trc) tk0 = (long)__builtin_amdgcn_s_memrealtime();");
         solve(pl.K_loop, rhs_with(true), [&](long t) -> std::string {
             if (t < n + p) return "";
             return V("dz", t - n - p);
         });
+        ln("if (trc) t_kkt += (long)__builtin_amdgcn_s_memrealtime() - tk0;");
         dsl_from_dz(true);
         step_length();
         begin_phase(false, true);
@@ -722,16 +732,19 @@ struct Gen {
         }
         close();
         // corrector / centering solve (kktsolve_2, Auxilary.c:524-564)
+        ln("if (trc) tk0 = (long)__builtin_amdgcn_s_memrealtime();");
         solve(pl.K_loop, rhs_with(false), [&](long t) -> std::string {
             if (t < n) return V("dx", t);
             if (t < n + p) return V("dy", t - n);
             return V("dz", t - n - p);
         });
+        ln("if (trc) t_kkt += (long)__builtin_amdgcn_s_memrealtime() - tk0;");
         dsl_from_dz(false);
         step_length();
         begin_phase(false, true);
         ln("ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;");
         ln("ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;");
+        ln("if (trc && it < " + S(QPB_TRACE_MAX) + ") { trc[4 + 7 * it + 5] = ap; trc[4 + 7 * it + 6] = ad; n_it = it + 1; }");
         for (long i = 0; i < n; i++) wr("x", i, madd(rd("x", i), V("dx", i), "ap"));
         for (long i = 0; i < p; i++) wr("y", i, madd(rd("y", i), V("dy", i), "ad"));
         for (long i = 0; i < m; i++) wr("s", i, madd(rd("s", i), V("dsl", i), "ap"));
@@ -750,6 +763,7 @@ struct Gen {
         store("s", m, "s");
         ln("a.flag[q] = flag; a.iters[q] = (int)(it0 + it); a.fval[q] = fval;");
         ln("if (QPB_WARM) a.sig[q] = sigma;");
+        ln("if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }");
         ln("if (a.stats) { double *o = a.stats + tile * 384 + lane; o[0] = st_rx; o[64] = st_ry; o[128] = st_rz;"
            " o[192] = st_mu; o[256] = ap; o[320] = ad; }");
         o << "}\n";

@@ -44,7 +44,15 @@ struct KernelArgs {
     // receives the last sigma.
     double *sig = nullptr;
     long warm = 0;
+    // warm variant only (the drop-in's QP_SOLVE): per QP q, at trace + q * QPB_TRACE_STRIDE,
+    // [0] s_memrealtime ticks (100 MHz) in the factorisations (LDL_numeric), [1] in the KKT
+    // factor + solves (kktsolve_1 / _2), [2] loop-top evaluations recorded, [3] iterations
+    // recorded, then per loop pass i < QPB_TRACE_MAX: fval, n_rx, n_ry, n_rz, n_mu
+    // (before the exit test) and alpha_p, alpha_d (after the update) at [4 + 7 i ..]
+    double *trace = nullptr;
 };
+constexpr int QPB_TRACE_MAX = 256;
+constexpr long QPB_TRACE_STRIDE = 4 + 7L * QPB_TRACE_MAX;
 
 std::string kernel_name(const Plan &pl, const GenOptions &opt);
 // Pick workgroup size / LDS placement for a plan (fast mode): keep every matrix

@@ -40,6 +40,7 @@ struct qpb_args {
     unsigned *ctr;            // arrival counter (zero between launches)
     double *sig;              // per-QP sigma: in (warm) / out (NULL: not tracked)
     long warm;                // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
+    double *trace;            // warm variant: per-QP timers + per-iteration statistics (or NULL)
 };
 
 // Staging / H0 knobs.  Round 1 saw an illegal-address fault with ZF128, AADPP and
@@ -59,6 +60,8 @@ struct qpb_args {
 #ifndef QPB_WARM
 #define QPB_WARM 0        // 1: the warm-solve variant (qpb_solve_warm), compiled on demand
 #endif
+#define QPB_TRACE_MAX 256                       // = qpb::QPB_TRACE_MAX (qpb_codegen.hpp)
+#define QPB_TRACE_STRIDE (4 + 7 * QPB_TRACE_MAX)
 #ifndef QPB_R_TIMING
 #define QPB_R_TIMING 0    // 2: per-QP start / end (realtime, cycles), iterations, hardware ids into stats;
                           // 3: cycles per phase (H0 + setup solve, residuals, factor, predictor,
@@ -520,6 +523,12 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     double sigf = sigma;       // options->sigma when this row's loop ends (a frozen row's own
                                // sigma keeps being recomputed while the rest of the wave runs)
 #define QPB_SIGF sigf = sigma
+    // the drop-in's timers and verbose trace (KernelArgs::trace, qpb_codegen.hpp):
+    // s_memrealtime ticks in the factorisations and in factor + solves, and the
+    // statistics the reference prints per iteration (qpSWIFT.c:506-517, 598-600)
+    double *const trc = (a.trace && valid && c == 0) ? a.trace + qc * QPB_TRACE_STRIDE : nullptr;
+    long t_fac = 0, t_kkt = 0, n_top = 0, n_it = 0;
+#define QPB_CLK() ((long)__builtin_amdgcn_s_memrealtime())
 #else
     constexpr long it0 = 0;
     constexpr int flag0 = 3;
@@ -576,6 +585,18 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         double mu = 0.0;
         if (it >= 0) {
             const double mu_it = sz * (1.0 / NZ);
+#if QPB_WARM
+            {
+                double fq[1] = {isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0};
+                qpb_rsum<1>(fq);
+                if (trc && act && it < QPB_TRACE_MAX) {
+                    double *e = trc + 4 + 7 * it;
+                    e[0] = fq[0]; e[1] = __builtin_sqrt(red[0]); e[2] = NY > 0 ? __builtin_sqrt(red[1]) : 0.0;
+                    e[3] = __builtin_sqrt(red[2]); e[4] = mu_it;
+                    n_top = it + 1;
+                }
+            }
+#endif
             if (act) {
                 fv = isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0;      // objective (Auxilary.c:1133-1141)
                 st_rx2 = red[0];
@@ -595,7 +616,13 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         }
 #if QPB_R_LATEFAC
         // factor after the exit test: the wave's last pass skips it
+#if QPB_WARM
+        const long tf0 = QPB_CLK();
+#endif
         factor(w0, w1);
+#if QPB_WARM
+        { const long d_ = QPB_CLK() - tf0; t_fac += d_; t_kkt += d_; }
+#endif
         QPB_TM(2);
 #endif
         if (!pc) sigma = a.sigma_d;
@@ -634,7 +661,13 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         }
         if (qpb_any(act && pc)) {
             // predictor (kktsolve_1, Auxilary.c:471-515), ds = -s.*z
+#if QPB_WARM
+            const long ts0 = QPB_CLK();
+#endif
             solve(w0, w1, rx, ry, rz0 + s0, rz1 + s1, dx, dy, dz0, dz1);
+#if QPB_WARM
+            t_kkt += QPB_CLK() - ts0;
+#endif
             dsl0 = -s0 * __builtin_fma(dz0, rzi0, 1.0);
             dsl1 = -s1 * __builtin_fma(dz1, rzi1, 1.0);
             step_length();
@@ -652,13 +685,26 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         }
         QPB_TM(3);
         // corrector / centering (kktsolve_2, Auxilary.c:524-564)
+#if QPB_WARM
+        const long tc0 = QPB_CLK();
+#endif
         solve(w0, w1, rx, ry, __builtin_fma(-cc0, rzi0, rz0 + s0), __builtin_fma(-cc1, rzi1, rz1 + s1), dx, dy, dz0,
               dz1);
+#if QPB_WARM
+        t_kkt += QPB_CLK() - tc0;
+#endif
         dsl0 = __builtin_fma(__builtin_fma(-s0, dz0, cc0), rzi0, -s0);
         dsl1 = __builtin_fma(__builtin_fma(-s1, dz1, cc1), rzi1, -s1);
         step_length();
         ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
         ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
+#if QPB_WARM
+        if (trc && act && it < QPB_TRACE_MAX) {
+            trc[4 + 7 * it + 5] = ap;
+            trc[4 + 7 * it + 6] = ad;
+            n_it = it + 1;
+        }
+#endif
         if (act) {
             if (isx) x = __builtin_fma(dx, ap, x);
             if (isy) y = __builtin_fma(dy, ad, y);
@@ -704,6 +750,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             a.fval[q] = fr[0];
 #if QPB_WARM
             a.sig[q] = sigf;
+            if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
 #endif
 #if QPB_R_TIMING == 3
             QPB_TM(4);
@@ -743,4 +790,5 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_R_WPE) QPB_KERNEL_NAME(
 #endif
 #undef QPB_TM
 #undef QPB_SIGF
+#undef QPB_CLK
 #endif  // QPB_ROW_COMMON_ONLY

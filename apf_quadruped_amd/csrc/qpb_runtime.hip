@@ -813,7 +813,7 @@ int qpb_plan_compile(qpb_plan *plan) {
 int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
                       const double *c, const double *h, const double *b, const qpb_settings *st,
                       double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
-                      double *stats, double *best, void *stream, double *sig, bool warm) {
+                      double *stats, double *best, void *stream, double *sig, bool warm, double *trace) {
     if (warm && !sig) return fail(QPB_EINVAL, "a warm solve needs sigma");
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     if (B < 0) return fail(QPB_EINVAL, "need B >= 0");
@@ -871,6 +871,7 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
     a.maxit = st->maxit;
     a.sig = sig;
     a.warm = warm ? 1 : 0;
+    a.trace = warm ? trace : nullptr;      // only the warm variants trace
     if (tree && (rc = qpb::tree_tables_on_device(plan, &a.tab, tree2))) return rc;
     // qpb_solve_best on the row kernel: the argmin runs inside the solve launch
     // (its last wave reduces the per-wave partials), saving the separate launch
@@ -904,7 +905,7 @@ int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const do
               double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
               double *stats, void *stream) {
     return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, nullptr, stream,
-                         nullptr, false);
+                         nullptr, false, nullptr);
 }
 
 int qpb_solve_best(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
@@ -913,7 +914,7 @@ int qpb_solve_best(qpb_plan *plan, long B, const double *P, const double *A, con
                    double *stats, double *best, void *stream) {
     if (!best) return fail(QPB_EINVAL, "qpb_solve_best: best is NULL");
     return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, best, stream,
-                         nullptr, false);
+                         nullptr, false, nullptr);
 }
 
 int qpb_solve_warm(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
@@ -922,7 +923,7 @@ int qpb_solve_warm(qpb_plan *plan, long B, const double *P, const double *A, con
                    double *stats, double *sigma, void *stream) {
     if (!sigma) return fail(QPB_EINVAL, "qpb_solve_warm: sigma is NULL");
     return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, nullptr, stream, sigma,
-                         true);
+                         true, nullptr);
 }
 
 /* ---- plan groups: one launch for a mixed-pattern batch (qpb_group_*) ---- */

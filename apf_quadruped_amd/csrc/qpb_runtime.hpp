@@ -73,8 +73,10 @@ int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<s
 std::string wave_source_of(const qpb_plan *plan);   // wave or row form, as the plan chose
 int set_error(int code, const char *msg);
 // qpb_solve / qpb_solve_best / qpb_solve_warm in one: best != NULL fuses the
-// argmin; sig != NULL receives every QP's last sigma (and, warm, supplies it)
+// argmin; sig != NULL receives every QP's last sigma (and, warm, supplies it);
+// trace (warm only): KernelArgs::trace, QPB_TRACE_STRIDE doubles per QP
 int solve_ex(qpb_plan *plan, long B, const double *P, const double *A, const double *G, const double *c,
              const double *h, const double *b, const qpb_settings *st, double *x, double *y, double *z, double *s,
-             int *flag, int *iters, double *fval, double *stats, double *best, void *stream, double *sig, bool warm);
+             int *flag, int *iters, double *fval, double *stats, double *best, void *stream, double *sig, bool warm,
+             double *trace = nullptr);
 }  // namespace qpb

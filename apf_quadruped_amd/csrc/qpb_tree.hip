@@ -34,11 +34,14 @@ struct qpb_args {
     unsigned *ctr;
     double *sig;            // per-QP sigma: in (warm) / out (NULL: not tracked)
     long warm;              // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
+    double *trace;            // warm variant: per-QP timers + per-iteration statistics (or NULL)
 };
 
 #ifndef QPB_WARM
 #define QPB_WARM 0              // 1: the warm-solve variant (qpb_solve_warm), compiled on demand
 #endif
+#define QPB_TRACE_MAX 256                       // = qpb::QPB_TRACE_MAX (qpb_codegen.hpp)
+#define QPB_TRACE_STRIDE (4 + 7 * QPB_TRACE_MAX)
 
 #define NX QPB_NX
 #define NY QPB_NY
@@ -745,6 +748,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
     __syncthreads();
     QPB_ROWS(if (r < NX) xp[u] = V[r];)
     stage = ST_TOP;
+    // the drop-in's timers and verbose trace (KernelArgs::trace, qpb_codegen.hpp):
+    // s_memrealtime ticks in the factorisations and in factor + solves, and the
+    // statistics the reference prints per iteration (qpSWIFT.c:506-517, 598-600)
+    double *const trc = (a.trace && t == 0) ? a.trace + q * QPB_TRACE_STRIDE : nullptr;
+    long t_fac = 0, t_kkt = 0, n_top = 0, n_it = 0;
+#define QPB_CLK() ((long)__builtin_amdgcn_s_memrealtime())
 #else
     constexpr long it0 = 0;
     constexpr int flag0 = 3;
@@ -795,6 +804,18 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
                 n_rz = __builtin_sqrt(acc[2]);
                 n_mu = acc[3] * invm;
             }
+#if QPB_WARM
+            {
+                // (the objective needs its own gather program over R, which holds the
+                // residuals here: the tree kernel traces fval only at the end -- NaN)
+                if (trc && it < QPB_TRACE_MAX) {
+                    double *e = trc + 4 + 7 * it;
+                    e[0] = __builtin_nan("");
+                    e[1] = n_rx; e[2] = n_ry; e[3] = n_rz; e[4] = n_mu;
+                    n_top = it + 1;
+                }
+            }
+#endif
             if (n_rx < a.tol && n_rz < a.tol && (NY == 0 || n_ry < a.tol) && n_mu < a.abstol) {
                 flag = 0;
                 conv = true;
@@ -830,9 +851,19 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         } else {
             rhs();
         }
+#if QPB_WARM
+        const long tk0 = QPB_CLK();
+#endif
         if (fac) factor();                // its level barriers order the rhs before the solve
         else __syncthreads();
+#if QPB_WARM
+        const long tk1 = QPB_CLK();
+        if (fac) t_fac += tk1 - tk0;
+#endif
         solve();
+#if QPB_WARM
+        t_kkt += QPB_CLK() - tk0;
+#endif
         if (stage == ST_INIT) {
             QPB_ROWS(V[r] = r < NX + NY ? W[pv[u]] : 0.0;)
             __syncthreads();
@@ -867,6 +898,13 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         alpha_d = ab[1] < 1e10 ? ab[1] : 1.0;
         alpha_p = 0.99 * alpha_p > 1.0 ? 1.0 : 0.99 * alpha_p;
         alpha_d = 0.99 * alpha_d > 1.0 ? 1.0 : 0.99 * alpha_d;
+#if QPB_WARM
+        if (trc && it < QPB_TRACE_MAX) {
+            trc[4 + 7 * it + 5] = alpha_p;
+            trc[4 + 7 * it + 6] = alpha_d;
+            n_it = it + 1;
+        }
+#endif
         QPB_ROWS(
             if (r < NX) V[r] = __builtin_fma(W[pv[u]], alpha_p, V[r]);
             else if (r < NX + NY) V[r] = __builtin_fma(W[pv[u]], alpha_d, V[r]);
@@ -916,6 +954,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         a.fval[q] = fv[0];
 #if QPB_WARM
         a.sig[q] = sigma;
+        if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
 #endif
         if (a.stats) {
             double *st = a.stats + tile * (6 * 64) + ql;

@@ -39,11 +39,14 @@ struct qpb_args {
     unsigned *ctr;
     double *sig;                  // per-QP sigma: in (warm) / out (NULL: not tracked)
     long warm;                    // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
+    double *trace;            // warm variant: per-QP timers + per-iteration statistics (or NULL)
 };
 
 #ifndef QPB_WARM
 #define QPB_WARM 0                // 1: the warm-solve variant (qpb_solve_warm), compiled on demand
 #endif
+#define QPB_TRACE_MAX 256                       // = qpb::QPB_TRACE_MAX (qpb_codegen.hpp)
+#define QPB_TRACE_STRIDE (4 + 7 * QPB_TRACE_MAX)
 
 // tuning knobs (defaults = measured best; scripts/sweep.py "wave:KNOB=V,...")
 #ifndef QPB_W_GG           // 1: G(r,i)G(r,j) products in registers; 0: recompute from LDS
@@ -956,6 +959,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     const int flag0 = a.flag[q];   // stats->Flag it enters with (QP_FATAL after setup)
     sigma = a.sig[q];
     it = 0;
+    // the drop-in's timers and verbose trace (KernelArgs::trace, qpb_codegen.hpp):
+    // s_memrealtime ticks in the factorisations and in factor + solves, and the
+    // statistics the reference prints per iteration (qpSWIFT.c:506-517, 598-600)
+    double *const trc = (a.trace && lane == 0) ? a.trace + q * QPB_TRACE_STRIDE : nullptr;
+    long t_fac = 0, t_kkt = 0, n_top = 0, n_it = 0;
+#define QPB_CLK() ((long)__builtin_amdgcn_s_memrealtime())
 #else
     constexpr long it0 = 0;
     constexpr int flag0 = 3;
@@ -978,6 +987,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         // both, and the LDL's latency-bound pivot chain is scheduled together
         // with the residual products and reductions.
         if (QPB_W_TIMING) fstamp = it == 1 ? 360 : 0;
+#if QPB_WARM
+        const long tf0 = QPB_CLK();
+#endif
         factor_publish(kd);
         // residuals (Auxilary.c:745-786), objective (Auxilary.c:1133-1141)
         if (lane < NX) Vb[lane] = x;
@@ -987,6 +999,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         if (lane < NY) Vb[NX + NZ + lane] = y;
         qpb_wsync();
         factor_ldl();
+#if QPB_WARM
+        long tf1 = QPB_CLK() - tf0;   // + the transpose below
+#endif
         if (QPB_W_TIMING && it == 1) QPB_TS(364);
         double tp = 0.0;
         ry = by;
@@ -1040,6 +1055,17 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             }
         }
         bool pc = true;
+#if QPB_WARM
+        {
+            const double fq = qpb_rsum<ROWS_X>(isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0);
+            if (trc && it < QPB_TRACE_MAX) {
+                double *e = trc + 4 + 7 * it;
+                e[0] = fq; e[1] = __builtin_sqrt(st_rx2); e[2] = __builtin_sqrt(st_ry2); e[3] = __builtin_sqrt(st_rz2);
+                e[4] = st_mu;
+                n_top = it + 1;
+            }
+        }
+#endif
         if (it >= 0) {
             if (st_rx2 < tol2 && st_rz2 < tol2 && (NY == 0 || st_ry2 < tol2) && st_mu < a.abstol) {
                 flag = (QPB_WARM && it0 + it == a.maxit) ? 2 : 0;
@@ -1049,7 +1075,15 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             pc = sigma > a.sigma_d;
         }
         QPB_TS(it >= 0 ? 9 + 8 * it : 5);
+#if QPB_WARM
+        const long tt0 = QPB_CLK();
+#endif
         factor_transpose();
+#if QPB_WARM
+        tf1 += QPB_CLK() - tt0;
+        t_fac += tf1;
+        t_kkt += tf1;
+#endif
         QPB_TS(it >= 0 ? 10 + 8 * it : 6);
         if (!pc) sigma = a.sigma_d;
         double cc[ZC];
@@ -1081,7 +1115,13 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 bz[t] = pass == 2 ? hz[t] : (pass == 0 ? rz[t] + s[t] : __builtin_fma(-cc[t], rzi[t], rz[t] + s[t]));
             if (pass == 2) { bxv = -cx; byv = by; }
             if (QPB_W_TIMING) sstamp = (it == 1 && pass == 0) ? 300 : 0;
+#if QPB_WARM
+            const long ts0 = QPB_CLK();
+#endif
             solve(bxv, byv, bz, dx, dy, dz);
+#if QPB_WARM
+            t_kkt += QPB_CLK() - ts0;
+#endif
             QPB_TS(it >= 0 ? (pass == 0 ? 11 : 13) + 8 * it : 3);
             if (pass == 2) {
                 // initial point: x0, y0 from the solve; s0, z0 from r = h - G x0
@@ -1137,6 +1177,13 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             QPB_TS(14 + 8 * it);
             ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
             ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
+#if QPB_WARM
+            if (trc && it < QPB_TRACE_MAX) {
+                trc[4 + 7 * it + 5] = ap;
+                trc[4 + 7 * it + 6] = ad;
+                n_it = it + 1;
+            }
+#endif
             if (isx) x = __builtin_fma(dx, ap, x);
             if (isy) y = __builtin_fma(dy, ad, y);
 #pragma unroll
@@ -1168,6 +1215,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         a.fval[q] = fval;
 #if QPB_WARM
         a.sig[q] = sigma;
+        if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
 #endif
         if (a.stats && !QPB_W_TIMING) {
             double *o = a.stats + tile * 384 + ql;

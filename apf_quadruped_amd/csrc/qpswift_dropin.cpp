@@ -13,7 +13,9 @@
 // here: without a GPU, QP_SOLVE reports QP_FATAL.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -79,11 +81,12 @@ struct Priv {
     double *zmem = nullptr, *zdev = nullptr;   // zero-copy slab (host / device address)
     long nP = 0, nA = 0, nG = 0, nin = 0, nout = 0;
     long oP = 0, oA = 0, oG = 0, oc = 0, oh = 0, ob = 0, ox = 0, oy = 0, oz = 0, os = 0, ost = 0, ofv = 0,
-         oin = 0, oout = 0, ototal = 0;
+         oin = 0, oout = 0, otr = 0, ototal = 0;
     // kkt_initialize's point is in x, y, z, s (QP_SETUP ran it on the device):
     // QP_SOLVE then continues from the object's state (a warm solve), as the
     // reference's QP_SOLVE always does; otherwise its first QP_SOLVE is cold
     bool inited = false;
+    const double *trace = nullptr;   // the last warm solve's trace (host copy, for verbose)
 };
 
 // Public struct first so that a QP* is also a Handle*.
@@ -375,6 +378,7 @@ int ensure_device(Priv &v, const QP &q) {
         v.nout = q.n + q.p + 2 * q.m + 6 + 1;   // x y z s stats fval
         v.oin = take(v.nin);
         v.oout = take(v.nout + 2);              // + flag, iters (two ints in one double slot), sigma
+        v.otr = take(qpb::QPB_TRACE_STRIDE);   // timers + per-iteration statistics (warm solves)
         v.ofv = v.oout + v.nout - 1;
         v.ototal = o;
     }
@@ -392,7 +396,7 @@ int ensure_device(Priv &v, const QP &q) {
         }
         w.dcap = v.ototal;
     }
-    const long hneed = v.nin + v.nout + 2;
+    const long hneed = v.nin + v.nout + 2 + qpb::QPB_TRACE_STRIDE;
     if (!zero_copy(v) && w.hcap < hneed) {
         if (w.hmem) (void)hipHostFree(w.hmem);
         w.hcap = 0;
@@ -445,6 +449,45 @@ CallState call_state(const Priv &v, const QP &q, long maxit) {
 
 // Results of one launch back into the QP object.  `setup_init`: the launch was
 // QP_SETUP's kkt_initialize (maxit = 0): only x, y, z, s change.
+// options->verbose > 0: the reference's messages (qpSWIFT.c:484-488, 506-509,
+// 598-641), printed after the launch from the kernel's trace, in the same order
+void print_verbose(const Priv &v, const QP &q, const double *tr, long it0) {
+    const long ntop = tr ? (long)tr[2] : 0, nit = tr ? (long)tr[3] : 0;
+    for (long i = 0; i < std::max(ntop, nit); i++) {
+        const double *e = tr + 4 + 7 * i;
+        if (i < ntop)
+            printf("It: %ld || pcost : %e || rx:%e   ||  ry:%e ||  rz:%e || mu:%e\n", it0 + i, e[0], e[1], e[2], e[3],
+                   e[4]);
+        if (i < nit) printf("      || Primal Step Size : %f || Dual Step Size   : %f\n", e[5], e[6]);
+    }
+    const stats &st = v.st;
+    if (st.Flag == QP_OPTIMAL) {
+        printf("\nOptimal Solution Found\n");
+        printf("Solve Time     : %f ms\n", (st.tsolve + st.tsetup) * 1000.0);
+    } else if (st.Flag == QP_MAXIT) {
+        printf("\nMaximum Iterations reached\n");
+        printf("Solve Time     : %f ms\n", st.tsolve * 1000.0);
+    }
+    if (st.Flag == QP_OPTIMAL || st.Flag == QP_MAXIT) {
+        printf("KKT_Solve Time : %f ms\n", st.kkt_time * 1000.0);
+        printf("LDL Time       : %f ms\n", st.ldl_numeric * 1000.0);
+        printf("Iterations     : %ld\n\n", st.IterationCount);
+    }
+    if (st.Flag == QP_FATAL) printf("\nUnknown Error Detected\n\n");
+    if (st.Flag == QP_KKTFAIL) printf("\nLDL Factorization fail\n\n");
+    (void)q;
+    fflush(stdout);
+}
+
+// timers from the kernel's trace: kkt_time (this call's factor + solves,
+// qpSWIFT.c:554-586, 611) and ldl_numeric (accumulated, Auxilary.c:476-484);
+// s_memrealtime runs at 100 MHz
+void take_timers(Priv &v, const double *tr) {
+    if (!tr) return;
+    v.st.kkt_time = tr[1] * 1e-8;
+    v.st.ldl_numeric += tr[0] * 1e-8;
+}
+
 void take_results(Priv &v, QP &q, const double *x, const double *y, const double *z, const double *s,
                   const double *stv, double fval, const int *fl_it, double sigma, long maxit, bool setup_init) {
     const long n = q.n, m = q.m, p = q.p;
@@ -495,7 +538,8 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     int *dfl = reinterpret_cast<int *>(d + ofl);
     int rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
                            p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz,
-                           d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, nullptr, v.stream, d + osg, cs.warm);
+                           d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, nullptr, v.stream, d + osg, cs.warm,
+                           d + v.otr);
     if (hipStreamSynchronize(v.stream) != hipSuccess && !rc) rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: kernel failed");
     if (rc) return rc;
     std::vector<double> tmp((size_t)(n + p + 2 * m + 6));
@@ -511,6 +555,10 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     int iv[2];
     std::memcpy(iv, h + ofl, sizeof(iv));
     take_results(v, q, tx, ty, tz, ts, tst, h[v.ofv], iv, h[osg], cs.st.maxit, setup_init);
+    if (cs.warm) {
+        take_timers(v, h + v.otr);
+        v.trace = h + v.otr;
+    }
     return QPB_OK;
 }
 
@@ -588,7 +636,7 @@ int solve_staged(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     if (!rc)
         rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
                            p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz,
-                           d + v.os, fl, fl + 1, d + v.ofv, d + v.ost, nullptr, v.stream, sg, cs.warm);
+                           d + v.os, fl, fl + 1, d + v.ofv, d + v.ost, nullptr, v.stream, sg, cs.warm, d + v.otr);
     qpb::CopySegs gc{};
     long qo = v.oout;
     auto gather = [&](long src, long k, long ss) {
@@ -606,6 +654,11 @@ int solve_staged(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     if (!rc && hipMemcpyAsync(hout, d + v.oout, sizeof(double) * (size_t)(v.nout + 2), hipMemcpyDeviceToHost,
                               v.stream) != hipSuccess)
         rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: download failed");
+    double *htr = hout + v.nout + 2;        // the trace: header + the entries maxit can fill
+    const long ntr = 4 + 7 * std::min<long>(std::max<long>(cs.st.maxit, 0), qpb::QPB_TRACE_MAX);
+    if (!rc && cs.warm && hipMemcpyAsync(htr, d + v.otr, sizeof(double) * (size_t)ntr, hipMemcpyDeviceToHost,
+                                         v.stream) != hipSuccess)
+        rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: trace download failed");
     if (hipStreamSynchronize(v.stream) != hipSuccess && !rc) rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: kernel failed");
     if (rc) return rc;
     const double *r = hout;
@@ -613,6 +666,10 @@ int solve_staged(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     std::memcpy(iv, hout + v.nout, sizeof(iv));
     take_results(v, q, r, r + n, r + n + p, r + n + p + m, r + n + p + 2 * m, hout[v.nout - 1], iv, hout[v.nout + 1],
                  cs.st.maxit, setup_init);
+    if (cs.warm) {
+        take_timers(v, htr);
+        v.trace = htr;
+    }
     return QPB_OK;
 }
 
@@ -721,6 +778,13 @@ qp_int QP_SOLVE(QP *myQP) {
     if (!myQP) return QP_FATAL;
     const auto t0 = clk::now();
     Priv &v = *handle_of(myQP)->priv;
+    const bool verbose = myQP->options && myQP->options->verbose > 0;
+    if (verbose) {                                  // qpSWIFT.c:484-488
+        printf("****qpSWIFT : Sparse Quadratic Programming Solver****\n\n");
+        printf("================Data Statistics======================\n");
+    }
+    const long it0 = v.st.IterationCount;
+    v.trace = nullptr;
     int rc;
     if (!v.plan) {
         rc = qpb::set_error(QPB_ECOMPILE, ("QP_SOLVE: no kernel for this QP: " + v.err).c_str());
@@ -729,6 +793,7 @@ qp_int QP_SOLVE(QP *myQP) {
     }
     if (rc) v.st.Flag = QP_FATAL;
     v.st.tsolve = seconds_since(t0);
+    if (verbose) print_verbose(v, *myQP, v.trace, it0);
     return v.st.Flag;
 }
 

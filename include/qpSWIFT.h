@@ -13,36 +13,42 @@
  *
  * Behaviour (see INTEGRATION.md for the full list of differences):
  *   QP_SETUP / QP_SETUP_dense  build the pattern plan (KKT layout, ordering,
- *       elimination tree, generated kernel) on the host and cache it by sparsity
+ *       elimination tree, generated kernels) on the host and cache it by sparsity
  *       pattern; the matrices are converted exactly as the reference does
- *       (dense -> CSC drops exact zeros).  No GPU work happens here.
- *   QP_SOLVE  uploads the values, runs setup's initial point + the Mehrotra
- *       loop in ONE kernel launch on the current HIP device, and copies x, y,
- *       z, s and the statistics back.  There is no CPU fallback: without a
- *       usable GPU it returns QP_FATAL and qpb_last_error() says why.
+ *       (dense -> CSC drops exact zeros).  Like the reference (qpSWIFT.c:447),
+ *       setup leaves kkt_initialize's point in x, y, z, s: one device launch
+ *       (QPSWIFT_HIP_SETUP_INIT=0 skips it: x, y, z, s then stay zero until the
+ *       first QP_SOLVE, which runs the initial point itself -- one launch per
+ *       tick instead of two, at the price of that difference).
+ *   QP_SOLVE  continues from the QP object's state as the reference does
+ *       (qpSWIFT.c:502-601): its x, y, z, s, stats->IterationCount, stats->Flag
+ *       and options->sigma, at most options->maxit more iterations, QP_MAXIT only
+ *       when IterationCount reaches exactly maxit; one launch of the plan's
+ *       warm-solve kernel on the current HIP device, then x, y, z, s, the
+ *       statistics and options->sigma are written back.  There is no CPU
+ *       fallback: without a usable GPU it returns QP_FATAL and qpb_last_error()
+ *       says why.
  *   Arithmetic: by default the fast kernels (FMA, reciprocal pivots; the
  *   wave-cooperative kernel where eligible), which factor with the same
  *   permutation, pivots and regularisations and agree with qpSWIFT to rounding.
  *   QPSWIFT_HIP_EXACT=1 in the environment selects the bit-faithful kernel (the
  *   reference's operation order, IEEE division, no FMA): bit-identical to
- *   qpSWIFT when given the same permutation.  With Permut == NULL the KKT is
- *   ordered by this library's restatement of SuiteSparse AMD (amd_l_order with
- *   amd_l_defaults, src/qpSWIFT/qpSWIFT.c:424-440), which yields qpSWIFT's own
- *   permutation (bit-for-bit, tests/test_amd.py); stats->AMD_RESULT is then 0,
- *   and -3 when Permut is given, as in the reference.
- *
- * Fields that differ from the reference:
- *   stats->kkt_time, stats->ldl_numeric  always 0: the factorisation and the
- *       triangular solves are fused with the rest of each iteration into one
- *       device launch, so they have no separate host-side timing; tsetup and
- *       tsolve hold the host wall time of QP_SETUP* / QP_SOLVE.
- *   options->sigma  every QP_SOLVE starts from SIGMA (100) -- the value the
- *       reference's setup stores (qpSWIFT.c:74, 275) -- and the final sigma is
- *       not written back (the reference leaves its last sigma there).
- *   options->verbose  accepted and ignored (no printing).
- *   QP_SOLVE on the same QP object again re-runs the initial point and the loop
- *       from the current input values (the reference continues from its last
- *       iterate; for a converged QP both return the same x at once).
+ *   qpSWIFT when given the same permutation, across repeated QP_SOLVE calls too.
+ *   With Permut == NULL the KKT is ordered by this library's restatement of
+ *   SuiteSparse AMD (amd_l_order with amd_l_defaults, src/qpSWIFT/qpSWIFT.c:
+ *   424-440), which yields qpSWIFT's own permutation (bit-for-bit,
+ *   tests/test_amd.py); stats->AMD_RESULT is then 0, and -3 when Permut is
+ *   given, as in the reference.
+ *   stats->kkt_time / ldl_numeric  device time (s_memrealtime, 100 MHz) of this
+ *       call's factorisations + triangular solves / of the factorisations
+ *       (accumulated over calls, reset by setup), measured inside the kernel
+ *       (the reference times kktsolve_1/_2 and LDL_numeric on the host,
+ *       qpSWIFT.c:554-586, Auxilary.c:476-484); tsetup and tsolve hold the host
+ *       wall time of QP_SETUP* / QP_SOLVE.
+ *   options->verbose > 0  the reference's messages (qpSWIFT.c:484-488, 506-509,
+ *       598-641) on stdout, the per-iteration lines printed after the launch from
+ *       the kernel's trace (up to 256 iterations per call; the tree kernel, used
+ *       only for KKT systems beyond the wave kernel's range, traces pcost as nan).
  */
 #ifndef QPSWIFT_HIP_DROPIN_H
 #define QPSWIFT_HIP_DROPIN_H

@@ -31,6 +31,7 @@ static qpb_dim3 threadIdx, blockIdx;
 static inline double qpb_emu_rcp(double v) { return 1.0 / v; }
 #define __builtin_amdgcn_rcp(v) qpb_emu_rcp(v)
 #define __builtin_amdgcn_readfirstlane(v) (v)
+#define __builtin_amdgcn_s_memrealtime() 0UL
 """
 
 DRIVER = r"""
@@ -48,7 +49,7 @@ class QpbArgs(C.Structure):
                                           "fval", "stats")] + \
                [("B", C.c_long), ("tol", C.c_double), ("abstol", C.c_double), ("sigma_d", C.c_double),
                 ("maxit", C.c_long)] + [(n, C.c_void_p) for n in ("tab", "best", "part", "ctr", "sig")] + \
-               [("warm", C.c_long)]
+               [("warm", C.c_long), ("trace", C.c_void_p)]
 
 
 def build_emulator(src: str, exact: bool, cache_dir=None):
