@@ -253,7 +253,9 @@ std::string generate_tree_kernel(const Plan &pl, int wg, std::string *name_out, 
       << "\n#define QPB_LNZ " << lnz << "\n#define QPB_NNZP " << nP << "\n#define QPB_NNZA " << nA
       << "\n#define QPB_NNZG " << nG << "\n#define QPB_WG " << wg << "\n";
     // four 192-thread workgroups per CU are three waves per SIMD: <= 168 registers
-    if (wg == 192) o << "#define QPB_T_WPE 3\n";
+    // and 4 prefetched descriptor rounds, not 8: 58 -> 14 spilled registers, MPC 10 x
+    // 1 024 QPs 1.72 -> 1.48 ms, HBM 183 -> 51 MB per launch (profiles/r03_tree_pf.log)
+    if (wg == 192) o << "#define QPB_T_WPE 3\n#define QPB_T_PF 4\n";
     if (const char *e = getenv("QPB_TREE_OPTS")) {     // experiment knobs (#ifndef blocks of qpb_tree.hip)
         std::istringstream in(e);
         std::string kv;

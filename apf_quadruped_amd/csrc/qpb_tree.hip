@@ -280,9 +280,12 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
         // a use of every prefetched value on every path: otherwise the compiler
         // sinks each load into the one branch that reads it, right before its use,
         // and the prefetch no longer runs ahead
-        static_assert(QPB_T_PF == 8, "qpb_keep lists eight descriptor slots");
-        asm volatile("" ::"v"(S.h), "v"(S.d[0]), "v"(S.d[1]), "v"(S.d[2]), "v"(S.d[3]), "v"(S.d[4]), "v"(S.d[5]),
-                     "v"(S.d[6]), "v"(S.d[7]));
+        static_assert(QPB_T_PF == 8 || QPB_T_PF == 4, "qpb_keep lists four or eight descriptor slots");
+        if constexpr (QPB_T_PF == 8)
+            asm volatile("" ::"v"(S.h), "v"(S.d[0]), "v"(S.d[1]), "v"(S.d[2]), "v"(S.d[3]), "v"(S.d[4]), "v"(S.d[5]),
+                         "v"(S.d[6]), "v"(S.d[7]));
+        else
+            asm volatile("" ::"v"(S.h), "v"(S.d[0]), "v"(S.d[1]), "v"(S.d[2]), "v"(S.d[3]));
         QPB_SEG(2, "s"(0));
         if (S.rb & (1 << 17)) {
             panel(S.doff, S.toff);                      // supernode panels of this level (list, count)

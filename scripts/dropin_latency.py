@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--shape", default="c1", choices=["c1", "c30", "c30_trot", "c30_crawl"])
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--tol", type=float, default=1e-2)        # the controller's (main.cpp:1651)
+    ap.add_argument("--setup-init", type=int, default=1, help="QPSWIFT_HIP_SETUP_INIT (recorded only)")
     a = ap.parse_args()
     from apf_quadruped_amd import _lib, plans, qpswift_abi as abi, workloads as W
     if a.mode == "exact":
@@ -66,7 +67,7 @@ def main():
     L = _lib.lib()
     run(L)                                   # first ticks: plan + kernel (cache) + device buffers
     lat, flags, xs = run(L)
-    out = dict(shape=a.shape, mode=a.mode, tol=a.tol, ticks=a.ticks, optimal=float((flags == 0).mean()),
+    out = dict(shape=a.shape, mode=a.mode, tol=a.tol, ticks=a.ticks, setup_init=a.setup_init, optimal=float((flags == 0).mean()),
                gpu_us_median=float(np.median(lat) * 1e6), gpu_us_p99=float(np.percentile(lat, 99) * 1e6),
                gpu_setup_us=float(run.seg[0]), gpu_solve_us=float(run.seg[1]))
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libqpswift_ref.so")
