@@ -187,9 +187,15 @@ class Plan:
         L.qpb_plan_tree_tables(self._h, buf, size)
         return buf.raw[:size]
 
-    def compile(self, warm: bool = False, B: int = 1) -> None:
+    def compile(self, warm: bool = False, B: int = 1, serve: bool = False) -> bool:
         """Compile (or fetch from the code-object cache) the plan's kernels; warm:
-        the warm-solve variant qpb_solve_warm launches for a batch of B."""
+        the warm-solve variant qpb_solve_warm launches for a batch of B; serve: the
+        persistent forms of the one-QP kernel the drop-in's device solves use
+        (False when that kernel has none)."""
+        if serve:
+            rc = _lib.lib().qpb_plan_compile_serve(self._h)
+            check(min(rc, 0), "qpb_plan_compile_serve")
+            return rc == 0
         if warm:
             check(_lib.lib().qpb_plan_compile_warm(self._h, int(B)), "qpb_plan_compile_warm")
         else:

@@ -9,7 +9,9 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cctype>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -523,19 +525,69 @@ int compile_tree2(qpb_plan *plan) {
 // the name <kname>_w (a separate code object, so the cold kernels -- the batched
 // hot path -- keep their register allocation).
 static std::mutex g_warm_mu;
-int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
-                 std::shared_ptr<std::vector<char>> **slot) {
+
+// Device side of qpb::serve_ex, prepended to a QPB_SERVE variant's source.  The
+// mailbox lives in fine-grained (coherent) pinned host memory: the request word is
+// read with system-scope loads (no cache holds it), the answer is written after a
+// system-scope release, which makes the solve's results visible to the host first.
+// The wave polls with a short sleep between reads and leaves after `idle` ticks of
+// the 100 MHz s_memrealtime clock without a new request, or on the stop value, so
+// every launch ends on its own.
+static const char *kServePrelude = R"QPBS(
+struct qpb_mailbox;
+#define QPB_SERVE_STOP (~0ull)
+static __device__ __forceinline__ unsigned long long qpb_uniform64(unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+static __device__ bool qpb_serve_wait(qpb_mailbox *mb, unsigned long long *last, unsigned long long idle,
+                                      unsigned long long *t_seen) {
+    unsigned long long *req = (unsigned long long *)mb;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const unsigned long long r = qpb_uniform64(__hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (r == QPB_SERVE_STOP) return false;
+        if (r != *last) {
+            *last = r;
+            *t_seen = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            return true;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle) return false;
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
+// the answer: [16] the request's number, [32] the ticks from seeing it to here
+static __device__ void qpb_serve_done(qpb_mailbox *mb, unsigned long long r, unsigned long long t_seen) {
+    unsigned long long *ack = (unsigned long long *)mb + 16, *dt = (unsigned long long *)mb + 32;
+    if ((threadIdx.x & 63) == 0) *dt = __builtin_amdgcn_s_memrealtime() - t_seen;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(ack, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+)QPBS";
+
+// a variant of a plan's kernel: `<kname>_w` (warm), `_s` (persistent cold) or `_ws`
+// (persistent warm) -- its source with QPB_WARM / QPB_SERVE set, under that name
+int compile_variant(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src,
+                           bool exact, bool warm, bool serve, std::shared_ptr<std::vector<char>> **slot) {
+    const std::string vname = kname + (warm ? (serve ? "_ws" : "_w") : "_s");
     {
         std::lock_guard<std::mutex> lk(g_warm_mu);
-        *slot = &plan->warm_code[kname];     // std::map nodes are stable
+        *slot = &plan->warm_code[vname];     // std::map nodes are stable
     }
-    const std::string wname = kname + "_w";
-    return compile_kernel(wname, [&] {
+    return compile_kernel(vname, [&] {
         std::string src = gen_src();
-        for (size_t pos = 0; (pos = src.find(kname, pos)) != std::string::npos; pos += wname.size())
-            src.replace(pos, kname.size(), wname);
-        return "#define QPB_WARM 1\n" + src;
+        for (size_t pos = 0; (pos = src.find(kname, pos)) != std::string::npos; pos += vname.size())
+            src.replace(pos, kname.size(), vname);
+        return std::string(warm ? "#define QPB_WARM 1\n" : "") + (serve ? "#define QPB_SERVE 1\n" : "") +
+               (serve ? kServePrelude : "") + src;
     }, exact, *slot);
+}
+
+int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
+                 std::shared_ptr<std::vector<char>> **slot) {
+    return compile_variant(plan, kname, gen_src, exact, true, false, slot);
 }
 
 int load_function(const std::string &kname, const std::shared_ptr<std::vector<char>> &code, hipFunction_t *fn) {
@@ -795,6 +847,18 @@ int qpb_plan_compile_warm(qpb_plan *plan, long B) {
     return qpb::compile_warm(plan, kn, gen, !wave && !tree && plan->gen.exact, &slot);
 }
 
+int qpb_plan_compile_serve(qpb_plan *plan) {
+    if (!plan) return fail(QPB_EINVAL, "NULL plan");
+    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
+                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || 1 <= plan->wave_max_batch)));
+    if (!wave) return qpb::SERVE_NONE;
+    std::shared_ptr<std::vector<char>> *slot = nullptr;
+    auto gen = [plan] { return qpb::wave_source_of(plan); };
+    int rc = qpb::compile_variant(plan, plan->wave_kname, gen, false, false, true, &slot);
+    if (!rc) rc = qpb::compile_variant(plan, plan->wave_kname, gen, false, true, true, &slot);
+    return rc;
+}
+
 int qpb_plan_compile(qpb_plan *plan) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     const int k = plan->kernel_pref;
@@ -896,6 +960,156 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
     // separate single-block launch (agent-coherent stores + counter tail), DESIGN.md
     if (best && !fused) return qpb_argmin(B, fval, flag, best, stream);
     return QPB_OK;
+}
+
+// ---- persistent one-QP solver (qpb::Server) ---------------------------------
+namespace {
+constexpr unsigned long long kStop = ~0ull;
+unsigned long long serve_idle_ticks() {      // s_memrealtime ticks (100 MHz)
+    static const unsigned long long t = [] {
+        const char *e = getenv("QPSWIFT_HIP_SERVE_IDLE_MS");
+        const double ms = e ? atof(e) : 20.0;
+        return (unsigned long long)(std::max(0.1, std::min(ms, 1000.0)) * 1e5);
+    }();
+    return t;
+}
+unsigned long long mb_load(const unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+void mb_store(unsigned long long *p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+}  // namespace
+
+int qpb::serve_stop(Server *srv) {
+    if (!srv || !srv->running) return QPB_OK;
+    mb_store(srv->mb, kStop);
+    const hipError_t e = hipStreamSynchronize((hipStream_t)srv->stream);
+    srv->running = false;
+    srv->kname.clear();
+    mb_store(srv->mb, srv->seq);             // the next launch starts from `seq` again
+    return e == hipSuccess ? QPB_OK : fail(QPB_EHIP, std::string("persistent solver: ") + hipGetErrorString(e));
+}
+
+qpb::Server::~Server() {
+    (void)serve_stop(this);
+    if (stream) (void)hipStreamDestroy((hipStream_t)stream);
+    if (mb) (void)hipHostFree(mb);
+}
+
+int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A, const double *G, const double *c,
+                  const double *h, const double *b, const qpb_settings *st, double *x, double *y, double *z,
+                  double *s, int *flag, int *iters, double *fval, double *stats, double *sig, bool warm,
+                  double *trace) {
+    if (!plan || !srv) return fail(QPB_EINVAL, "NULL plan or server");
+    if (warm && !sig) return fail(QPB_EINVAL, "a warm solve needs sigma");
+    const qpb::Plan &pl = plan->pl;
+    if (!P || !G || !c || !h || !x || !z || !s || !flag || !iters || !fval) return fail(QPB_EINVAL, "NULL data pointer");
+    if (pl.p > 0 && (!A || !b || !y)) return fail(QPB_EINVAL, "p > 0 needs A, b and y");
+    // the kernel solve_ex would launch for one QP must be the row or the wave form
+    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
+                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || 1 <= plan->wave_max_batch)));
+    if (!wave) return SERVE_NONE;
+    std::shared_ptr<std::vector<char>> *slot = nullptr;
+    int rc = compile_variant(plan, plan->wave_kname, [plan] { return qpb::wave_source_of(plan); }, false, warm, true,
+                             &slot);
+    const std::string kn = plan->wave_kname + (warm ? "_ws" : "_s");
+    hipFunction_t fn;
+    if (!rc) rc = load_function(kn, *slot, &fn);
+    if (rc) return rc;
+    qpb_settings def;
+    qpb_default_settings(&def);
+    if (!st) st = &def;
+    KernelArgs a;
+    std::memset((void *)&a, 0, sizeof a);    // compared bytewise below
+    a.P = P; a.A = A; a.G = G; a.c = c; a.h = h; a.b = b;
+    a.x = x; a.y = y; a.z = z; a.s = s;
+    a.flag = flag; a.iters = iters; a.fval = fval; a.stats = stats;
+    a.B = 1;
+    a.tol = st->reltol / std::sqrt(3.0);
+    a.abstol = st->abstol;
+    a.sigma_d = st->sigma_d;
+    a.maxit = st->maxit;
+    a.sig = sig;
+    a.warm = warm ? 1 : 0;
+    a.trace = warm ? trace : nullptr;
+    if (!srv->mb) {
+        void *m = nullptr;
+        if (hipHostMalloc(&m, 512, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+            return fail(QPB_ENOMEM, "persistent solver: mailbox allocation failed");
+        std::memset(m, 0, 512);
+        void *md = nullptr;
+        if (hipHostGetDevicePointer(&md, m, 0) != hipSuccess) {
+            (void)hipHostFree(m);
+            return fail(QPB_EHIP, "persistent solver: mailbox has no device address");
+        }
+        srv->mb = (unsigned long long *)m;
+        srv->mb_dev = (unsigned long long *)md;
+        srv->seq = 0;
+    }
+    if (!srv->stream) {
+        hipStream_t sm;
+        if (hipStreamCreateWithFlags(&sm, hipStreamNonBlocking) != hipSuccess)
+            return fail(QPB_EHIP, "persistent solver: stream creation failed");
+        srv->stream = sm;
+    }
+    hipStream_t sm = (hipStream_t)srv->stream;
+    // a running kernel with other arguments or code: stop it first
+    if (srv->running && (srv->kname != kn || std::memcmp(&srv->args, &a, sizeof a) != 0) && (rc = serve_stop(srv)))
+        return rc;
+    unsigned long long *req = srv->mb, *ack = srv->mb + 16;
+    auto launch = [&](unsigned long long last) {
+        unsigned long long idle = serve_idle_ticks();
+        void *mbd = srv->mb_dev;
+        void *params[] = {&a, &mbd, &last, &idle};
+        const hipError_t e = hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, sm, params, nullptr);
+        if (e != hipSuccess) return fail(QPB_EHIP, std::string("persistent solver launch: ") + hipGetErrorString(e));
+        srv->running = true;
+        srv->kname = kn;
+        srv->args = a;
+        srv->launches++;
+        return QPB_OK;
+    };
+    // a kernel that left on its own (idle) is relaunched before the request
+    if (srv->running) {
+        const hipError_t q = hipStreamQuery(sm);
+        if (q == hipSuccess) srv->running = false;
+        else if (q != hipErrorNotReady) {
+            srv->running = false;
+            return fail(QPB_EHIP, std::string("persistent solver: ") + hipGetErrorString(q));
+        }
+    }
+    if (!srv->running && (rc = launch(srv->seq))) return rc;
+    const unsigned long long r = ++srv->seq;
+    mb_store(req, r);
+    srv->requests++;
+    // wait for the answer; every ~20 us make sure the kernel is still there (it
+    // may have left idle just before the request arrived: then launch again, the
+    // new launch finds the request pending)
+    const auto t0 = std::chrono::steady_clock::now();
+    auto tq = t0;
+    for (unsigned k = 1;; k++) {
+        if (mb_load(ack) == r) {
+            srv->dev_ticks = srv->mb[32];
+            return QPB_OK;
+        }
+        __builtin_ia32_pause();
+        if ((k & 63) != 0) continue;
+        const auto now = std::chrono::steady_clock::now();
+        if (now - tq < std::chrono::microseconds(20)) continue;
+        tq = now;
+        const hipError_t q = hipStreamQuery(sm);
+        if (q == hipErrorNotReady) {
+            if (now - t0 > std::chrono::seconds(60)) {
+                (void)serve_stop(srv);
+                return fail(QPB_EHIP, "persistent solver: no answer within 60 s");
+            }
+            continue;
+        }
+        srv->running = false;
+        if (q != hipSuccess) return fail(QPB_EHIP, std::string("persistent solver: ") + hipGetErrorString(q));
+        if (mb_load(ack) == r) {
+            srv->dev_ticks = srv->mb[32];
+            return QPB_OK;
+        }
+        if ((rc = launch(r - 1))) return rc;
+    }
 }
 
 extern "C" {

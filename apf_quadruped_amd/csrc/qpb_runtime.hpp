@@ -42,8 +42,8 @@ struct qpb_plan {
     std::shared_ptr<std::vector<char>> tree2_code;
     std::vector<char> tree2_tables;
     std::map<int, void *> tree2_dev;
-    // warm-solve variants (qpb_solve_warm; QPB_WARM = 1), compiled on first use:
-    // cold kernel name -> code of "<name>_w"
+    // variants compiled on first use, by name: "<name>_w" warm solve (qpb_solve_warm;
+    // QPB_WARM = 1), "<name>_s" / "<name>_ws" persistent cold / warm (qpb::serve_ex)
     std::map<std::string, std::shared_ptr<std::vector<char>>> warm_code;
     std::vector<int> ctl_table;                 // controller-QP assembly entries (qpb_assemble_controller)
     std::map<int, void *> ctl_dev;              // device -> uploaded entries
@@ -70,6 +70,9 @@ int compile_tree2(qpb_plan *plan);
 int compile_tree(qpb_plan *plan);
 int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
                  std::shared_ptr<std::vector<char>> **slot);
+// a variant of a plan's kernel: "<kname>_w" (warm), "_s" / "_ws" (persistent cold / warm)
+int compile_variant(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
+                    bool warm, bool serve, std::shared_ptr<std::vector<char>> **slot);
 std::string wave_source_of(const qpb_plan *plan);   // wave or row form, as the plan chose
 int set_error(int code, const char *msg);
 // qpb_solve / qpb_solve_best / qpb_solve_warm in one: best != NULL fuses the
@@ -79,4 +82,37 @@ int solve_ex(qpb_plan *plan, long B, const double *P, const double *A, const dou
              const double *h, const double *b, const qpb_settings *st, double *x, double *y, double *z, double *s,
              int *flag, int *iters, double *fval, double *stats, double *best, void *stream, double *sig, bool warm,
              double *trace = nullptr);
+
+// A persistent solver for one QP at a time (the drop-in's per-tick QP_SETUP /
+// QP_SOLVE): one wave of the plan's row or wave kernel, compiled with QPB_SERVE,
+// stays resident and solves whenever the host posts a request in a mailbox in
+// mapped pinned memory, so a solve costs no launch and no stream synchronisation.
+// The kernel leaves by itself after `idle` without a request (and on a stop
+// request); the host relaunches it when it finds it gone.  Its arguments (data
+// pointers, settings) are fixed per launch: a call with different ones stops it
+// and launches anew.
+struct Server {
+    std::string kname;                   // code object of the running launch
+    KernelArgs args{};
+    void *stream = nullptr;              // its own non-blocking stream
+    unsigned long long *mb = nullptr;    // mailbox: [0] request, [16] answer, [32] its device ticks (host address)
+    unsigned long long *mb_dev = nullptr;
+    unsigned long long seq = 0;          // last request posted
+    bool running = false;                // launched and not seen to end
+    long requests = 0, launches = 0;
+    unsigned long long dev_ticks = 0;    // the last answer: 100 MHz ticks from request seen to answer
+    Server() = default;
+    Server(const Server &) = delete;
+    Server &operator=(const Server &) = delete;
+    ~Server();                           // stops the kernel, frees the mailbox and stream
+};
+constexpr int SERVE_NONE = 1;            // serve_ex: this plan's one-QP kernel has no persistent form
+// One QP (B = 1, the tiled slot of QP 0) through `srv`: returns once the results are
+// in x .. trace.  SERVE_NONE when the plan's kernel for one QP is neither the row
+// nor the wave form (the caller launches instead).
+int serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A, const double *G, const double *c,
+             const double *h, const double *b, const qpb_settings *st, double *x, double *y, double *z, double *s,
+             int *flag, int *iters, double *fval, double *stats, double *sig, bool warm, double *trace);
+// Stop the kernel (if running) and wait for it to leave; the mailbox stays.
+int serve_stop(Server *srv);
 }  // namespace qpb

@@ -328,11 +328,18 @@ static __device__ __forceinline__ long qpb_xcd_block() {
     return (nb & 7) ? (long)b : (long)(b & 7) * (nb >> 3) + (b >> 3);
 }
 
+#if QPB_SERVE
+// the persistent form (end of file) runs the body once per request, on QP 0
+static __device__ __forceinline__ void qpb_wave_body(const qpb_args &a, double *qpb_lds) {
+    const long qpb_blk = 0;
+#else
 extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * LDS_WAVE];
+    const long qpb_blk = qpb_xcd_block();
+#endif
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long q = qpb_xcd_block() * WPB + wv;
+    const long q = qpb_blk * WPB + wv;
     if (q >= a.B) return;                    // wave-uniform
     double *__restrict__ Ls = qpb_lds + wv * LDS_WAVE;
     const long tile = q >> 6;
@@ -1234,3 +1241,17 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     }
 #endif
 }
+
+#if QPB_SERVE
+// persistent form (the drop-in's QP_SOLVE, qpb::serve_ex): one wave, QP 0, one
+// solve per request posted in the mailbox (qpb_serve_wait, runtime prelude)
+extern "C" __global__ void __launch_bounds__(QPB_WG, 1)
+QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned long long idle) {
+    __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * LDS_WAVE];
+    unsigned long long t_seen = 0;
+    while (qpb_serve_wait(mb, &last, idle, &t_seen)) {
+        qpb_wave_body(a, qpb_lds);
+        qpb_serve_done(mb, last, t_seen);
+    }
+}
+#endif

@@ -53,6 +53,17 @@ void key_append(std::string &k, const long *v, long n) {
     k.push_back('|');
 }
 
+// QP_SETUP / QP_SOLVE through the workspace's persistent solvers (qpb::serve_ex;
+// zero-copy plans on the row or wave kernel).  QPSWIFT_HIP_SERVE=0: a launch and a
+// stream synchronisation per call instead.
+bool serve_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("QPSWIFT_HIP_SERVE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 struct Priv {
     PlanPtr plan;
     std::string err;
@@ -87,6 +98,7 @@ struct Priv {
     // reference's QP_SOLVE always does; otherwise its first QP_SOLVE is cold
     bool inited = false;
     const double *trace = nullptr;   // the last warm solve's trace (host copy, for verbose)
+    qpb::Server *srv = nullptr;      // the workspace's persistent solvers (cold, warm)
 };
 
 // Public struct first so that a QP* is also a Handle*.
@@ -190,6 +202,8 @@ PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const
         rc = raw->wave_ok && raw->kernel_pref != 1 ? qpb::compile_wave(raw) : qpb::compile_plan(raw);
         // QP_SOLVE continues from the QP's state: the warm-solve variant
         if (!rc) rc = qpb_plan_compile_warm(raw, 1);
+        // ... and the persistent forms the device solves go to (none: tree / lane)
+        if (!rc && serve_enabled() && qpb_plan_compile_serve(raw) < 0) rc = -1;
     }
     if (rc != 0) {
         err = qpb_last_error();
@@ -325,12 +339,16 @@ struct Workspace {
     double *zmem = nullptr;    // zero-copy slab: fine-grained pinned host memory the kernel reads / writes
     double *zdev = nullptr;    //   its device-side address
     long dcap = 0, hcap = 0, zcap = 0;   // doubles
+    // persistent solvers over the zero-copy slab: [0] QP_SETUP's initial point
+    // (cold, maxit 0), [1] QP_SOLVE (warm) -- qpb::serve_ex
+    qpb::Server srv[2];
     Workspace() = default;
     Workspace(const Workspace &) = delete;
     Workspace &operator=(const Workspace &) = delete;
     // released when the solving thread exits (a controller on pooled or
     // short-lived threads must not leak one stream + slabs per thread)
     ~Workspace() {
+        for (auto &sv : srv) (void)qpb::serve_stop(&sv);   // before the slab they read goes
         if (stream) {
             (void)hipStreamSynchronize(stream);
             (void)hipStreamDestroy(stream);
@@ -355,6 +373,7 @@ bool zero_copy_enabled() {
     return z;
 }
 thread_local std::map<int, Workspace> t_ws;
+
 
 bool zero_copy(const Priv &v) { return zero_copy_enabled() && !v.plan->gen.exact; }
 
@@ -407,6 +426,7 @@ int ensure_device(Priv &v, const QP &q) {
         w.hcap = hneed;
     }
     if (zero_copy(v) && w.zcap < v.ototal) {
+        for (auto &sv : w.srv) (void)qpb::serve_stop(&sv);
         if (w.zmem) (void)hipHostFree(w.zmem);
         w.zcap = 0;
         w.zdev = nullptr;
@@ -427,6 +447,7 @@ int ensure_device(Priv &v, const QP &q) {
     v.zmem = w.zmem;
     v.zdev = w.zdev;
     v.stream = w.stream;
+    v.srv = w.srv;
     return QPB_OK;
 }
 
@@ -536,11 +557,21 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
         h[osg] = q.options->sigma;
     }
     int *dfl = reinterpret_cast<int *>(d + ofl);
-    int rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
+    // the persistent solver answers without a launch; plans whose one-QP kernel has
+    // no persistent form (and QPSWIFT_HIP_SERVE=0) launch and synchronise
+    int rc = qpb::SERVE_NONE;
+    if (serve_enabled())
+        rc = qpb::serve_ex(v.plan.get(), &v.srv[cs.warm ? 1 : 0], d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG,
+                           d + v.oc, d + v.oh, p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr,
+                           d + v.oz, d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, d + osg, cs.warm, d + v.otr);
+    if (rc == qpb::SERVE_NONE) {
+        rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
                            p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz,
                            d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, nullptr, v.stream, d + osg, cs.warm,
                            d + v.otr);
-    if (hipStreamSynchronize(v.stream) != hipSuccess && !rc) rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: kernel failed");
+        if (hipStreamSynchronize(v.stream) != hipSuccess && !rc)
+            rc = qpb::set_error(QPB_EHIP, "QP_SOLVE: kernel failed");
+    }
     if (rc) return rc;
     std::vector<double> tmp((size_t)(n + p + 2 * m + 6));
     double *tx = tmp.data(), *ty = tx + n, *tz = ty + p, *ts = tz + m, *tst = ts + m;
@@ -799,5 +830,18 @@ qp_int QP_SOLVE(QP *myQP) {
 
 void QP_CLEANUP(QP *myQP) { release(myQP); }
 void QP_CLEANUP_dense(QP *myQP) { release(myQP); }
+
+int qpb_dropin_serve_stats(long out[4]) {
+    if (!out) return qpb::set_error(QPB_EINVAL, "NULL argument");
+    out[0] = out[1] = out[2] = out[3] = 0;
+    for (auto &kv : t_ws)
+        for (int k = 0; k < 2; k++) {
+            const qpb::Server &sv = kv.second.srv[k];
+            out[0] += sv.requests;
+            out[1] += sv.launches;
+            if (sv.dev_ticks) out[2 + k] = (long)sv.dev_ticks * 10;
+        }
+    return QPB_OK;
+}
 
 }  // extern "C"

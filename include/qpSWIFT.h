@@ -18,14 +18,21 @@
  *       (dense -> CSC drops exact zeros).  Like the reference (qpSWIFT.c:447),
  *       setup leaves kkt_initialize's point in x, y, z, s: one device launch
  *       (QPSWIFT_HIP_SETUP_INIT=0 skips it: x, y, z, s then stay zero until the
- *       first QP_SOLVE, which runs the initial point itself -- one launch per
- *       tick instead of two, at the price of that difference).
+ *       first QP_SOLVE, which runs the initial point itself -- one device solve
+ *       per tick instead of two, at the price of that difference).
  *   QP_SOLVE  continues from the QP object's state as the reference does
  *       (qpSWIFT.c:502-601): its x, y, z, s, stats->IterationCount, stats->Flag
  *       and options->sigma, at most options->maxit more iterations, QP_MAXIT only
- *       when IterationCount reaches exactly maxit; one launch of the plan's
- *       warm-solve kernel on the current HIP device, then x, y, z, s, the
- *       statistics and options->sigma are written back.  There is no CPU
+ *       when IterationCount reaches exactly maxit; the plan's warm-solve kernel
+ *       runs on the current HIP device, then x, y, z, s, the statistics and
+ *       options->sigma are written back.
+ *   Device solves (setup's initial point, QP_SOLVE) go to a persistent solver:
+ *       one resident wave per kind (cold / warm) and solving thread polls a
+ *       mailbox in mapped host memory, so a call costs no kernel launch and no
+ *       stream synchronisation; it leaves after QPSWIFT_HIP_SERVE_IDLE_MS
+ *       (default 20) without a call and is relaunched by the next one.  Plans
+ *       whose one-QP kernel is the tree or the exact lane kernel, and
+ *       QPSWIFT_HIP_SERVE=0, launch + synchronise per call.  There is no CPU
  *       fallback: without a usable GPU it returns QP_FATAL and qpb_last_error()
  *       says why.
  *   Arithmetic: by default the fast kernels (FMA, reciprocal pivots; the

@@ -133,6 +133,10 @@ int  qpb_plan_compile(qpb_plan *plan);
 /* The same for the warm-solve variant qpb_solve_warm launches for a batch of B
  * (compiled on first use otherwise). */
 int  qpb_plan_compile_warm(qpb_plan *plan, long B);
+/* Compile (or fetch from the code-object cache) the persistent forms of the plan's
+ * one-QP kernel that the drop-in's device solves use (include/qpSWIFT.h): 0, or 1
+ * when that kernel (tree or lane) has none. */
+int  qpb_plan_compile_serve(qpb_plan *plan);
 
 int  qpb_solve(qpb_plan *plan, long B,
                const double *P, const double *A, const double *G,
@@ -303,6 +307,12 @@ const char *qpb_compiler(void);
  * instruction's VGPR operand within 2 wait states or a VALU EXEC write within 5
  * (report says where), -1 cannot audit (no llvm-objdump). */
 int qpb_audit_dpp(const void *code, long size, char *report, long cap);
+/* The drop-in's persistent solvers on the calling thread (include/qpSWIFT.h):
+ * out[0] = device solves they answered, out[1] = kernel launches they took
+ * (first use, relaunch after an idle exit or new arguments), out[2] / out[3] =
+ * nanoseconds the resident wave spent on the last cold (setup) / warm (QP_SOLVE)
+ * request, from seeing it to posting the answer (s_memrealtime). */
+int qpb_dropin_serve_stats(long out[4]);
 
 #ifdef __cplusplus
 }

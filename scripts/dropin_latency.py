@@ -44,8 +44,10 @@ def main():
     # conversion costs ~4 us per array on this host, which the C controller does not pay
     args = [tuple(abi.dptr(X[t]) for X in (P, A, G, c, h, b)) for t in range(a.ticks)]
 
+    serve = (C.c_long * 4)()
+
     def run(lib):
-        lat, flags, xs, seg = [], [], [], []
+        lat, flags, xs, seg, dev = [], [], [], [], []
         for t in range(a.ticks):
             Pt, At, Gt, ct, ht, bt = args[t]
             t0 = time.perf_counter()
@@ -61,7 +63,11 @@ def main():
             lib.QP_CLEANUP_dense(qp)
             lat.append(time.perf_counter() - t0)
             seg.append((t1 - t0, t3 - t2))
+            if lib is L:                     # the resident wave's own time (persistent solver)
+                L.qpb_dropin_serve_stats(serve)
+                dev.append((serve[2], serve[3]))
         run.seg = np.median(np.array(seg), axis=0) * 1e6
+        run.dev = np.median(np.array(dev), axis=0) * 1e-3 if dev else None
         return np.array(lat), np.array(flags), np.array(xs)
 
     L = _lib.lib()
@@ -70,6 +76,9 @@ def main():
     out = dict(shape=a.shape, mode=a.mode, tol=a.tol, ticks=a.ticks, setup_init=a.setup_init, optimal=float((flags == 0).mean()),
                gpu_us_median=float(np.median(lat) * 1e6), gpu_us_p99=float(np.percentile(lat, 99) * 1e6),
                gpu_setup_us=float(run.seg[0]), gpu_solve_us=float(run.seg[1]))
+    L.qpb_dropin_serve_stats(serve)
+    out.update(serve_requests=int(serve[0]), serve_launches=int(serve[1]),
+               serve_dev_setup_us=float(run.dev[0]), serve_dev_solve_us=float(run.dev[1]))
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libqpswift_ref.so")
     if os.path.exists(ref_so):
         R = abi.bind_qpswift(C.CDLL(ref_so))
