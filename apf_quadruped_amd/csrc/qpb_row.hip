@@ -536,7 +536,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #endif
     int flag = flag0;
     for (;;) {
-        if (it >= 0 && it >= a.maxit) {
+        if ((QPB_WARM || it >= 0) && it >= a.maxit) {
             // qpSWIFT.c:598-601: QP_MAXIT only when IterationCount == maxit
             if (act) { itq = it0 + it; flag = (!QPB_WARM || itq == a.maxit) ? 2 : flag0; QPB_SIGF; }
             break;
@@ -583,7 +583,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #endif
         bool pc = true;
         double mu = 0.0;
-        if (it >= 0) {
+        if (QPB_WARM || it >= 0) {
             const double mu_it = sz * (1.0 / NZ);
 #if QPB_WARM
             {
@@ -638,7 +638,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             ap = bm[0] > 1e-10 ? __builtin_amdgcn_rcp(bm[0]) : 1.0;
             ad = bm[1] > 1e-10 ? __builtin_amdgcn_rcp(bm[1]) : 1.0;
         };
-        if (it < 0) {
+        if (!QPB_WARM && it < 0) {
             // setup solve, rhs [-c; b; h] (Auxilary.c:1010-1040): x0, y0; then
             // s0, z0 from r = h - G x0 = -dz (w = 1 exactly here)
             solve(w0, w1, -cx, by, hz0, hz1, dx, dy, dz0, dz1);

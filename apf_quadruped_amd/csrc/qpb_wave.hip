@@ -330,15 +330,16 @@ static __device__ __forceinline__ long qpb_xcd_block() {
 
 #if QPB_SERVE
 // the persistent form (end of file) runs the body once per request, on QP 0
-static __device__ __forceinline__ void qpb_wave_body(const qpb_args &a, double *qpb_lds) {
+static __device__ __forceinline__ void qpb_wave_body(const qpb_args &a, double *qpb_lds, unsigned qpb_tid) {
     const long qpb_blk = 0;
 #else
 extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args a) {
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * LDS_WAVE];
     const long qpb_blk = qpb_xcd_block();
+    const unsigned qpb_tid = threadIdx.x;
 #endif
-    const int lane = threadIdx.x & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = qpb_tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(qpb_tid >> 6);
     const long q = qpb_blk * WPB + wv;
     if (q >= a.B) return;                    // wave-uniform
     double *__restrict__ Ls = qpb_lds + wv * LDS_WAVE;
@@ -979,7 +980,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     int flag = flag0;
     for (;;) {
         // qpSWIFT.c:598-601: QP_MAXIT only when IterationCount == maxit
-        if (it >= 0 && it >= a.maxit) { flag = (!QPB_WARM || it0 + it == a.maxit) ? 2 : flag0; break; }
+        if ((QPB_WARM || it >= 0) && it >= a.maxit) { flag = (!QPB_WARM || it0 + it == a.maxit) ? 2 : flag0; break; }
         QPB_TS(it >= 0 ? 8 + 8 * it : 2);
         // updatekktmatrix (Auxilary.c:211-215): z diagonal -s/z.  The setup
         // system has -I there, which is this with s = z = 1 (iteration -1).
@@ -1053,7 +1054,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             qpb_rsum_n<ROWS_R>(red);
             if (QPB_W_TIMING && it == 1) QPB_TS(366);
             sz = red[3];
-            if (it >= 0) {
+            if (QPB_WARM || it >= 0) {
                 fv = isx ? x * __builtin_fma(-0.5, tp, cx) : 0.0;      // summed at exit
                 st_rx2 = red[0];
                 st_ry2 = NY > 0 ? red[1] : 0.0;
@@ -1073,7 +1074,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             }
         }
 #endif
-        if (it >= 0) {
+        if (QPB_WARM || it >= 0) {
             if (st_rx2 < tol2 && st_rz2 < tol2 && (NY == 0 || st_ry2 < tol2) && st_mu < a.abstol) {
                 flag = (QPB_WARM && it0 + it == a.maxit) ? 2 : 0;
                 break;
@@ -1114,7 +1115,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         // pass 2: setup solve, rhs [-c; b; h]; pass 0: predictor (kktsolve_1,
         // Auxilary.c:471-515), ds = -s.*z; pass 1: corrector / centering
         // (kktsolve_2, Auxilary.c:524-564)
-        int pass = it < 0 ? 2 : (pc ? 0 : 1);
+        int pass = (!QPB_WARM && it < 0) ? 2 : (pc ? 0 : 1);
         for (;;) {
             double bxv = rx, byv = ry, bz[ZC];
 #pragma unroll
@@ -1250,7 +1251,11 @@ QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned l
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * LDS_WAVE];
     unsigned long long t_seen = 0;
     while (qpb_serve_wait(mb, &last, idle, &t_seen)) {
-        qpb_wave_body(a, qpb_lds);
+        // a fresh lane index per request: nothing derived from it is hoisted out of
+        // this loop (that would hold extra registers through the solve)
+        unsigned tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        qpb_wave_body(a, qpb_lds, tid);
         qpb_serve_done(mb, last, t_seen);
     }
 }
