@@ -203,7 +203,10 @@ static __device__ __forceinline__ void qpb_run(const int *ms, int nsteps, const 
                                                const D *__restrict__ desc, Term term, Pre pre, Post post,
                                                Panel panel) {
     if (nsteps <= 0) return;
-    const int l = threadIdx.x;
+    // the lane index, opaque here: the per-lane table addresses below are formed per
+    // run instead of being hoisted out of the IPM loop and held (spilled) across it
+    int l = threadIdx.x;
+    asm volatile("" : "+v"(l));
     qpb_set<D> A, B;
     auto prefetch = [&](int st, qpb_set<D> &S) {
         st = st < nsteps ? st : nsteps - 1;
@@ -531,7 +534,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
 #if QPB_T_MSLDS
     __shared__ __attribute__((aligned(16))) int MS[QPB_MS_TOTAL];
 #endif
-    const int t = threadIdx.x;
+    int t = threadIdx.x;                         // opaque at every stage (the loop below)
     const long q = qpb_xcd_block();
     if (q >= a.B) return;                        // workgroup-uniform
     const long tile = q >> 6;
@@ -763,6 +766,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
 #endif
     int flag = flag0;
     for (;;) {
+        // masks and addresses derived from the lane index are formed where used, not
+        // hoisted out of the loop (held across it they spill)
+        asm volatile("" : "+v"(t));
         if (stage == ST_INITZ || stage == ST_TOP) {
             if (stage == ST_TOP && it >= a.maxit) break;
             products(V);
