@@ -15,6 +15,8 @@
 // samples generated on the device never round-trip through the host.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <cstring>
 #include <string>
 #include <vector>
@@ -423,21 +425,34 @@ extern "C" int qpb_assemble_controller(const qpb_plan *plan_c, long B, const dou
     qpb_plan *plan = const_cast<qpb_plan *>(plan_c);
     if (!plan) return qpb::set_error(QPB_EINVAL, "NULL plan");
     if (B < 0) return qpb::set_error(QPB_EINVAL, "need B >= 0");
-    if (plan->ctl_table.empty()) plan->ctl_table = controller_entries(plan->pl);
-    if (plan->ctl_table.empty()) return qpb::set_error(QPB_ESHAPE, "plan is not a 30/68/18 controller stance QP");
-    if (B == 0) return QPB_OK;
-    if (!terms || !P || !A || !G || !c || !h || !b) return qpb::set_error(QPB_EINVAL, "NULL data pointer");
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return qpb::set_error(QPB_EHIP, "hipGetDevice failed (no GPU?)");
-    void *&tab = plan->ctl_dev[dev];
-    if (!tab) {
-        const size_t bytes = plan->ctl_table.size() * sizeof(int);
-        if (hipMalloc(&tab, bytes) != hipSuccess) { tab = nullptr; return qpb::set_error(QPB_ENOMEM, "assembly table"); }
-        if (hipMemcpy(tab, plan->ctl_table.data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
-            return qpb::set_error(QPB_EHIP, "assembly table upload");
+    // the plan's entry table (host, then per device) is built once, under a lock:
+    // concurrent callers on one plan must not build or upload it twice
+    void *tab = nullptr;
+    size_t nent = 0;
+    {
+        static std::mutex mu;
+        std::lock_guard<std::mutex> lk(mu);
+        if (plan->ctl_table.empty()) plan->ctl_table = controller_entries(plan->pl);
+        if (plan->ctl_table.empty()) return qpb::set_error(QPB_ESHAPE, "plan is not a 30/68/18 controller stance QP");
+        if (B == 0) return QPB_OK;
+        if (!terms || !P || !A || !G || !c || !h || !b) return qpb::set_error(QPB_EINVAL, "NULL data pointer");
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return qpb::set_error(QPB_EHIP, "hipGetDevice failed (no GPU?)");
+        nent = plan->ctl_table.size();
+        auto it = plan->ctl_dev.find(dev);
+        if (it != plan->ctl_dev.end()) tab = it->second;
+        else {
+            const size_t bytes = nent * sizeof(int);
+            if (hipMalloc(&tab, bytes) != hipSuccess) return qpb::set_error(QPB_ENOMEM, "assembly table");
+            if (hipMemcpy(tab, plan->ctl_table.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+                (void)hipFree(tab);     // nothing half-uploaded stays in the cache
+                return qpb::set_error(QPB_EHIP, "assembly table upload");
+            }
+            plan->ctl_dev[dev] = tab;
+        }
     }
     const qpb::Plan &pl = plan->pl;
-    CtlArgs a{terms, terms_shared ? 0L : 1L, wdes, (const int *)tab, (int)(plan->ctl_table.size() / 2),
+    CtlArgs a{terms, terms_shared ? 0L : 1L, wdes, (const int *)tab, (int)(nent / 2),
               (int)pl.Pin.nnz(), (int)pl.A.nnz(), (int)pl.G.nnz(), mu, P, A, G, c, h, b, check, B};
     if (check)
         hipLaunchKernelGGL(qpb_fill_int_k, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, check,

@@ -58,7 +58,10 @@ enum Ordering : int {
     ORDER_MINDEG = 1,   // own exact minimum degree, lowest-index ties
     ORDER_AMD = 2,      // the reference's AMD (amd_l_order with amd_l_defaults): Permut = NULL
     ORDER_LEAVES = 3,   // own: z rows, y rows, then x in natural order (small QPs)
-    ORDER_OWN = 4,      // request only: ORDER_LEAVES for n, p <= 16, m <= 32, else ORDER_MINDEG
+    ORDER_OWN = 4,      // request only: ORDER_LEAVES for n, p <= 64, m <= 256 (the wave kernel's
+                        // range: its dense block is then the x block), else ORDER_MINDEG.  A plan
+                        // in that range that a large batch sends to the lane or tree kernel also
+                        // gets the dense x block (more fill than minimum degree; not measured)
 };
 
 // amd_l_order's status codes (include/qpSWIFT/amd.h): OK, OK but the columns were
