@@ -426,8 +426,8 @@ def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
 
 def limiter_for(B):
     """What the SQ counters say bounds the row kernel at this batch
-    (profiles/r02_sq_row.json, scripts/gpu_sq.sh + scripts/sq_summary.py)."""
-    f = os.path.join(ROOT, "profiles", "r02_sq_row.json")
+    (profiles/r03_sq_row.json, scripts/gpu_sq.sh + scripts/sq_summary.py)."""
+    f = os.path.join(ROOT, "profiles", "r03_sq_row.json")
     if not os.path.exists(f):
         return None
     r = json.load(open(f)).get(f"B={B}")
@@ -437,7 +437,7 @@ def limiter_for(B):
     return {"kind": r.get("kind", "VALU issue + LDS/memory latency (neither HBM nor FP64 peak)"),
             "valu_active_frac": fr["valu_active"], "waitcnt_frac": fr["wait_any (s_waitcnt: LDS / memory)"],
             "waves_per_simd": r["waves_per_simd_avg"], "fp64_lane_fma_per_qp": r["per_qp"]["fma_f64_lane_ops"],
-            "source": "profiles/r02_sq_row.json"}
+            "source": "profiles/r03_sq_row.json"}
 
 
 def controller_apf_leg(dev, K=8192, steps=20, warmup=3):

@@ -5,4 +5,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeou
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; fatal $rc smoke
 timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -c 1500 gpurun_out/bench.log; fatal $rc bench
 rm -rf gpurun_out/prof; timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 200 --no-cpu > gpurun_out/prof.log 2>&1; rc=$?; echo "rocprof rc=$rc"; fatal $rc rocprof
-find gpurun_out/prof -name "*kernel_stats.csv" | head -3
+python3 scripts/prof_summary.py gpurun_out/prof/run_results.db gpurun_out/kernel_by_grid.csv gpurun_out/kernel_stats.csv > /dev/null && head -8 gpurun_out/kernel_stats.csv
