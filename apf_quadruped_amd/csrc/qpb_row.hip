@@ -54,6 +54,14 @@ struct qpb_args {
 #ifndef QPB_R_LATEFAC
 #define QPB_R_LATEFAC 1   // factor after the exit test (0: before it, overlapping the reductions)
 #endif
+#ifndef QPB_R_REGH0
+#if defined(QPB_R_WPE) && QPB_R_WPE > 1
+#define QPB_R_REGH0 0     // two-wave form: <= 256 registers, H0 / -P rows stay in LDS
+#else
+#define QPB_R_REGH0 0     // 1: the lane's H0 and -P rows held in registers (no LDS
+                          // round trip at the start of every factor and residual pass)
+#endif
+#endif
 #ifndef QPB_R_ALIAS
 #define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
 #endif
@@ -389,8 +397,8 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #pragma unroll
     for (int l = 0; l < NY1; l++) nAc[l] = (isx && NY > 0) ? -Ad[ix * NY + l] : 0.0;
     // H0 = P (upper triangle, symmetrised) + 1e7 A'A (the leaf y rows folded into the x block)
+    double nP[NX], H0[NX];
     {
-        double nP[NX], H0[NX];
 #pragma unroll
         for (int j = 0; j < NX; j++) {
             nP[j] = -Pd[j * NX + ix];
@@ -410,7 +418,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             qpb_for<0, NX>([&](auto jc) { qpb_fx<decltype(jc)::value>(H0[decltype(jc)::value], qs, -nAc[l]); });
         }
 #endif
-        if (isx) {
+        if (!QPB_R_REGH0 && isx) {
 #pragma unroll
             for (int j = 0; j < NX; j++) { PR[c * NX + j] = nP[j]; H0s[c * NX + j] = H0[j]; }
         }
@@ -423,7 +431,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     // then the LDL' of H (rows of -L in H, 1/D in rDd), -L transposed into Lt
     auto factor = [&](double w0, double w1) {
 #pragma unroll
-        for (int e = 0; e < NX; e++) H[e] = H0s[ix * NX + e];
+        for (int e = 0; e < NX; e++) H[e] = QPB_R_REGH0 ? H0[e] : H0s[ix * NX + e];
         qpb_for<0, NZ>([&](auto rc) {
             constexpr int r = decltype(rc)::value;
             const double wr = r < 16 ? qpb_nb<(r & 15)>(w0) : qpb_nb<(r & 15)>(w1);
@@ -550,7 +558,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         qpb_fence(x, y, z0, z1);
         double tp = 0.0, ry = by, rz0 = hz0 - s0, rz1 = hz1 - s1, nPr[NX];
 #pragma unroll
-        for (int j = 0; j < NX; j++) nPr[j] = PR[ix * NX + j];
+        for (int j = 0; j < NX; j++) nPr[j] = QPB_R_REGH0 ? nP[j] : PR[ix * NX + j];
         qpb_for<0, NX>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
             qpb_fx<j>(rz0, x, nGl[j]);
