@@ -795,10 +795,12 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 // persistent form (the drop-in's QP_SOLVE, qpb::serve_ex): one wave, QP 0, one
 // solve per request posted in the mailbox (qpb_serve_wait, runtime prelude)
 extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_R_WPE)
-QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned long long idle) {
+QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned long long idle,
+                unsigned long long life) {
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * 4 * LDS_ROW];
+    const unsigned long long t_launch = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_seen = 0;
-    while (qpb_serve_wait(mb, &last, idle, &t_seen)) {
+    while (qpb_serve_wait(mb, &last, idle, life, t_launch, &t_seen)) {
         qpb_row_body(a, 0, 0, qpb_lds);
         qpb_serve_done(mb, last, t_seen);
     }

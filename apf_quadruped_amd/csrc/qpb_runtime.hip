@@ -541,7 +541,12 @@ static __device__ __forceinline__ unsigned long long qpb_uniform64(unsigned long
     const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
     return ((unsigned long long)hi << 32) | lo;
 }
+// idle: ticks without a request before leaving; life: ticks since the launch
+// (t_launch) after which the wave leaves at its next idle moment, so that work
+// queued behind it on a shared hardware queue (more streams than queues) waits
+// at most that long
 static __device__ bool qpb_serve_wait(qpb_mailbox *mb, unsigned long long *last, unsigned long long idle,
+                                      unsigned long long life, unsigned long long t_launch,
                                       unsigned long long *t_seen) {
     unsigned long long *req = (unsigned long long *)mb;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -554,7 +559,8 @@ static __device__ bool qpb_serve_wait(qpb_mailbox *mb, unsigned long long *last,
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
             return true;
         }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > idle) return false;
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        if (now - t0 > idle || now - t_launch > life) return false;
         __builtin_amdgcn_s_sleep(4);
     }
 }
@@ -965,12 +971,17 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
 // ---- persistent one-QP solver (qpb::Server) ---------------------------------
 namespace {
 constexpr unsigned long long kStop = ~0ull;
-unsigned long long serve_idle_ticks() {      // s_memrealtime ticks (100 MHz)
-    static const unsigned long long t = [] {
-        const char *e = getenv("QPSWIFT_HIP_SERVE_IDLE_MS");
-        const double ms = e ? atof(e) : 20.0;
-        return (unsigned long long)(std::max(0.1, std::min(ms, 1000.0)) * 1e5);
-    }();
+unsigned long long ms_ticks(const char *env, double dflt) {     // s_memrealtime ticks (100 MHz)
+    const char *e = getenv(env);
+    const double ms = e ? atof(e) : dflt;
+    return (unsigned long long)(std::max(0.1, std::min(ms, 10000.0)) * 1e5);
+}
+unsigned long long serve_idle_ticks() {
+    static const unsigned long long t = ms_ticks("QPSWIFT_HIP_SERVE_IDLE_MS", 20.0);
+    return t;
+}
+unsigned long long serve_life_ticks() {
+    static const unsigned long long t = ms_ticks("QPSWIFT_HIP_SERVE_LIFE_MS", 10.0);
     return t;
 }
 unsigned long long mb_load(const unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
@@ -1055,9 +1066,9 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
         return rc;
     unsigned long long *req = srv->mb, *ack = srv->mb + 16;
     auto launch = [&](unsigned long long last) {
-        unsigned long long idle = serve_idle_ticks();
+        unsigned long long idle = serve_idle_ticks(), life = serve_life_ticks();
         void *mbd = srv->mb_dev;
-        void *params[] = {&a, &mbd, &last, &idle};
+        void *params[] = {&a, &mbd, &last, &idle, &life};
         const hipError_t e = hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, sm, params, nullptr);
         if (e != hipSuccess) return fail(QPB_EHIP, std::string("persistent solver launch: ") + hipGetErrorString(e));
         srv->running = true;

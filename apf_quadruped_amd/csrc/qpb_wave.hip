@@ -1247,10 +1247,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 // persistent form (the drop-in's QP_SOLVE, qpb::serve_ex): one wave, QP 0, one
 // solve per request posted in the mailbox (qpb_serve_wait, runtime prelude)
 extern "C" __global__ void __launch_bounds__(QPB_WG, 1)
-QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned long long idle) {
+QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned long long idle,
+                unsigned long long life) {
     __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * LDS_WAVE];
+    const unsigned long long t_launch = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_seen = 0;
-    while (qpb_serve_wait(mb, &last, idle, &t_seen)) {
+    while (qpb_serve_wait(mb, &last, idle, life, t_launch, &t_seen)) {
         // a fresh lane index per request: nothing derived from it is hoisted out of
         // this loop (that would hold extra registers through the solve)
         unsigned tid = threadIdx.x;

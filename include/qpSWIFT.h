@@ -30,7 +30,9 @@
  *       one resident wave per kind (cold / warm) and solving thread polls a
  *       mailbox in mapped host memory, so a call costs no kernel launch and no
  *       stream synchronisation; it leaves after QPSWIFT_HIP_SERVE_IDLE_MS
- *       (default 20) without a call and is relaunched by the next one.  Plans
+ *       (default 20) without a call, or at its first idle moment after
+ *       QPSWIFT_HIP_SERVE_LIFE_MS (default 10: work queued behind it on a shared
+ *       hardware queue waits no longer), and is relaunched by the next call.  Plans
  *       whose one-QP kernel is the tree or the exact lane kernel, and
  *       QPSWIFT_HIP_SERVE=0, launch + synchronise per call.  There is no CPU
  *       fallback: without a usable GPU it returns QP_FATAL and qpb_last_error()

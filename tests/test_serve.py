@@ -97,3 +97,31 @@ def test_served_alternating_patterns():
             _check(_solve(g, q), g, q, name)
             r = _solve(g, q, null_perm=True)
             assert r["flag"] == int(g["flag"][q]), (name, r["error"])
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(os.environ.get("QPSWIFT_HIP_SERVE") == "0", reason="persistent solver switched off")
+def test_served_solvers_per_thread():
+    """Two solving threads at once (C1 and C30 stance): each thread's workspace has
+    its own resident solvers, mailboxes and slab, so concurrent ticks neither block
+    nor mix up each other's results."""
+    import threading
+    gs = {"c1": golden("c1_tol1e-2"), "c30": golden("c30_tol1e-2")}
+    errors = []
+
+    def worker(name):
+        try:
+            g = gs[name]
+            for rnd in range(6):
+                q = rnd % g["x"].shape[0]
+                _check(_solve(g, q), g, q, name)
+        except Exception as e:            # surfaced below: pytest sees only the main thread
+            errors.append(f"{name}: {e!r}")
+
+    ts = [threading.Thread(target=worker, args=(n,)) for n in gs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ts), "a solving thread hung"
+    assert not errors, errors
