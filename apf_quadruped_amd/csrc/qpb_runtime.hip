@@ -557,6 +557,10 @@ static __device__ bool qpb_serve_wait(qpb_mailbox *mb, unsigned long long *last,
             *last = r;
             *t_seen = __builtin_amdgcn_s_memrealtime();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            // the fence's L1 invalidate completes asynchronously: wait for it before the
+            // body's first load, or lines this CU read for the previous request (the
+            // zero-copy slab, re-read every request) can be served stale
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             return true;
         }
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
@@ -573,11 +577,23 @@ static __device__ void qpb_serve_done(qpb_mailbox *mb, unsigned long long r, uns
 }
 )QPBS";
 
-// a variant of a plan's kernel: `<kname>_w` (warm), `_s` (persistent cold) or `_ws`
-// (persistent warm) -- its source with QPB_WARM / QPB_SERVE set, under that name
+// a variant's name: `<kname>_w` (warm), `_s<tag>` (persistent cold) or `_ws<tag>`
+// (persistent warm); the persistent forms carry a hash of the prelude they are
+// built with, so a changed prelude never reuses a cached code object
+static std::string variant_name(const std::string &kname, bool warm, bool serve) {
+    static const std::string tag = [] {
+        char t[9];
+        snprintf(t, sizeof t, "%08x", (unsigned)(fnv1a(kServePrelude) & 0xffffffffu));
+        return std::string(t);
+    }();
+    return kname + (warm ? (serve ? "_ws" : "_w") : "_s") + (serve ? tag : std::string());
+}
+
+// a variant of a plan's kernel -- its source with QPB_WARM / QPB_SERVE set, under
+// variant_name()
 int compile_variant(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src,
                            bool exact, bool warm, bool serve, std::shared_ptr<std::vector<char>> **slot) {
-    const std::string vname = kname + (warm ? (serve ? "_ws" : "_w") : "_s");
+    const std::string vname = variant_name(kname, warm, serve);
     {
         std::lock_guard<std::mutex> lk(g_warm_mu);
         *slot = &plan->warm_code[vname];     // std::map nodes are stable
@@ -1020,7 +1036,7 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
     std::shared_ptr<std::vector<char>> *slot = nullptr;
     int rc = compile_variant(plan, plan->wave_kname, [plan] { return qpb::wave_source_of(plan); }, false, warm, true,
                              &slot);
-    const std::string kn = plan->wave_kname + (warm ? "_ws" : "_s");
+    const std::string kn = variant_name(plan->wave_kname, warm, true);
     hipFunction_t fn;
     if (!rc) rc = load_function(kn, *slot, &fn);
     if (rc) return rc;

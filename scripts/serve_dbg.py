@@ -1,0 +1,16 @@
+"""Drop-in trot golden, QP by QP: iterations and max |x - golden| with the
+persistent solver, in file order and QP 1 alone first (debug of a mismatch)."""
+import os, sys, json
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from apf_quadruped_amd import dropin
+g = np.load(os.path.join(ROOT, "tests/golden/mixed_trot_brfl.npz"))
+n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
+tol, maxit = float(g["tol"]), int(g["maxit"])
+order = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else list(range(g["x"].shape[0]))
+for q in order:
+    r = dropin.solve_dense(n, m, p, g["P"][q], g["A"][q], g["G"][q], g["c"][q], g["h"][q], g["b"][q],
+                           ordering=int(g["ordering"]), reltol=tol, abstol=tol, maxit=maxit)
+    print(json.dumps({"q": q, "flag": r["flag"], "iters": r["iters"], "g_iters": int(g["iters"][q]),
+                      "dx": float(np.abs(r["x"] - g["x"][q]).max()), "dz": float(np.abs(r["z"] - g["z"][q]).max())}))
