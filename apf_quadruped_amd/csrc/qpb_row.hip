@@ -62,6 +62,11 @@ struct qpb_args {
                           // round trip at the start of every factor and residual pass)
 #endif
 #endif
+#ifndef QPB_R_LAZYREG
+#define QPB_R_LAZYREG 0   // 1: pivot regularisation checked once per factor, the factor redone only
+                          // when needed (measured: 1 024 QPs 32.7 vs 32.9 us, no gain; the two-wave
+                          // form spills 34 more registers with it)
+#endif
 #ifndef QPB_R_ALIAS
 #define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
 #endif
@@ -92,6 +97,12 @@ static __device__ __forceinline__ double qpb_rcp_reg(double d) {
     asm("" : "+v"(r));     // keeps the rare regularised case from becoming a branch
     const double reg = d > 0.0 ? 1e7 : -1e7;
     return __builtin_fabs(d) <= 1e-14 ? reg : r;
+}
+
+// the same 1/d without the regularisation select (QPB_R_LAZYREG's fast pass)
+static __device__ __forceinline__ double qpb_rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    return __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
 }
 
 template <int J0, int J1, class F> static __device__ __forceinline__ void qpb_for(F &&f) {
@@ -428,8 +439,14 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     QPB_TM(0);
     double H[NX], rDd = 0.0;
     // factor with z diagonal kd: H = H0 + G' diag(w) G, w = -1/regularise(kd),
-    // then the LDL' of H (rows of -L in H, 1/D in rDd), -L transposed into Lt
-    auto factor = [&](double w0, double w1) {
+    // then the LDL' of H (rows of -L in H, 1/D in rDd), -L transposed into Lt.
+    // Pivot regularisation off the pivot chain (QPB_R_LAZYREG): the fast pass takes
+    // every 1/D as v_rcp_f64 + Newton and tracks min |D|; only when some pivot is
+    // <= 1e-14 (ldl.c:273-274) is the factor redone with the regularised reciprocal
+    // -- the same operations as the fast pass otherwise, so the same bits.
+    auto factor_core = [&](double w0, double w1, auto regc) -> double {
+        constexpr bool REG = decltype(regc)::value != 0;
+        double dmin = __builtin_huge_val();
 #pragma unroll
         for (int e = 0; e < NX; e++) H[e] = QPB_R_REGH0 ? H0[e] : H0s[ix * NX + e];
         qpb_for<0, NZ>([&](auto rc) {
@@ -447,7 +464,13 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         double dpiv = qpb_nb<0>(H[0]);
         qpb_for<0, NX>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            const double rd = qpb_rcp_reg(dpiv);
+            double rd;
+            if constexpr (REG || !QPB_R_LAZYREG) {
+                rd = qpb_rcp_reg(dpiv);
+            } else {
+                rd = qpb_rcp_nr(dpiv);
+                dmin = __builtin_fmin(dmin, __builtin_fabs(dpiv));
+            }
             if constexpr (k + 1 < NX) {
                 const double h = qpb_nb<k + 1>(H[k]), hkk = qpb_nb<k + 1>(H[k + 1]);
                 dpiv = __builtin_fma(h, h * -rd, hkk);
@@ -460,6 +483,11 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             });
             H[k] = c > k ? nl : 0.0;
         });
+        return dmin;
+    };
+    auto factor = [&](double w0, double w1) {
+        const double dmin = factor_core(w0, w1, qpb_ic<0>{});
+        if (QPB_R_LAZYREG && qpb_any(dmin <= 1e-14)) factor_core(w0, w1, qpb_ic<1>{});   // wave-uniform, rare
         // column c of -L, contiguous for lane c: Tx[c*NX + k] = -L(k, c)
         if (isx) {
 #pragma unroll

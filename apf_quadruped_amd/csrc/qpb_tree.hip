@@ -405,11 +405,23 @@ template <int J> static __device__ __forceinline__ double qpb_nb(double v) {
 // Off in the 192-thread form (168 registers for three waves per SIMD): there it
 // spills more (148 vs 108 B of scratch per lane) for the same time, and the spill
 // traffic of 1 024 MPC QPs grows from 93 to 166 MB written per launch.
+// a pivot reciprocal: regularised (REG), or v_rcp_f64 + Newton with min |d| tracked
+// for the caller's one check per factor (QPB_T_LAZYREG)
+template <bool REG> static __device__ __forceinline__ double qpb_piv_rcp(double d, double &dmin) {
+    if constexpr (REG) return qpb_rcp_reg(d);
+    dmin = __builtin_fmin(dmin, __builtin_fabs(d));
+    return qpb_rcp(d);
+}
+#ifndef QPB_T_LAZYREG
+#define QPB_T_LAZYREG 0   // 1: measured slower on 1 024 MPC QPs (1.48 vs 1.46 ms: 3 spilled registers)
+#endif
+
 #ifndef QPB_T_PDUP
 #define QPB_T_PDUP (QPB_WG != 192)
 #endif
-template <int W>
-static __device__ __forceinline__ void qpb_pfac(double *__restrict__ L, const int *__restrict__ rec, int lane) {
+template <int W, bool REG>
+static __device__ __forceinline__ void qpb_pfac(double *__restrict__ L, const int *__restrict__ rec, int lane,
+                                                double &dmin) {
     const int j0 = rec[0], R = rec[2];
     const int *lp = rec + 3;
     if constexpr (QPB_T_PDUP && W <= 16) {
@@ -424,7 +436,7 @@ static __device__ __forceinline__ void qpb_pfac(double *__restrict__ L, const in
             double myr = 0.0;
             qpb_tfor<0, W>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
-                const double rk = qpb_rcp_reg(qpb_nb<k>(P[k]));
+                const double rk = qpb_piv_rcp<REG>(qpb_nb<k>(P[k]), dmin);
                 myr = pr == k ? rk : myr;
                 const double f = -P[k] * rk;
                 qpb_tfor<k + 1, W>([&](auto cc) {
@@ -447,7 +459,7 @@ static __device__ __forceinline__ void qpb_pfac(double *__restrict__ L, const in
     double myr = 0.0;
 #pragma unroll
     for (int k = 0; k < W; k++) {
-        const double rk = qpb_rcp_reg(qpb_rl(P[k], k));
+        const double rk = qpb_piv_rcp<REG>(qpb_rl(P[k], k), dmin);
         myr = lane == k ? rk : myr;
         const double f = -P[k] * rk;
 #pragma unroll
@@ -616,7 +628,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
         }
         __syncthreads();
     };
-    auto factor = [&]() {
+    // QPB_T_LAZYREG: the panel pivots skip the regularisation select and track min |D|;
+    // the caller re-assembles and refactors with it only when some panel pivot is
+    // <= 1e-14 (ldl.c:273-274) -- otherwise the same operations, so the same bits
+    auto factor = [&](auto regc) -> double {
+        constexpr bool REG = decltype(regc)::value != 0 || !QPB_T_LAZYREG;
+        double dmin = __builtin_huge_val();
         QPB_TIC();
         qpb_run(QPB_STEPS(fac, FAC), QPB_fac_NSTEPS, TI + QPB_I_fac_hdr, TD + QPB_D_fac,
                 [&](double acc, unsigned long long d) {
@@ -636,13 +653,14 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
                     for (int i = threadIdx.x >> 6; i < count; i += NW) {
                         const int *rec = SN + SN[list + i];
                         switch (rec[1]) {
-#define QPB_PF(w) case w: qpb_pfac<w>(L, rec, threadIdx.x & 63); break;
+#define QPB_PF(w) case w: qpb_pfac<w, REG>(L, rec, threadIdx.x & 63, dmin); break;
                             QPB_PANEL_WIDTHS(QPB_PF)
 #undef QPB_PF
                         }
                     }
                 });
         QPB_TOC(tm_fac);
+        return dmin;
     };
     // W (permuted rhs) -> W (permuted solution)
     auto solve = [&]() {
@@ -863,8 +881,15 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
 #if QPB_WARM
         const long tk0 = QPB_CLK();
 #endif
-        if (fac) factor();                // its level barriers order the rhs before the solve
-        else __syncthreads();
+        if (fac) {                        // its level barriers order the rhs before the solve
+            const double dm = factor(qpb_tic<0>{});
+            if (QPB_T_LAZYREG && __syncthreads_or(dm <= 1e-14)) {     // a tiny panel pivot: rare
+                assemble(stage == ST_INIT ? qpb_asrc_i : qpb_asrc_l);
+                factor(qpb_tic<1>{});
+            }
+        } else {
+            __syncthreads();
+        }
 #if QPB_WARM
         const long tk1 = QPB_CLK();
         if (fac) t_fac += tk1 - tk0;

@@ -52,6 +52,9 @@ struct qpb_args {
 #ifndef QPB_W_GG           // 1: G(r,i)G(r,j) products in registers; 0: recompute from LDS
 #define QPB_W_GG (QPB_NNZG <= 48)
 #endif
+#ifndef QPB_W_LAZYREG      // 1: pivot regularisation checked once per factor (redone only when needed);
+#define QPB_W_LAZYREG 0    // off: AMD-ordered plans regularise their y pivots in most factors, so the
+#endif                     // factor ran twice (controller call batched 2.73 -> 24.7 ms, C30 tick 335 -> 520 us)
 #ifndef QPB_W_MFMA         // 1: the leaf z rows' G'diag(w)G as an MFMA GEMM (v_mfma_f64_16x16x4f64)
 #define QPB_W_MFMA (!QPB_W_GG && QPB_NX <= 64)
 #endif
@@ -298,6 +301,15 @@ static __device__ __forceinline__ double qpb_rcp_reg(double d) {
     return __builtin_fabs(d) <= 1e-14 ? reg : r;
 }
 
+// a pivot reciprocal: regularised (REG), or v_rcp_f64 + Newton with min |d| tracked
+// for the caller's one check per factor (QPB_W_LAZYREG)
+template <bool REG> static __device__ __forceinline__ double qpb_piv_rcp(double d, double &dmin) {
+    if constexpr (REG) return qpb_rcp_reg(d);
+    dmin = __builtin_fmin(dmin, __builtin_fabs(d));
+    const double r = __builtin_amdgcn_rcp(d);
+    return __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+}
+
 template <int J0, int J1, class F> static __device__ __forceinline__ void qpb_for(F &&f) {
     if constexpr (J0 < J1) {
         f(qpb_ic<J0>{});
@@ -515,7 +527,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     // after a wsync: H = H0 + G_L' W G_L, then the right-looking LDL' of the
     // dense block in permutation order (registers and DPP only)
     int fstamp = 0;     // timing build: factor-internal stamps base (0 = off)
-    auto factor_ldl = [&]() {
+    // QPB_W_LAZYREG: the pivot reciprocals skip the regularisation select (ldl.c:273-274)
+    // and track min |D|; the caller redoes the factor with it only when some pivot is
+    // <= 1e-14 -- otherwise the same operations, so the same bits.
+    auto factor_ldl = [&](auto regc) -> double {
+        constexpr bool REG = decltype(regc)::value != 0 || !QPB_W_LAZYREG;
+        double dmin = __builtin_huge_val();
         const int ln = qpb_opaque(lane);
         if constexpr (QPB_W_H0RE) {
             h0_row(H);
@@ -655,7 +672,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         const int lr = ln & 15;
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
-            const double rd = qpb_rcp_reg(dpiv);
+            const double rd = qpb_piv_rcp<REG>(dpiv, dmin);
             if constexpr (k + 1 < ND) {
                 constexpr int r1 = k + 1;
                 const double h = qpb_dpp<0x150 + (r1 & 15)>(r1 < 16 ? Hlo[k] : Hhi[k]);
@@ -708,7 +725,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             if constexpr ((QPB_W_ABL & 1) != 0) return;
 #if QPB_W_BLK
             constexpr int k0 = k & ~15, k1 = (k0 + 16 < ND) ? k0 + 16 : ND;
-            const double rd = qpb_rcp_reg(dpiv);
+            const double rd = qpb_piv_rcp<REG>(dpiv, dmin);
             if constexpr (k + 1 < k1) {
                 const double h = qpb_xb<k + 1>(H[k]), hkk = qpb_xb<k + 1>(H[k + 1]);
                 dpiv = __builtin_fma(h, h * -rd, hkk);
@@ -767,7 +784,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 Tx[nb + ln] = H[k1];                                  // column k1 for step k1
             }
 #else
-            const double rd = qpb_rcp_reg(dpiv);
+            const double rd = qpb_piv_rcp<REG>(dpiv, dmin);
             if constexpr (k + 1 < ND) {
                 const double h = qpb_xb<k + 1>(H[k]), hkk = qpb_xb<k + 1>(H[k + 1]);
                 dpiv = __builtin_fma(h, h * -rd, hkk);
@@ -796,6 +813,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         });
 #endif  // QPB_W_DUP
         if (fstamp) QPB_TS(fstamp + 2);
+        return dmin;
     };
     // transpose -L through LDS: lane e gets column e (0 on and above the
     // diagonal); the first wsync also orders every earlier Vb read before the
@@ -1006,7 +1024,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             if (isz[t]) Vb[NX + lane + 64 * t] = z[t];
         if (lane < NY) Vb[NX + NZ + lane] = y;
         qpb_wsync();
-        factor_ldl();
+        // (a dense block of <= 16 rows lives in DPP row 0: the other rows' broadcasts
+        // are not pivots and do not vote)
+        if (QPB_W_LAZYREG && __builtin_amdgcn_ballot_w64(factor_ldl(qpb_ic<0>{}) <= 1e-14 && (ND > 16 || lane < 16)) != 0)
+            factor_ldl(qpb_ic<1>{});                        // a tiny pivot: rare, wave-uniform
+        else if (!QPB_W_LAZYREG)
+            factor_ldl(qpb_ic<1>{});
 #if QPB_WARM
         long tf1 = QPB_CLK() - tf0;   // + the transpose below
 #endif
