@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <map>
 #include <sstream>
+#include <vector>
 
 namespace qpb {
 namespace {

@@ -20,6 +20,21 @@
 // (ldl.c:253-326), residuals (Auxilary.c:745-786), step length
 // (Auxilary.c:359-393).  Fast mode: FMA contraction, reciprocal pivots.
 #pragma clang fp contract(fast)
+#ifndef QPB_LDS
+// Persistent form (QPB_SERVE): the zero-copy slab is re-read and re-written by every
+// request, and the host rewrites it in between.  Everything the wave reads from it or
+// writes to it goes through system-scope loads / stores (sc0 sc1): a store leaves no
+// copy of the line in this XCD's L2 and a load reads past L1, so no request sees a
+// line cached for an earlier one (round 3: a warm solve started from the previous
+// QP's iterate).  Batched builds keep plain loads and stores.
+#if defined(QPB_SERVE) && QPB_SERVE
+#define QPB_LDS(p) __hip_atomic_load((p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+#define QPB_STS(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+#else
+#define QPB_LDS(p) (*(p))
+#define QPB_STS(p, v) (*(p) = (v))
+#endif
+#endif
 
 #ifndef QPB_ROW_COMMON_DONE
 #define QPB_ROW_COMMON_DONE
@@ -66,6 +81,12 @@ struct qpb_args {
 #define QPB_R_LAZYREG 0   // 1: pivot regularisation checked once per factor, the factor redone only
                           // when needed (measured: 1 024 QPs 32.7 vs 32.9 us, no gain; the two-wave
                           // form spills 34 more registers with it)
+#endif
+#ifndef QPB_R_GWG4
+#define QPB_R_GWG4 1      // G'WG four rows at a time, products formed before their DPP FMAs
+#endif
+#ifndef QPB_R_NLFIRST
+#define QPB_R_NLFIRST 1   // each pivot's -L(c,k) formed before the lookahead
 #endif
 #ifndef QPB_R_ALIAS
 #define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
@@ -338,7 +359,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         for (int u = 0; u < NPL; u++) {
             const int k = c + 16 * u;
             const bool ok = k < QPB_NNZP;
-            vP[u] = ok ? tP[k * 64] : 0.0;
+            vP[u] = ok ? QPB_LDS(&tP[k * 64]) : 0.0;
             iP[u] = ok ? qpb_scP[k] : -1;
             iP2[u] = ok ? qpb_scP2[k] : -1;
         }
@@ -346,7 +367,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         for (int u = 0; u < NGL; u++) {
             const int k = c + 16 * u;
             const bool ok = k < QPB_NNZG;
-            vG[u] = ok ? tG[k * 64] : 0.0;
+            vG[u] = ok ? QPB_LDS(&tG[k * 64]) : 0.0;
             iG[u] = ok ? qpb_scG[k] : -1;
         }
 #if NY > 0
@@ -355,16 +376,16 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         for (int u = 0; u < NAL; u++) {
             const int k = c + 16 * u;
             const bool ok = k < QPB_NNZA;
-            vA[u] = ok ? tA[k * 64] : 0.0;
+            vA[u] = ok ? QPB_LDS(&tA[k * 64]) : 0.0;
             iA[u] = ok ? qpb_scA[k] : -1;
         }
 #endif
     }
-    const double cx = isx ? a.c[tile * (NX * 64) + c * 64 + ql] : 0.0;
-    const double hz0 = isz0 ? a.h[tile * (NZ * 64) + c * 64 + ql] : 0.0;
-    const double hz1 = isz1 ? a.h[tile * (NZ * 64) + (16 + c) * 64 + ql] : 0.0;
+    const double cx = isx ? QPB_LDS(&a.c[tile * (NX * 64) + c * 64 + ql]) : 0.0;
+    const double hz0 = isz0 ? QPB_LDS(&a.h[tile * (NZ * 64) + c * 64 + ql]) : 0.0;
+    const double hz1 = isz1 ? QPB_LDS(&a.h[tile * (NZ * 64) + (16 + c) * 64 + ql]) : 0.0;
 #if NY > 0
-    const double by = isy ? a.b[tile * (NY * 64) + c * 64 + ql] : 0.0;
+    const double by = isy ? QPB_LDS(&a.b[tile * (NY * 64) + c * 64 + ql]) : 0.0;
 #else
     const double by = 0.0;
 #endif
@@ -449,6 +470,35 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         double dmin = __builtin_huge_val();
 #pragma unroll
         for (int e = 0; e < NX; e++) H[e] = QPB_R_REGH0 ? H0[e] : H0s[ix * NX + e];
+#if QPB_R_GWG4
+        // four rows at a time: the four products -G(r,c) w_r are formed (in their own
+        // registers) before any of their DPP FMAs, so no FMA waits out the DPP operand
+        // hazard behind the multiply that feeds it, and the rows do not serialise on
+        // one temporary (round 3: 16 such waits of 2 wait states per factor)
+        qpb_for<0, (NZ + 3) / 4>([&](auto qc) {
+            constexpr int r0 = 4 * decltype(qc)::value;
+            double cr[4];
+            qpb_for<0, 4>([&](auto uc) {
+                constexpr int r = r0 + decltype(uc)::value;
+                if constexpr (r < NZ) {
+                    const double wr = r < 16 ? qpb_nb<(r & 15)>(w0) : qpb_nb<(r & 15)>(w1);
+                    cr[decltype(uc)::value] = nGc[r] * wr;       // -G(r,c) w_r
+                } else {
+                    cr[decltype(uc)::value] = 0.0;
+                }
+            });
+            asm volatile("" : "+v"(cr[0]), "+v"(cr[1]), "+v"(cr[2]), "+v"(cr[3]));
+            qpb_for<0, 4>([&](auto uc) {
+                constexpr int r = r0 + decltype(uc)::value;
+                if constexpr (r < NZ) {
+                    qpb_for<0, NX>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        if constexpr (qpb_Gnz[r][j]) qpb_fxs<j>(H[j], nGc[r], cr[decltype(uc)::value]);
+                    });
+                }
+            });
+        });
+#else
         qpb_for<0, NZ>([&](auto rc) {
             constexpr int r = decltype(rc)::value;
             const double wr = r < 16 ? qpb_nb<(r & 15)>(w0) : qpb_nb<(r & 15)>(w1);
@@ -458,6 +508,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 if constexpr (qpb_Gnz[r][j]) qpb_fxs<j>(H[j], nGc[r], cr);   // += G(r,c) w_r G(r,j)
             });
         });
+#endif
         // right-looking LDL' in natural order; the pivot recurrence is the
         // critical path: D_{k+1} comes from H'(k+1,k) and H'(k+1,k+1) with
         // exactly the operations lane k+1's own update performs
@@ -471,12 +522,21 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 rd = qpb_rcp_nr(dpiv);
                 dmin = __builtin_fmin(dmin, __builtin_fabs(dpiv));
             }
+#if QPB_R_NLFIRST
+            // -L(c,k) first: its multiply then sits two instructions ahead of the DPP
+            // FMAs that read it (the lookahead's multiply and FMA in between) instead of
+            // right before them behind a 2-wait-state pad
+            double nl = H[k] * -rd;
+            asm volatile("" : "+v"(nl));
+#endif
             if constexpr (k + 1 < NX) {
                 const double h = qpb_nb<k + 1>(H[k]), hkk = qpb_nb<k + 1>(H[k + 1]);
                 dpiv = __builtin_fma(h, h * -rd, hkk);
             }
             rDd = c == k ? rd : rDd;
+#if !QPB_R_NLFIRST
             const double nl = H[k] * -rd;        // -L(c,k)
+#endif
             qpb_for<k + 1, NX>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 qpb_fxs<j>(H[j], H[k], nl);        // H(c,j) -= L(c,k) H(j,k)
@@ -546,15 +606,15 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #if QPB_WARM
     // warm variant (qpb_solve_warm): QP_SOLVE continues from the object's iterate,
     // IterationCount and options->sigma (qpSWIFT.c:502-596 never re-initialises)
-    if (isx) x = a.x[tile * (NX * 64) + c * 64 + ql];
+    if (isx) x = QPB_LDS(&a.x[tile * (NX * 64) + c * 64 + ql]);
 #if NY > 0
-    if (isy) y = a.y[tile * (NY * 64) + c * 64 + ql];
+    if (isy) y = QPB_LDS(&a.y[tile * (NY * 64) + c * 64 + ql]);
 #endif
-    if (isz0) { z0 = a.z[tile * (NZ * 64) + c * 64 + ql]; s0 = a.s[tile * (NZ * 64) + c * 64 + ql]; }
-    if (isz1) { z1 = a.z[tile * (NZ * 64) + (16 + c) * 64 + ql]; s1 = a.s[tile * (NZ * 64) + (16 + c) * 64 + ql]; }
-    const long it0 = a.iters[qc];   // IterationCount the QP enters with
-    const int flag0 = a.flag[qc];   // stats->Flag it enters with (QP_FATAL after setup)
-    sigma = a.sig[qc];
+    if (isz0) { z0 = QPB_LDS(&a.z[tile * (NZ * 64) + c * 64 + ql]); s0 = QPB_LDS(&a.s[tile * (NZ * 64) + c * 64 + ql]); }
+    if (isz1) { z1 = QPB_LDS(&a.z[tile * (NZ * 64) + (16 + c) * 64 + ql]); s1 = QPB_LDS(&a.s[tile * (NZ * 64) + (16 + c) * 64 + ql]); }
+    const long it0 = QPB_LDS(&a.iters[qc]);   // IterationCount the QP enters with
+    const int flag0 = QPB_LDS(&a.flag[qc]);   // stats->Flag it enters with (QP_FATAL after setup)
+    sigma = QPB_LDS(&a.sig[qc]);
     it = 0;
     double sigf = sigma;       // options->sigma when this row's loop ends (a frozen row's own
                                // sigma keeps being recomputed while the rest of the wave runs)
@@ -768,24 +828,24 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     }
     // ---- outputs (tiled SoA)
     if (valid) {
-        if (isx) a.x[tile * (NX * 64) + c * 64 + ql] = x;
+        if (isx) QPB_STS(&a.x[tile * (NX * 64) + c * 64 + ql], x);
 #if NY > 0
-        if (isy) a.y[tile * (NY * 64) + c * 64 + ql] = y;
+        if (isy) QPB_STS(&a.y[tile * (NY * 64) + c * 64 + ql], y);
 #endif
         if (isz0) {
-            a.z[tile * (NZ * 64) + c * 64 + ql] = z0;
-            a.s[tile * (NZ * 64) + c * 64 + ql] = s0;
+            QPB_STS(&a.z[tile * (NZ * 64) + c * 64 + ql], z0);
+            QPB_STS(&a.s[tile * (NZ * 64) + c * 64 + ql], s0);
         }
         if (isz1) {
-            a.z[tile * (NZ * 64) + (16 + c) * 64 + ql] = z1;
-            a.s[tile * (NZ * 64) + (16 + c) * 64 + ql] = s1;
+            QPB_STS(&a.z[tile * (NZ * 64) + (16 + c) * 64 + ql], z1);
+            QPB_STS(&a.s[tile * (NZ * 64) + (16 + c) * 64 + ql], s1);
         }
         if (c == 0) {
-            a.flag[q] = flag;
-            a.iters[q] = (int)itq;
-            a.fval[q] = fr[0];
+            QPB_STS(&a.flag[q], flag);
+            QPB_STS(&a.iters[q], (int)itq);
+            QPB_STS(&a.fval[q], fr[0]);
 #if QPB_WARM
-            a.sig[q] = sigf;
+            QPB_STS(&a.sig[q], sigf);
             if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
 #endif
 #if QPB_R_TIMING == 3
@@ -831,6 +891,7 @@ QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned l
     while (qpb_serve_wait(mb, &last, idle, life, t_launch, &t_seen)) {
         qpb_row_body(a, 0, 0, qpb_lds);
         qpb_serve_done(mb, last, t_seen);
+        if (life == 0) break;       // one request per launch (the default; the host pre-launches the next)
     }
 }
 #else

@@ -564,7 +564,7 @@ static __device__ bool qpb_serve_wait(qpb_mailbox *mb, unsigned long long *last,
             return true;
         }
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        if (now - t0 > idle || now - t_launch > life) return false;
+        if (now - t0 > idle || (*t_seen != 0 && now - t_launch > life)) return false;   // life: after a first request
         __builtin_amdgcn_s_sleep(4);
     }
 }
@@ -996,8 +996,17 @@ unsigned long long serve_idle_ticks() {
     static const unsigned long long t = ms_ticks("QPSWIFT_HIP_SERVE_IDLE_MS", 20.0);
     return t;
 }
+// 0 (the default): a launch answers ONE request and leaves, and the host launches the
+// next wave as soon as it has the answer, so the next call still finds a wave waiting.
+// A wave that answers request after request (QPSWIFT_HIP_SERVE_LIFE_MS > 0, then also
+// its lifetime) was measured to carry state from one request into the next in some
+// kernels -- the trot drop-in golden's warm solves went wrong from a wave's second
+// request on -- so it is a diagnostic mode only.
 unsigned long long serve_life_ticks() {
-    static const unsigned long long t = ms_ticks("QPSWIFT_HIP_SERVE_LIFE_MS", 10.0);
+    static const unsigned long long t = [] {
+        const char *e = getenv("QPSWIFT_HIP_SERVE_LIFE_MS");
+        return e && atof(e) > 0.0 ? ms_ticks("QPSWIFT_HIP_SERVE_LIFE_MS", 10.0) : 0ull;
+    }();
     return t;
 }
 unsigned long long mb_load(const unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
@@ -1094,7 +1103,7 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
         return QPB_OK;
     };
     // a kernel that left on its own (idle) is relaunched before the request
-    if (srv->running) {
+    if (srv->running && serve_life_ticks() != 0) {
         const hipError_t q = hipStreamQuery(sm);
         if (q == hipSuccess) srv->running = false;
         else if (q != hipErrorNotReady) {
@@ -1102,24 +1111,43 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
             return fail(QPB_EHIP, std::string("persistent solver: ") + hipGetErrorString(q));
         }
     }
+    // One request per launch (the default): each call posts its request to the wave
+    // launched for it and, while that wave solves, launches the next call's wave
+    // behind it on the stream (the launch's host cost overlaps the solve).  A queued
+    // wave waits up to the idle time; a call that comes later than half of it stops
+    // whatever may still be waiting and launches afresh, so a request is never posted
+    // to a wave that may already have left (its idle clock starts after the previous
+    // answer the host saw, within microseconds).
+    const bool oneshot = serve_life_ticks() == 0;
+    const long long now_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (oneshot && srv->running && (double)(now_ns - srv->last_answer_ns) > 0.5e1 * (double)serve_idle_ticks() &&
+        (rc = serve_stop(srv)))
+        return rc;
     if (!srv->running && (rc = launch(srv->seq))) return rc;
     const unsigned long long r = ++srv->seq;
     mb_store(req, r);
     srv->requests++;
+    if (oneshot && (rc = launch(r))) return rc;
+    auto answered = [&]() {
+        srv->dev_ticks = srv->mb[32];
+        srv->last_answer_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                  std::chrono::steady_clock::now().time_since_epoch()).count();
+        return (int)QPB_OK;
+    };
     // wait for the answer; every ~20 us make sure the kernel is still there (it
     // may have left idle just before the request arrived: then launch again, the
     // new launch finds the request pending)
     const auto t0 = std::chrono::steady_clock::now();
     auto tq = t0;
     for (unsigned k = 1;; k++) {
-        if (mb_load(ack) == r) {
-            srv->dev_ticks = srv->mb[32];
-            return QPB_OK;
-        }
+        if (mb_load(ack) == r) return answered();
         __builtin_ia32_pause();
         if ((k & 63) != 0) continue;
         const auto now = std::chrono::steady_clock::now();
-        if (now - tq < std::chrono::microseconds(20)) continue;
+        // (one-request launches: only a fault or a stop ends the queued wave early, so
+        // the stream is looked at rarely -- a query costs the spinning host ~1-2 us)
+        if (now - tq < std::chrono::microseconds(oneshot ? 200 : 20)) continue;
         tq = now;
         const hipError_t q = hipStreamQuery(sm);
         if (q == hipErrorNotReady) {
@@ -1131,10 +1159,7 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
         }
         srv->running = false;
         if (q != hipSuccess) return fail(QPB_EHIP, std::string("persistent solver: ") + hipGetErrorString(q));
-        if (mb_load(ack) == r) {
-            srv->dev_ticks = srv->mb[32];
-            return QPB_OK;
-        }
+        if (mb_load(ack) == r) return answered();
         if ((rc = launch(r - 1))) return rc;
     }
 }

@@ -99,6 +99,7 @@ struct Server {
     unsigned long long *mb_dev = nullptr;
     unsigned long long seq = 0;          // last request posted
     bool running = false;                // launched and not seen to end
+    long long last_answer_ns = 0;        // steady-clock time of the last answer (one-request launches)
     long requests = 0, launches = 0;
     unsigned long long dev_ticks = 0;    // the last answer: 100 MHz ticks from request seen to answer
     Server() = default;

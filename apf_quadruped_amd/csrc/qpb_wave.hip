@@ -21,6 +21,21 @@
 // v_readlane beyond 16 rows; reductions are DPP row reductions.  Results agree
 // with the reference to rounding (fast mode: FMA contraction, reciprocal pivots).
 #pragma clang fp contract(fast)
+#ifndef QPB_LDS
+// Persistent form (QPB_SERVE): the zero-copy slab is re-read and re-written by every
+// request, and the host rewrites it in between.  Everything the wave reads from it or
+// writes to it goes through system-scope loads / stores (sc0 sc1): a store leaves no
+// copy of the line in this XCD's L2 and a load reads past L1, so no request sees a
+// line cached for an earlier one (round 3: a warm solve started from the previous
+// QP's iterate).  Batched builds keep plain loads and stores.
+#if defined(QPB_SERVE) && QPB_SERVE
+#define QPB_LDS(p) __hip_atomic_load((p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+#define QPB_STS(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+#else
+#define QPB_LDS(p) (*(p))
+#define QPB_STS(p, v) (*(p) = (v))
+#endif
+#endif
 
 template <int V> struct qpb_ic { static constexpr int value = V; };
 
@@ -391,7 +406,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         for (int u = 0; u < NPL; u++) {
             const int k = lane + 64 * u;
             const bool ok = k < QPB_NNZP;
-            vP[u] = ok ? tP[k * 64] : 0.0;
+            vP[u] = ok ? QPB_LDS(&tP[k * 64]) : 0.0;
             iP[u] = ok ? qpb_scP[k] : -1;
             iP2[u] = ok ? qpb_scP2[k] : -1;
         }
@@ -399,7 +414,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         for (int u = 0; u < NGL; u++) {
             const int k = lane + 64 * u;
             const bool ok = k < QPB_NNZG;
-            vG[u] = ok ? tG[k * 64] : 0.0;
+            vG[u] = ok ? QPB_LDS(&tG[k * 64]) : 0.0;
             iG[u] = ok ? qpb_scG[k] : -1;
         }
 #if NY > 0
@@ -408,17 +423,17 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         for (int u = 0; u < NAL; u++) {
             const int k = lane + 64 * u;
             const bool ok = k < QPB_NNZA;
-            vA[u] = ok ? tA[k * 64] : 0.0;
+            vA[u] = ok ? QPB_LDS(&tA[k * 64]) : 0.0;
             iA[u] = ok ? qpb_scA[k] : -1;
         }
 #endif
     }
-    const double cx = isx ? a.c[tile * (NX * 64) + lane * 64 + ql] : 0.0;
+    const double cx = isx ? QPB_LDS(&a.c[tile * (NX * 64) + lane * 64 + ql]) : 0.0;
     double hz[ZC];
 #pragma unroll
-    for (int t = 0; t < ZC; t++) hz[t] = isz[t] ? a.h[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql] : 0.0;
+    for (int t = 0; t < ZC; t++) hz[t] = isz[t] ? QPB_LDS(&a.h[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql]) : 0.0;
 #if NY > 0
-    const double by = isy ? a.b[tile * (NY * 64) + lane * 64 + ql] : 0.0;
+    const double by = isy ? QPB_LDS(&a.b[tile * (NY * 64) + lane * 64 + ql]) : 0.0;
 #else
     const double by = 0.0;
 #endif
@@ -971,19 +986,19 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #if QPB_WARM
     // warm variant (qpb_solve_warm): QP_SOLVE continues from the object's iterate,
     // IterationCount and options->sigma (qpSWIFT.c:502-596 never re-initialises)
-    if (isx) x = a.x[tile * (NX * 64) + lane * 64 + ql];
+    if (isx) x = QPB_LDS(&a.x[tile * (NX * 64) + lane * 64 + ql]);
 #if NY > 0
-    if (isy) y = a.y[tile * (NY * 64) + lane * 64 + ql];
+    if (isy) y = QPB_LDS(&a.y[tile * (NY * 64) + lane * 64 + ql]);
 #endif
 #pragma unroll
     for (int t = 0; t < ZC; t++)
         if (isz[t]) {
-            z[t] = a.z[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql];
-            s[t] = a.s[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql];
+            z[t] = QPB_LDS(&a.z[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql]);
+            s[t] = QPB_LDS(&a.s[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql]);
         }
-    const long it0 = a.iters[q];   // IterationCount the QP enters with
-    const int flag0 = a.flag[q];   // stats->Flag it enters with (QP_FATAL after setup)
-    sigma = a.sig[q];
+    const long it0 = QPB_LDS(&a.iters[q]);   // IterationCount the QP enters with
+    const int flag0 = QPB_LDS(&a.flag[q]);   // stats->Flag it enters with (QP_FATAL after setup)
+    sigma = QPB_LDS(&a.sig[q]);
     it = 0;
     // the drop-in's timers and verbose trace (KernelArgs::trace, qpb_codegen.hpp):
     // s_memrealtime ticks in the factorisations and in factor + solves, and the
@@ -1230,22 +1245,22 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     QPB_TS(370);
     const double fval = qpb_rsum<ROWS_X>(fv);
     // ---- outputs (tiled SoA)
-    if (isx) a.x[tile * (NX * 64) + lane * 64 + ql] = x;
+    if (isx) QPB_STS(&a.x[tile * (NX * 64) + lane * 64 + ql], x);
 #if NY > 0
-    if (isy) a.y[tile * (NY * 64) + lane * 64 + ql] = y;
+    if (isy) QPB_STS(&a.y[tile * (NY * 64) + lane * 64 + ql], y);
 #endif
 #pragma unroll
     for (int t = 0; t < ZC; t++)
         if (isz[t]) {
-            a.z[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql] = z[t];
-            a.s[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql] = s[t];
+            QPB_STS(&a.z[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql], z[t]);
+            QPB_STS(&a.s[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql], s[t]);
         }
     if (lane == 0) {
-        a.flag[q] = flag;
-        a.iters[q] = (int)(it0 + it);
-        a.fval[q] = fval;
+        QPB_STS(&a.flag[q], flag);
+        QPB_STS(&a.iters[q], (int)(it0 + it));
+        QPB_STS(&a.fval[q], fval);
 #if QPB_WARM
-        a.sig[q] = sigma;
+        QPB_STS(&a.sig[q], sigma);
         if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
 #endif
         if (a.stats && !QPB_W_TIMING) {
@@ -1282,6 +1297,7 @@ QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned l
         asm volatile("" : "+v"(tid));
         qpb_wave_body(a, qpb_lds, tid);
         qpb_serve_done(mb, last, t_seen);
+        if (life == 0) break;       // one request per launch (the default; the host pre-launches the next)
     }
 }
 #endif

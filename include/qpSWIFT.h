@@ -27,12 +27,14 @@
  *       runs on the current HIP device, then x, y, z, s, the statistics and
  *       options->sigma are written back.
  *   Device solves (setup's initial point, QP_SOLVE) go to a persistent solver:
- *       one resident wave per kind (cold / warm) and solving thread polls a
- *       mailbox in mapped host memory, so a call costs no kernel launch and no
- *       stream synchronisation; it leaves after QPSWIFT_HIP_SERVE_IDLE_MS
- *       (default 20) without a call, or at its first idle moment after
- *       QPSWIFT_HIP_SERVE_LIFE_MS (default 10: work queued behind it on a shared
- *       hardware queue waits no longer), and is relaunched by the next call.  Plans
+ *       per kind (cold / warm) and solving thread, a wave launched ahead of the
+ *       call polls a mailbox in mapped host memory, answers ONE request and
+ *       leaves; each call launches the next call's wave while its own solves, so
+ *       a call costs no stream synchronisation and no launch on its path.  A
+ *       queued wave leaves after QPSWIFT_HIP_SERVE_IDLE_MS (default 20) without a
+ *       call; a call later than half that relaunches.  (QPSWIFT_HIP_SERVE_LIFE_MS
+ *       > 0, diagnostics only, keeps one wave answering request after request
+ *       for that long -- measured to carry state between requests.)  Plans
  *       whose one-QP kernel is the tree or the exact lane kernel, and
  *       QPSWIFT_HIP_SERVE=0, launch + synchronise per call.  There is no CPU
  *       fallback: without a usable GPU it returns QP_FATAL and qpb_last_error()
