@@ -132,3 +132,53 @@ def test_served_solvers_per_thread():
         t.join(timeout=120)
     assert not any(t.is_alive() for t in ts), "a solving thread hung"
     assert not errors, errors
+
+
+_LAUNCH_PATH = r"""
+import sys, json
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+sys.path.insert(0, sys.argv[1] + "/tests")
+from conftest import golden
+from apf_quadruped_amd import dropin
+out = {}
+for name in sys.argv[3].split(","):
+    g = golden(name)
+    n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    for q in range(g["x"].shape[0]):
+        r = dropin.solve_dense(n, m, p, g["P"][q], g["A"][q] if p else None, g["G"][q], g["c"][q], g["h"][q],
+                               g["b"][q] if p else None, ordering=int(g["ordering"]), reltol=tol, abstol=tol,
+                               maxit=maxit)
+        out[f"{name}/{q}"] = {"flag": r["flag"], "iters": r["iters"], "x": r["x"].tolist(), "z": r["z"].tolist()}
+json.dump(out, open(sys.argv[2], "w"))
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(os.environ.get("QPSWIFT_HIP_SERVE") == "0", reason="persistent solver switched off")
+def test_served_matches_launch_path(tmp_path):
+    """The controller's call (Permut = NULL) on every QP of four goldens, through the
+    persistent solver here and through launch + synchronise in a child process
+    (QPSWIFT_HIP_SERVE=0): the same flags and iteration counts and x, z within 1e-12
+    of scale -- a request that saw anything of an earlier one would differ."""
+    import json
+    import subprocess
+    import sys
+    names = ["c1_tol1e-2", "mixed_trot_brfl", "c30_tol1e-2", "c30_trot_tol1e-2"]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, QPSWIFT_HIP_SERVE="0")
+    res = tmp_path / "launch.json"
+    subprocess.run([sys.executable, "-c", _LAUNCH_PATH, root, str(res), ",".join(names)], env=env, check=True,
+                   timeout=180)
+    ref = json.load(open(res))
+    for name in names:
+        g = golden(name)
+        tol, maxit = float(g["tol"]), int(g["maxit"])
+        for q in range(g["x"].shape[0]):
+            r = dropin.solve_dense(*_args(g, q), ordering=int(g["ordering"]), reltol=tol, abstol=tol, maxit=maxit)
+            e = ref[f"{name}/{q}"]
+            assert (r["flag"], r["iters"]) == (e["flag"], e["iters"]), (name, q)
+            for k in ("x", "z"):
+                v = np.asarray(e[k])
+                assert np.abs(r[k] - v).max() <= 1e-12 * max(1.0, float(np.abs(v).max())), (name, q, k)
