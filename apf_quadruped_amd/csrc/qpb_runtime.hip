@@ -1131,6 +1131,8 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
     if (oneshot && (rc = launch(r))) return rc;
     auto answered = [&]() {
         srv->dev_ticks = srv->mb[32];
+        if (getenv("QPB_SERVE_DEBUG"))
+            fprintf(stderr, "[serve] %s request %llu exec %016llx\n", kn.c_str(), r, srv->mb[40]);
         srv->last_answer_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
                                   std::chrono::steady_clock::now().time_since_epoch()).count();
         return (int)QPB_OK;

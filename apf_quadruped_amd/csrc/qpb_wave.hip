@@ -67,6 +67,17 @@ struct qpb_args {
 #ifndef QPB_W_GG           // 1: G(r,i)G(r,j) products in registers; 0: recompute from LDS
 #define QPB_W_GG (QPB_NNZG <= 48)
 #endif
+#ifndef QPB_W_EXECDBG      // 1 (diagnostics): persistent form records each request's starting EXEC mask
+#define QPB_W_EXECDBG 0
+#endif
+#ifndef QPB_W_ASMV         // 1 (diagnostics): every inline asm volatile (no CSE / motion of the DPP asm)
+#define QPB_W_ASMV 0
+#endif
+#if QPB_W_ASMV
+#define QPB_W_ASM asm volatile
+#else
+#define QPB_W_ASM asm
+#endif
 #ifndef QPB_W_LAZYREG      // 1: pivot regularisation checked once per factor (redone only when needed);
 #define QPB_W_LAZYREG 0    // off: AMD-ordered plans regularise their y pivots in most factors, so the
 #endif                     // factor ran twice (controller call batched 2.73 -> 24.7 ms, C30 tick 335 -> 520 us)
@@ -208,7 +219,7 @@ template <int J> static __device__ __forceinline__ double qpb_xb(double v) {
 #endif
 template <int J> static __device__ __forceinline__ double qpb_fmac_xb(double acc, double v, double m) {
     if constexpr (ND <= 16) {
-        asm(QPB_DPP_PRE "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        QPB_W_ASM(QPB_DPP_PRE "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
             : "+v"(acc) : "v"(v), "v"(m), "i"(J));
         return acc;
     } else {
@@ -220,7 +231,7 @@ template <int J> static __device__ __forceinline__ double qpb_fmac_xb(double acc
 // two wait states the DPP read needs are inserted explicitly
 template <int J> static __device__ __forceinline__ double qpb_fmac_xb_dep(double acc, double v, double m) {
     if constexpr (ND <= 16) {
-        asm(QPB_DPP_DEP "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        QPB_W_ASM(QPB_DPP_DEP "v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf bound_ctrl:1"
             : "+v"(acc) : "v"(v), "v"(m), "i"(J));
         return acc;
     } else {
@@ -311,7 +322,7 @@ static __device__ __forceinline__ double qpb_regularise(double d) {
 static __device__ __forceinline__ double qpb_rcp_reg(double d) {
     double r = __builtin_amdgcn_rcp(d);
     r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
-    asm("" : "+v"(r));     // opaque but not a scheduling barrier
+    QPB_W_ASM("" : "+v"(r));     // opaque but not a scheduling barrier
     const double reg = d > 0.0 ? 1e7 : -1e7;
     return __builtin_fabs(d) <= 1e-14 ? reg : r;
 }
@@ -1291,6 +1302,13 @@ QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned l
     const unsigned long long t_launch = __builtin_amdgcn_s_memrealtime();
     unsigned long long t_seen = 0;
     while (qpb_serve_wait(mb, &last, idle, life, t_launch, &t_seen)) {
+#if QPB_W_EXECDBG
+        {   // diagnostics: the EXEC mask each request starts with -> mailbox word 40
+            const unsigned long long ex = __builtin_amdgcn_read_exec();
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_store((unsigned long long *)mb + 40, ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+#endif
         // a fresh lane index per request: nothing derived from it is hoisted out of
         // this loop (that would hold extra registers through the solve)
         unsigned tid = threadIdx.x;
