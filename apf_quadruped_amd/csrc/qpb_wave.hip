@@ -1293,6 +1293,16 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 }
 
 #if QPB_SERVE
+#ifndef QPB_W_SERVE_CALL   // 1 (diagnostics): each request's body is a call (noinline, its own
+#define QPB_W_SERVE_CALL 0 // LDS, the kernel arguments re-read per request): nothing of the body's
+#endif                     // register allocation spans the request loop
+#if QPB_W_SERVE_CALL
+static __device__ __attribute__((noinline)) void qpb_wave_req(const qpb_args *ap, unsigned tid) {
+    __shared__ __attribute__((aligned(16))) double req_lds[WPB * LDS_WAVE];
+    const qpb_args ra = *ap;
+    qpb_wave_body(ra, req_lds, tid);
+}
+#endif
 // persistent form (the drop-in's QP_SOLVE, qpb::serve_ex): one wave, QP 0, one
 // solve per request posted in the mailbox (qpb_serve_wait, runtime prelude)
 extern "C" __global__ void __launch_bounds__(QPB_WG, 1)
@@ -1313,7 +1323,12 @@ QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned l
         // this loop (that would hold extra registers through the solve)
         unsigned tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
+#if QPB_W_SERVE_CALL
+        (void)qpb_lds;
+        qpb_wave_req(&a, tid);
+#else
         qpb_wave_body(a, qpb_lds, tid);
+#endif
         qpb_serve_done(mb, last, t_seen);
         if (life == 0) break;       // one request per launch (the default; the host pre-launches the next)
     }
