@@ -1,5 +1,6 @@
 # Round 3: parity tests (configs first) + smoke + bench + rocprof kernel stats (one GPU call).
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+[ -e gpurun_out/FATAL ] && { echo "an earlier step of this call faulted: not starting"; exit 1; }
 fatal() { case "$1" in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR" gpurun_out/pytest_gpu.log | head -12; tail -15 gpurun_out/pytest_gpu.log; fatal $rc pytest
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; fatal $rc smoke
