@@ -1296,6 +1296,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #ifndef QPB_W_SERVE_CALL   // 1 (diagnostics): each request's body is a call (noinline, its own
 #define QPB_W_SERVE_CALL 0 // LDS, the kernel arguments re-read per request): nothing of the body's
 #endif                     // register allocation spans the request loop
+#ifndef QPB_W_SERVE_OPQ    // 1 (diagnostics): body inlined, kernel arguments opaque per request
+#define QPB_W_SERVE_OPQ 0
+#endif
 #if QPB_W_SERVE_CALL
 static __device__ __attribute__((noinline)) void qpb_wave_req(const qpb_args *ap, unsigned tid) {
     __shared__ __attribute__((aligned(16))) double req_lds[WPB * LDS_WAVE];
@@ -1326,6 +1329,17 @@ QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned l
 #if QPB_W_SERVE_CALL
         (void)qpb_lds;
         qpb_wave_req(&a, tid);
+#elif QPB_W_SERVE_OPQ
+        // diagnostics: every kernel argument opaque per request, so nothing derived
+        // from them is computed once and carried through the request loop
+        qpb_args ra = a;
+#define QPB_OPQ(f) asm volatile("" : "+s"(ra.f))
+        QPB_OPQ(P); QPB_OPQ(A); QPB_OPQ(G); QPB_OPQ(c); QPB_OPQ(h); QPB_OPQ(b);
+        QPB_OPQ(x); QPB_OPQ(y); QPB_OPQ(z); QPB_OPQ(s); QPB_OPQ(flag); QPB_OPQ(iters);
+        QPB_OPQ(fval); QPB_OPQ(stats); QPB_OPQ(B); QPB_OPQ(tol); QPB_OPQ(abstol); QPB_OPQ(sigma_d);
+        QPB_OPQ(maxit); QPB_OPQ(sig); QPB_OPQ(warm); QPB_OPQ(trace);
+#undef QPB_OPQ
+        qpb_wave_body(ra, qpb_lds, tid);
 #else
         qpb_wave_body(a, qpb_lds, tid);
 #endif
