@@ -443,3 +443,43 @@ def controller_qp(seed: int, qp_ids, phase: str = "stance"):
     if phase != "stance":
         return controller_swing_qp(seed, qp_ids, phase)
     return controller_qp_from_terms(controller_terms(seed, qp_ids))
+
+
+def _apf_state_draw(seed: int, rep_field: bool, min_exit: bool) -> dict:
+    """One random APF tick state (the fields of qpb_apf_state): stance feet around
+    the CoM with jitter, small CoM motion, the controller's nominal versors
+    (main.cpp:440-458), M_com = blkdiag(m I3, I_c), a 0.03 rad yaw."""
+    rng = np.random.default_rng(seed)
+    com = np.array([0.1, -0.05, 0.39, 0.01, -0.02, 0.03]) + rng.uniform(-0.01, 0.01, 6)
+    nom = FOOT_SIGNS * np.array([X_NOM, Y_NOM])
+    ee = com[None, :2] + nom + rng.uniform(-0.03, 0.03, (4, 2))
+    versor = nom / np.linalg.norm(nom, axis=1, keepdims=True)
+    M = np.zeros((6, 6))
+    M[:3, :3] = ROBOT_MASS * np.eye(3)
+    M[3:, 3:] = np.diag([0.35, 0.85, 0.95])
+    th = 0.03
+    R = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]])
+    return dict(ee=ee, com=com, com_vel=rng.uniform(-0.1, 0.1, 6), acc_des=rng.uniform(-0.5, 0.5, 6),
+                des_orient=np.array([0.0, 0.0]), rob_foot=rng.uniform(0.0, 0.5, 4), versor=versor,
+                lat_versor=np.array([1.0, 0.0]), R_wb=R, Mcom=M, mass=ROBOT_MASS, rep_field=rep_field,
+                min_exit=min_exit, fake_crawl=False)
+
+
+def apf_tick_state(seed: int = 7, rep_field: bool = True, min_exit: bool = False, fake_crawl: bool = False) -> dict:
+    """A plausible synthetic APF tick for the bench and the tests.  The robustness
+    indices are carried as the controller carries them from one gait step to the
+    next -- rob_foot = 0.35 rob_foot + 0.65 h_prev / period_st over a 0.4 s step
+    (main.cpp:1273-1276) -- and fake_crawl is what main.cpp:1307-1321 derives from
+    them (mean of the four < 0.34); states are drawn until it equals the requested
+    fake_crawl."""
+    for k in range(1000):
+        s = _apf_state_draw(seed + 7919 * k, rep_field, min_exit)
+        prev = np.random.default_rng(seed + 7919 * k + 1)
+        rob = prev.uniform(0.0, 0.6, 4)
+        h_prev = prev.uniform(0.0, 0.25, 4)
+        rf = [0.35 * float(rob[i]) + 0.65 * float(h_prev[i]) / 0.4 for i in range(4)]
+        s["rob_foot"] = np.asarray(rf)
+        s["fake_crawl"] = bool((rf[1] + rf[3] + rf[0] + rf[2]) / 4.0 < 0.34)
+        if s["fake_crawl"] == bool(fake_crawl):
+            return s
+    raise RuntimeError("no state with the requested fake_crawl")

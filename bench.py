@@ -56,7 +56,72 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-sample", type=int, default=65536)
     ap.add_argument("--cpu-passes", type=int, default=10)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch the ranks, join a gloo group and report each rank's env and shard, "
+                         "then stop before the first GPU call (CPU test of the --gpus N launcher)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this
+    script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
+    set as torch.distributed.run sets them) and return the worst exit code.  This
+    process never touches the GPU: it only counts devices (torch.cuda.device_count
+    does not initialise HIP on this image), and refuses to run fewer ranks than asked.
+    Rank 0 prints the JSON line; every rank's stderr passes through."""
+    import subprocess
+    n = args.gpus
+    if not args.dry_run:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}", file=sys.stderr)
+            return 2
+    port = int(os.environ.get("MASTER_PORT", 0)) or _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        print(f"bench.py: rank exit codes {codes}", file=sys.stderr)
+        return bad[0] if bad[0] > 0 else 1
+    return 0
+
+
+def dry_run(args, rank, world, local) -> None:
+    """The rank's view of the launch, exchanged over gloo: env, device index and the
+    QP ids it would own.  Stops before any GPU call."""
+    import torch
+    import torch.distributed as dist
+    from apf_quadruped_amd.shard import shard_range
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(rank, world, args.batch)
+    mine = torch.tensor([rank, local, world, lo, hi], dtype=torch.int64)
+    if world > 1:
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+    else:
+        parts = [mine]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_arg": args.gpus,
+                          "ranks": [dict(zip(("rank", "local_rank", "world", "lo", "hi"), p.tolist()))
+                                    for p in parts],
+                          "master": [os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")]}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def make_shard(plan, seed, q0, B, chunk=65536, gen=None):
@@ -449,14 +514,12 @@ def controller_apf_leg(dev, K=8192, steps=20, warmup=3):
     the reference's AMD ordering (QPB_ORDER_AMD: the pivots of qpSWIFT's Permut =
     NULL, so the answers are the reference's to 1e-6)."""
     import torch
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import apf_ref                      # a plausible tick state (synthetic)
     from apf_quadruped_amd import workloads as W
     from apf_quadruped_amd.batch import Plan, apf_state, apf_wrench, to_tiled
     d = W.controller_qp(0xD06B07 + 30, np.arange(1))
     plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], order="amd")
     plan.compile()
-    st = apf_state(**apf_ref.sample_state())
+    st = apf_state(**W.apf_tick_state())      # a plausible synthetic tick state
     rng = np.random.default_rng(11)
     targets = torch.from_numpy(to_tiled(np.asarray(st.com[:2])[None] + rng.uniform(-0.6, 0.6, (K, 2)))).to(dev)
     terms = torch.from_numpy(W.pack_terms(W.controller_terms(0xD06B07 + 43, np.arange(1)))[0].copy()).to(dev)
@@ -499,12 +562,21 @@ def traffic_for(kname, B):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))           # before anything touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; refusing to measure another rank count")
+    if args.dry_run:
+        dry_run(args, rank, world, local)
+        return
+    import torch
+    import torch.distributed as dist
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

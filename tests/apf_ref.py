@@ -72,35 +72,8 @@ def apf_wrench(s: dict, targets: np.ndarray):
 
 
 def sample_state(seed: int = 7, rep_field=True, min_exit=False, fake_crawl=False):
-    """A plausible tick: nominal stance feet around the CoM with jitter, small CoM
-    motion, the controller's nominal versors (main.cpp:440-458), and robustness
-    indices as the controller derives them (apf_update: the previous step's smoothed
-    indices and this step's accumulated 1/h over a 0.4 s step), so that fake_crawl
-    is what main.cpp:1320 sets -- the state is drawn until it matches the requested
-    fake_crawl."""
-    for k in range(1000):
-        s = _sample_state(seed + 7919 * k, rep_field, min_exit)
-        prev = np.random.default_rng(seed + 7919 * k + 1)
-        s["rob_foot"] = prev.uniform(0.0, 0.6, 4)
-        apf_update(s, prev.uniform(0.0, 0.25, 4), 0.4)
-        if s["fake_crawl"] == bool(fake_crawl):
-            return s
-    raise RuntimeError("no state with the requested fake_crawl")
-
-
-def _sample_state(seed, rep_field, min_exit):
-    rng = np.random.default_rng(seed)
-    com = np.array([0.1, -0.05, 0.39, 0.01, -0.02, 0.03]) + rng.uniform(-0.01, 0.01, 6)
-    ee = com[None, :2] + FOOT_OFF + rng.uniform(-0.03, 0.03, (4, 2))
-    vec = np.array([[0.186571, -0.289186], [-0.186571, -0.289186], [-0.186571, 0.289186], [0.186571, 0.289186]])
-    versor = vec / np.linalg.norm(vec, axis=1, keepdims=True)
-    Ic = np.diag([0.35, 0.85, 0.95])
-    M = np.zeros((6, 6))
-    M[:3, :3] = 21.261 * np.eye(3)
-    M[3:, 3:] = Ic
-    th = 0.03
-    R = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]])
-    return dict(ee=ee, com=com, com_vel=rng.uniform(-0.1, 0.1, 6), acc_des=rng.uniform(-0.5, 0.5, 6),
-                des_orient=np.array([0.0, 0.0]), rob_foot=rng.uniform(0.0, 0.5, 4), versor=versor,
-                lat_versor=np.array([1.0, 0.0]), R_wb=R, Mcom=M, mass=21.261, rep_field=rep_field,
-                min_exit=min_exit, fake_crawl=False)
+    """The synthetic tick state the bench uses (workloads.apf_tick_state); its
+    fake_crawl derivation is checked against apf_update in
+    tests/test_controller_assemble.py."""
+    from apf_quadruped_amd.workloads import apf_tick_state
+    return apf_tick_state(seed, rep_field, min_exit, fake_crawl)

@@ -161,3 +161,46 @@ def test_two_rank_gather_path_is_agreed_on_every_rank():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0] == res[1] == (True, "torch_fallback", None, True), res
+
+
+def _bench(args, env_extra=None, timeout=240):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_gpus_n_launches_n_ranks(n):
+    """`bench.py --gpus N` (no torchrun) starts N rank processes itself, each with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, which join one process group
+    (gloo in --dry-run, which stops before the first GPU call) and own contiguous
+    shards; rank 0 prints the one line with n_gpus == N."""
+    rc, line, err = _bench(["--gpus", str(n), "--batch", "8192", "--dry-run"])
+    assert rc == 0, err
+    assert line["n_gpus"] == n and line["gpus_arg"] == n
+    assert [(d["rank"], d["local_rank"], d["world"]) for d in line["ranks"]] == [(r, r, n) for r in range(n)]
+    assert [(d["lo"], d["hi"]) for d in line["ranks"]] == [(r * 8192, (r + 1) * 8192) for r in range(n)]
+    assert line["master"][0] == "127.0.0.1"
+
+
+def test_bench_refuses_rank_count_mismatch():
+    """Under an external launcher, --gpus must equal WORLD_SIZE: the bench never
+    measures another rank count than the one asked for."""
+    rc, line, err = _bench(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc != 0 and line is None and "WORLD_SIZE=2" in err
+
+
+def test_bench_refuses_missing_gpus():
+    """Without --dry-run, --gpus N on a machine with fewer than N GPUs exits
+    non-zero before starting any rank (no silent fallback to fewer ranks)."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this machine has two GPUs")
+    rc, line, err = _bench(["--gpus", "2"])
+    assert rc == 2 and line is None and "needs 2 visible GPUs" in err
