@@ -762,7 +762,7 @@ struct Gen {
         store("z", m, "z");
         store("s", m, "s");
         ln("a.flag[q] = flag; a.iters[q] = (int)(it0 + it); a.fval[q] = fval;");
-        ln("if (QPB_WARM) a.sig[q] = sigma;");
+        ln("if (QPB_WARM || a.sig) a.sig[q] = sigma;   // cold: options->sigma for the drop-in");
         ln("if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }");
         ln("if (a.stats) { double *o = a.stats + tile * 384 + lane; o[0] = st_rx; o[64] = st_ry; o[128] = st_rz;"
            " o[192] = st_mu; o[256] = ap; o[320] = ad; }");

@@ -847,6 +847,10 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #if QPB_WARM
             QPB_STS(&a.sig[q], sigf);
             if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
+#else
+            // options->sigma after a cold QP_SOLVE: this row's sigma when the wave stops --
+            // its own final sigma for the wave's last row to finish, e.g. the drop-in's B = 1
+            if (a.sig) QPB_STS(&a.sig[q], sigma);
 #endif
 #if QPB_R_TIMING == 3
             QPB_TM(4);

@@ -1002,18 +1002,51 @@ unsigned long long serve_idle_ticks() {
 // its lifetime) was measured to carry state from one request into the next in some
 // kernels -- the trot drop-in golden's warm solves went wrong from a wave's second
 // request on -- so it is a diagnostic mode only.
+// It is refused unless QPB_SERVE_DIAG=1 is set as well, so the knob alone can never
+// put wrong answers into a controller.
 unsigned long long serve_life_ticks() {
     static const unsigned long long t = [] {
         const char *e = getenv("QPSWIFT_HIP_SERVE_LIFE_MS");
-        return e && atof(e) > 0.0 ? ms_ticks("QPSWIFT_HIP_SERVE_LIFE_MS", 10.0) : 0ull;
+        if (!(e && atof(e) > 0.0)) return 0ull;
+        const char *d = getenv("QPB_SERVE_DIAG");
+        if (!(d && d[0] == '1')) {
+            fprintf(stderr, "qpswift-hip: QPSWIFT_HIP_SERVE_LIFE_MS ignored: multi-request persistent waves are a "
+                            "diagnostics mode (set QPB_SERVE_DIAG=1 as well); one request per wave\n");
+            return 0ull;
+        }
+        return ms_ticks("QPSWIFT_HIP_SERVE_LIFE_MS", 10.0);
     }();
     return t;
 }
+// the calling thread's servers, for serve_retire_thread (a server belongs to the
+// workspace of the thread that solves through it)
+thread_local std::vector<qpb::Server *> t_servers;
 unsigned long long mb_load(const unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 void mb_store(unsigned long long *p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
 }  // namespace
 
+// A retired server's wave saw the stop word (or will, the moment it starts): wait for
+// it to leave and re-arm the mailbox before the next launch.
+static int serve_settle(qpb::Server *srv) {
+    if (!srv->retiring) return QPB_OK;
+    srv->retiring = false;
+    const hipError_t e = hipStreamSynchronize((hipStream_t)srv->stream);
+    mb_store(srv->mb, srv->seq);
+    return e == hipSuccess ? QPB_OK : fail(QPB_EHIP, std::string("persistent solver: ") + hipGetErrorString(e));
+}
+
+void qpb::serve_retire_thread() {
+    for (Server *srv : t_servers) {
+        if (!srv->running) continue;
+        mb_store(srv->mb, kStop);        // the queued wave leaves at its next poll (~0.1 us)
+        srv->running = false;
+        srv->retiring = true;
+        srv->retires++;
+    }
+}
+
 int qpb::serve_stop(Server *srv) {
+    if (srv && srv->retiring) return serve_settle(srv);
     if (!srv || !srv->running) return QPB_OK;
     mb_store(srv->mb, kStop);
     const hipError_t e = hipStreamSynchronize((hipStream_t)srv->stream);
@@ -1025,6 +1058,8 @@ int qpb::serve_stop(Server *srv) {
 
 qpb::Server::~Server() {
     (void)serve_stop(this);
+    for (size_t i = 0; i < t_servers.size(); i++)
+        if (t_servers[i] == this) { t_servers.erase(t_servers.begin() + (long)i); break; }
     if (stream) (void)hipStreamDestroy((hipStream_t)stream);
     if (mb) (void)hipHostFree(mb);
 }
@@ -1086,6 +1121,11 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
         srv->stream = sm;
     }
     hipStream_t sm = (hipStream_t)srv->stream;
+    if (!srv->registered) {
+        t_servers.push_back(srv);
+        srv->registered = true;
+    }
+    if ((rc = serve_settle(srv))) return rc;
     // a running kernel with other arguments or code: stop it first
     if (srv->running && (srv->kname != kn || std::memcmp(&srv->args, &a, sizeof a) != 0) && (rc = serve_stop(srv)))
         return rc;
@@ -1162,16 +1202,29 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
         srv->running = false;
         if (q != hipSuccess) return fail(QPB_EHIP, std::string("persistent solver: ") + hipGetErrorString(q));
         if (mb_load(ack) == r) return answered();
+        // the wave had left: a fresh one answers r (it starts with last = r - 1) and,
+        // one request per launch, the next call's wave is queued behind it as usual
         if ((rc = launch(r - 1))) return rc;
+        if (oneshot && (rc = launch(r))) return rc;
     }
 }
 
 extern "C" {
 
+/* Retire the calling thread's queued persistent drop-in waves (qpb::serve_retire_thread):
+ * they leave within microseconds instead of polling for the idle time, so a device-wide
+ * synchronisation the caller is about to do cannot wait on them.  The batched solves
+ * call it themselves; the next QP_SOLVE relaunches. */
+int qpb_dropin_quiesce(void) {
+    qpb::serve_retire_thread();
+    return QPB_OK;
+}
+
 int qpb_solve(qpb_plan *plan, long B, const double *P, const double *A, const double *G,
               const double *c, const double *h, const double *b, const qpb_settings *st,
               double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
               double *stats, void *stream) {
+    qpb::serve_retire_thread();      // no queued drop-in wave of this thread outlives the caller's sync
     return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, nullptr, stream,
                          nullptr, false, nullptr);
 }
@@ -1180,6 +1233,7 @@ int qpb_solve_best(qpb_plan *plan, long B, const double *P, const double *A, con
                    const double *c, const double *h, const double *b, const qpb_settings *st,
                    double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
                    double *stats, double *best, void *stream) {
+    qpb::serve_retire_thread();      // no queued drop-in wave of this thread outlives the caller's sync
     if (!best) return fail(QPB_EINVAL, "qpb_solve_best: best is NULL");
     return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, best, stream,
                          nullptr, false, nullptr);
@@ -1189,6 +1243,7 @@ int qpb_solve_warm(qpb_plan *plan, long B, const double *P, const double *A, con
                    const double *c, const double *h, const double *b, const qpb_settings *st,
                    double *x, double *y, double *z, double *s, int *flag, int *iters, double *fval,
                    double *stats, double *sigma, void *stream) {
+    qpb::serve_retire_thread();      // no queued drop-in wave of this thread outlives the caller's sync
     if (!sigma) return fail(QPB_EINVAL, "qpb_solve_warm: sigma is NULL");
     return qpb::solve_ex(plan, B, P, A, G, c, h, b, st, x, y, z, s, flag, iters, fval, stats, nullptr, stream, sigma,
                          true, nullptr);
@@ -1249,6 +1304,7 @@ int qpb_group_compile(qpb_group *g) {
 }
 
 int qpb_group_solve(qpb_group *g, const qpb_io *io, const qpb_settings *st, double *best, void *stream) {
+    qpb::serve_retire_thread();
     if (!g || !io) return fail(QPB_EINVAL, "NULL group or io");
     const int nm = (int)g->p.size();
     qpb_settings def;

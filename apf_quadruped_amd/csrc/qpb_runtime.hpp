@@ -99,8 +99,10 @@ struct Server {
     unsigned long long *mb_dev = nullptr;
     unsigned long long seq = 0;          // last request posted
     bool running = false;                // launched and not seen to end
+    bool retiring = false;               // stop word posted by serve_retire_thread, launch not yet joined
+    bool registered = false;             // listed for serve_retire_thread (this thread's servers)
     long long last_answer_ns = 0;        // steady-clock time of the last answer (one-request launches)
-    long requests = 0, launches = 0;
+    long requests = 0, launches = 0, retires = 0;
     unsigned long long dev_ticks = 0;    // the last answer: 100 MHz ticks from request seen to answer
     Server() = default;
     Server(const Server &) = delete;
@@ -116,4 +118,11 @@ int serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A, cons
              int *flag, int *iters, double *fval, double *stats, double *sig, bool warm, double *trace);
 // Stop the kernel (if running) and wait for it to leave; the mailbox stays.
 int serve_stop(Server *srv);
+// Post the stop word to every running server of the calling thread without
+// waiting: their queued waves leave within microseconds, so a device-wide
+// synchronisation that follows (hipDeviceSynchronize, a batched solve's caller)
+// does not wait out the idle time.  The next serve_ex on a retired server joins the
+// old launch first.  Called by the batched entry points (qpb_solve*, qpb_group_solve)
+// and qpb_dropin_quiesce.
+void serve_retire_thread();
 }  // namespace qpb

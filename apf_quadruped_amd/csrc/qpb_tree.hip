@@ -989,6 +989,8 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_T_WPE) QPB_KERNEL_NAME(
 #if QPB_WARM
         a.sig[q] = sigma;
         if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
+#else
+        if (a.sig) a.sig[q] = sigma;            // options->sigma after a cold QP_SOLVE (drop-in)
 #endif
         if (a.stats) {
             double *st = a.stats + tile * (6 * 64) + ql;

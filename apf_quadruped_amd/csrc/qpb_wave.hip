@@ -1273,6 +1273,8 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #if QPB_WARM
         QPB_STS(&a.sig[q], sigma);
         if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
+#else
+        if (a.sig) QPB_STS(&a.sig[q], sigma);   // options->sigma after a cold QP_SOLVE (drop-in)
 #endif
         if (a.stats && !QPB_W_TIMING) {
             double *o = a.stats + tile * 384 + ql;
@@ -1333,11 +1335,15 @@ QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned l
         // diagnostics: every kernel argument opaque per request, so nothing derived
         // from them is computed once and carried through the request loop
         qpb_args ra = a;
-#define QPB_OPQ(f) asm volatile("" : "+s"(ra.f))
-        QPB_OPQ(P); QPB_OPQ(A); QPB_OPQ(G); QPB_OPQ(c); QPB_OPQ(h); QPB_OPQ(b);
-        QPB_OPQ(x); QPB_OPQ(y); QPB_OPQ(z); QPB_OPQ(s); QPB_OPQ(flag); QPB_OPQ(iters);
-        QPB_OPQ(fval); QPB_OPQ(stats); QPB_OPQ(B); QPB_OPQ(tol); QPB_OPQ(abstol); QPB_OPQ(sigma_d);
-        QPB_OPQ(maxit); QPB_OPQ(sig); QPB_OPQ(warm); QPB_OPQ(trace);
+        // (QPB_W_SERVE_OPQ = 1: every field; a larger value is a bit mask over the field
+        // groups below, for bisection -- bit k + 1 = group k)
+#define QPB_OPQ(k, f) if constexpr (QPB_W_SERVE_OPQ == 1 || ((QPB_W_SERVE_OPQ >> ((k) + 1)) & 1)) \
+            asm volatile("" : "+s"(ra.f))
+        QPB_OPQ(0, P); QPB_OPQ(0, A); QPB_OPQ(0, G); QPB_OPQ(0, c); QPB_OPQ(0, h); QPB_OPQ(0, b);
+        QPB_OPQ(1, x); QPB_OPQ(1, y); QPB_OPQ(1, z); QPB_OPQ(1, s);
+        QPB_OPQ(2, flag); QPB_OPQ(2, iters); QPB_OPQ(2, fval); QPB_OPQ(2, stats);
+        QPB_OPQ(3, B); QPB_OPQ(4, tol); QPB_OPQ(5, abstol); QPB_OPQ(6, sigma_d);
+        QPB_OPQ(7, maxit); QPB_OPQ(8, sig); QPB_OPQ(8, warm); QPB_OPQ(8, trace);
 #undef QPB_OPQ
         qpb_wave_body(ra, qpb_lds, tid);
 #else

@@ -313,6 +313,12 @@ int qpb_audit_dpp(const void *code, long size, char *report, long cap);
  * nanoseconds the resident wave spent on the last cold (setup) / warm (QP_SOLVE)
  * request, from seeing it to posting the answer (s_memrealtime). */
 int qpb_dropin_serve_stats(long out[4]);
+/* Post the stop word to the calling thread's queued persistent drop-in waves without
+ * waiting (they leave within microseconds): call before a device-wide synchronisation
+ * (hipDeviceSynchronize) in a thread that also ticks the drop-in, or it may wait out
+ * QPSWIFT_HIP_SERVE_IDLE_MS.  qpb_solve / qpb_solve_best / qpb_solve_warm /
+ * qpb_group_solve do this themselves.  The next QP_SOLVE relaunches (~20 us). */
+int qpb_dropin_quiesce(void);
 
 #ifdef __cplusplus
 }

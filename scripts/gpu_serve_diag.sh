@@ -1,7 +1,24 @@
-# Persistent solver, trot drop-in golden QP by QP (scripts/serve_dbg.py): one request
-# per launch (default) vs one wave answering request after request (diagnostic mode).
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-for v in oneshot multi oneshot2 multi2; do
-  ( case $v in multi*) export QPSWIFT_HIP_SERVE_LIFE_MS=10;; esac
-    timeout -k 10 120 python -u scripts/serve_dbg.py > gpurun_out/sd_$v.log 2>&1; echo "$v rc=$? bad=$(grep -c '"iters": [^5]' gpurun_out/sd_$v.log)" )
+# Persistent-solver diagnostics in one driver (replaces round 3's gpu_serve_diag2-5 and
+# gpu_serve_lat_opq): the trot drop-in golden QP by QP (scripts/serve_dbg.py) through
+# multi-request resident waves (QPSWIFT_HIP_SERVE_LIFE_MS=10 + the QPB_SERVE_DIAG=1 guard),
+# one process per variant.  Each argument is  name[:VAR=VAL[,VAR=VAL...]], e.g.
+#   bash scripts/gpu_serve_diag.sh inline opq:QPB_WAVE_OPTS=QPB_W_SERVE_OPQ=1 prera:QPB_PRERA_OFF=1
+# (QPB_WAVE_OPTS values with spaces: use '+' for the space).  oneshot:QPSWIFT_HIP_SERVE_LIFE_MS=0
+# is the shipped mode.  LAT=1 also times the tick of every variant (scripts/dropin_latency.py).
+cd "$GRAFT_REPO_ROOT"; out=gpurun_out/sd; mkdir -p $out; export TMPDIR=/tmp
+fatal() { case "$1" in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
+for spec in "$@"; do
+  name=${spec%%:*}; vars=; [ "$spec" != "$name" ] && vars=${spec#*:}
+  ( export QPSWIFT_HIP_SERVE_LIFE_MS=10 QPB_SERVE_DIAG=1
+    IFS=,; for kv in $vars; do export "${kv%%=*}=$(echo "${kv#*=}" | tr + ' ')"; done; unset IFS
+    timeout -k 10 180 python -u scripts/serve_dbg.py > $out/$name.log 2> $out/$name.err; rc=$?
+    fatal $rc $name
+    echo "$name [$vars] rc=$rc bad=$(grep -c '"iters": [^5]' $out/$name.log) n=$(grep -c '"q"' $out/$name.log)"
+    if [ "${LAT:-0}" = 1 ]; then
+      for sh in c1 c30 c30_trot; do
+        timeout -k 10 180 python -u scripts/dropin_latency.py --shape $sh --mode fast >> $out/$name.lat.jsonl 2>> $out/$name.err; rc=$?
+        fatal $rc $name.lat; [ $rc = 0 ] || exit $rc
+      done
+    fi
+    exit $rc ) || exit 1
 done

@@ -310,6 +310,32 @@ def test_dropin_resolve_sequence_matches_reference(name, null_perm, exact, monke
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", RESOLVE)
+@pytest.mark.parametrize("exact", [True, False])
+def test_dropin_resolve_without_setup_init(name, exact, monkeypatch):
+    """QPSWIFT_HIP_SETUP_INIT=0 (QP_SETUP leaves x, y, z, s unset; the first QP_SOLVE
+    is a cold solve that runs kkt_initialize itself): that cold solve must hand back
+    the sigma it ended with, so the next QP_SOLVE on the object continues from the
+    reference's options->sigma -- states after every call equal the reference's
+    (bit-identical with QPSWIFT_HIP_EXACT=1)."""
+    monkeypatch.setenv("QPSWIFT_HIP_SETUP_INIT", "0")
+    if exact:
+        monkeypatch.setenv("QPSWIFT_HIP_EXACT", "1")
+    g = golden(name)
+    n, m = int(g["n"]), int(g["m"])
+    for q in range(0, g["st_x"].shape[0], 3):
+        qp, keep = _resolve_setup(g, q, g["perm"][q])
+        try:
+            for k, (tol, maxit) in enumerate(g["calls"], start=1):
+                st = dropin.solve_again(qp, n, m, reltol=float(tol), abstol=float(tol), maxit=int(maxit))
+                _check_state(st, g, q, k, exact, f"{name}[{q}] call {k} (no setup init)")
+                if not exact:
+                    assert abs(st["sigma"] - float(g["st_sigma"][q, k])) <= 1e-6, (name, q, k)
+        finally:
+            (_lib.lib().QP_CLEANUP if "Pjc" in g else _lib.lib().QP_CLEANUP_dense)(qp)
+
+
+@pytest.mark.gpu
 def test_dropin_resolve_controller_shape():
     """The controller's 30/68/18 QP (Permut = NULL): tol 1e-2 then tightened to
     1e-6 on the same object -- flags and the cumulative IterationCount equal the
