@@ -88,6 +88,15 @@ struct qpb_args {
 #ifndef QPB_R_NLFIRST
 #define QPB_R_NLFIRST 1   // each pivot's -L(c,k) formed before the lookahead
 #endif
+#ifndef QPB_R_EARLYGWG
+#define QPB_R_EARLYGWG 0  // 1: H = H0 + G'WG formed before the exit test, between the residual products
+                          // and their reductions (independent work in the reductions' latency; wasted on
+                          // a wave's last pass), the pivot chain after it
+#endif
+#ifndef QPB_R_RCP1
+#define QPB_R_RCP1 0      // 1: pivot reciprocals without the Newton step (v_rcp_f64 alone, off the chain's
+                          // two dependent FMAs per pivot)
+#endif
 #ifndef QPB_R_ALIAS
 #define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
 #endif
@@ -116,6 +125,15 @@ static __device__ __forceinline__ double qpb_rcp_reg(double d) {
     double r = __builtin_amdgcn_rcp(d);
     r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
     asm("" : "+v"(r));     // keeps the rare regularised case from becoming a branch
+    const double reg = d > 0.0 ? 1e7 : -1e7;
+    return __builtin_fabs(d) <= 1e-14 ? reg : r;
+}
+
+// the pivot's 1 / regularise(d) (QPB_R_RCP1: the bare v_rcp_f64)
+static __device__ __forceinline__ double qpb_rcp_piv(double d) {
+    if constexpr (!QPB_R_RCP1) return qpb_rcp_reg(d);
+    double r = __builtin_amdgcn_rcp(d);
+    asm("" : "+v"(r));
     const double reg = d > 0.0 ? 1e7 : -1e7;
     return __builtin_fabs(d) <= 1e-14 ? reg : r;
 }
@@ -465,9 +483,8 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     // every 1/D as v_rcp_f64 + Newton and tracks min |D|; only when some pivot is
     // <= 1e-14 (ldl.c:273-274) is the factor redone with the regularised reciprocal
     // -- the same operations as the fast pass otherwise, so the same bits.
-    auto factor_core = [&](double w0, double w1, auto regc) -> double {
-        constexpr bool REG = decltype(regc)::value != 0;
-        double dmin = __builtin_huge_val();
+    // H = H0 + G' diag(w) G
+    auto gwg = [&](double w0, double w1) {
 #pragma unroll
         for (int e = 0; e < NX; e++) H[e] = QPB_R_REGH0 ? H0[e] : H0s[ix * NX + e];
 #if QPB_R_GWG4
@@ -509,6 +526,11 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             });
         });
 #endif
+    };
+    // LDL' of H in place
+    auto pivots = [&](auto regc) -> double {
+        constexpr bool REG = decltype(regc)::value != 0;
+        double dmin = __builtin_huge_val();
         // right-looking LDL' in natural order; the pivot recurrence is the
         // critical path: D_{k+1} comes from H'(k+1,k) and H'(k+1,k+1) with
         // exactly the operations lane k+1's own update performs
@@ -517,7 +539,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             constexpr int k = decltype(kc)::value;
             double rd;
             if constexpr (REG || !QPB_R_LAZYREG) {
-                rd = qpb_rcp_reg(dpiv);
+                rd = qpb_rcp_piv(dpiv);
             } else {
                 rd = qpb_rcp_nr(dpiv);
                 dmin = __builtin_fmin(dmin, __builtin_fabs(dpiv));
@@ -545,8 +567,13 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         });
         return dmin;
     };
-    auto factor = [&](double w0, double w1) {
-        const double dmin = factor_core(w0, w1, qpb_ic<0>{});
+    auto factor_core = [&](double w0, double w1, auto regc) -> double {
+        gwg(w0, w1);
+        return pivots(regc);
+    };
+    // the factor; early: H = H0 + G'WG was formed already (QPB_R_EARLYGWG)
+    auto factor = [&](double w0, double w1, bool early = false) {
+        const double dmin = early ? pivots(qpb_ic<0>{}) : factor_core(w0, w1, qpb_ic<0>{});
         if (QPB_R_LAZYREG && qpb_any(dmin <= 1e-14)) factor_core(w0, w1, qpb_ic<1>{});   // wave-uniform, rare
         // column c of -L, contiguous for lane c: Tx[c*NX + k] = -L(k, c)
         if (isx) {
@@ -667,6 +694,9 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         double red[4] = {isx ? rx * rx : 0.0, isy ? ry * ry : 0.0,
                          (isz0 ? rz0 * rz0 : 0.0) + (isz1 ? rz1 * rz1 : 0.0),
                          (isz0 ? s0 * z0 : 0.0) + (isz1 ? s1 * z1 : 0.0)};
+#if QPB_R_EARLYGWG && QPB_R_LATEFAC
+        gwg(w0, w1);       // independent of the residuals: issued into the reductions' latency
+#endif
         qpb_rsum<4>(red);
         const double sz = red[3];
         const double rsz = qpb_rcp(sz);            // formrho's 1 / s'z, off the predictor's chain
@@ -715,7 +745,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #if QPB_WARM
         const long tf0 = QPB_CLK();
 #endif
-        factor(w0, w1);
+        factor(w0, w1, QPB_R_EARLYGWG != 0);
 #if QPB_WARM
         { const long d_ = QPB_CLK() - tf0; t_fac += d_; t_kkt += d_; }
 #endif

@@ -403,6 +403,8 @@ def mixed_patterns_leg(tol, dev, per_pattern=1024, steps=50, warmup=5):
     B = per_pattern * len(legs)
     return {"batch": B, "patterns": [L["name"] for L in legs], "value": B * steps / el,
             "ms_per_step": el * 1e3 / steps, "kernel": group.kernel_name(), "kernel_ms": kms,
+            "traffic": traffic_for(group.kernel_name()),
+            "algorithmic_bytes_per_launch": sum(L["plan"].bytes_per_qp() * per_pattern for L in legs),
             "member_kernels": [L["plan"].kernel_name(per_pattern) for L in legs],
             "kkt_N": [L["plan"].info.N for L in legs],
             "per_plan_streams": {"value": B * steps / el_streams, "ms_per_step": el_streams * 1e3 / steps},
@@ -446,7 +448,8 @@ def trace_leg(tol, dev, steps=20, warmup=3):
     Bt = sum(Bs)
     return {"workload": f"recorded Gazebo traces: {Bt} logged steps of 5 DogBot runs, {len(Bs)} stance sets, one group launch",
             "batch": Bt, "value": Bt * steps / el, "unit": "QP solves/s", "ms_per_step": el * 1e3 / steps,
-            "kernel": grp.kernel_name(), "stance_sets": [int(b[0]) for b in batches],
+            "kernel": grp.kernel_name(), "traffic": traffic_for(grp.kernel_name()),
+            "stance_sets": [int(b[0]) for b in batches],
             "optimal_frac": float((flags == 0).float().mean().item()), "mean_iters": float(iters.mean().item()),
             "max_iters": int(iters.max().item())}
 
@@ -485,7 +488,7 @@ def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
     el = time.perf_counter() - t0
     return {"workload": f"configs[4] per-GPU share: {B} APF-sampled C1 QPs assembled on the device + solved + argmin",
             "batch": B, "value": B * steps / el, "unit": "QP solves/s", "ms_per_step": el * 1e3 / steps,
-            "input_bytes_per_qp": 18 * 8, "kernel": plan.kernel_name(B),
+            "input_bytes_per_qp": 18 * 8, "kernel": plan.kernel_name(B), "traffic": traffic_for(plan.kernel_name(B), B),
             "optimal_frac": float((out["flag"] == 0).float().mean().item())}
 
 
@@ -546,15 +549,23 @@ def controller_apf_leg(dev, K=8192, steps=20, warmup=3):
     return {"workload": f"controller call batched: {K} APF-sampled candidates of one tick, wrench + 30/68/18 "
                         "assembly on the device + solve (AMD order, tol 1e-2) + argmin",
             "batch": K, "value": K * steps / el, "unit": "QP solves/s", "ms_per_step": el * 1e3 / steps,
-            "kernel": plan.kernel_name(K), "input_bytes_per_candidate": 16,
+            "kernel": plan.kernel_name(K), "traffic": traffic_for(plan.kernel_name(K), K),
+            "algorithmic_bytes_per_launch": plan.bytes_per_qp() * K, "input_bytes_per_candidate": 16,
             "optimal_frac": float((out["flag"] == 0).float().mean().item()),
             "mean_iters": float(out["iters"].float().mean().item()), "best": best.cpu().tolist()}
 
 
-def traffic_for(kname, B):
+def traffic_for(kname, B=None):
+    """HBM bytes per launch of kernel `kname` at batch B from the PMC passes committed in
+    profiles/traffic.json (scripts/traffic_all.py); a kernel profiled at one grid only
+    (plan groups) matches by name."""
     tfile = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tfile):
-        t = json.load(open(tfile)).get(f"{kname}@{B}")
+        data = json.load(open(tfile))
+        t = data.get(f"{kname}@{B}")
+        if t is None:
+            same = [v for v in data.values() if v.get("kernel") == kname]
+            t = same[0] if len(same) == 1 else None
         if t:
             return float(t["hbm_bytes_per_launch"])
     return None
