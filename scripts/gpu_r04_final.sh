@@ -15,5 +15,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 -s KILL 400 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/fin/pmc_$c -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/fin/pmc_$c.log 2>&1
   rc=$?; echo "pmc $c rc=$rc"; fatal $rc pmc_$c; [ $rc = 0 ] || exit $rc
 done
-f=$(ls gpurun_out/fin/pmc_FETCH_SIZE/*counter_collection.csv | head -1); w=$(ls gpurun_out/fin/pmc_WRITE_SIZE/*counter_collection.csv | head -1)
+f=$(find gpurun_out/fin/pmc_FETCH_SIZE -name '*counter_collection.csv' | head -1); w=$(find gpurun_out/fin/pmc_WRITE_SIZE -name '*counter_collection.csv' | head -1)
 python3 scripts/traffic_all.py "$f" "$w" > gpurun_out/fin/traffic.log; echo "traffic rc=$?"; cp profiles/traffic.json gpurun_out/fin/traffic.json
