@@ -70,6 +70,9 @@ struct qpb_args {
 #ifndef QPB_W_EXECDBG      // 1 (diagnostics): persistent form records each request's starting EXEC mask
 #define QPB_W_EXECDBG 0
 #endif
+#ifndef QPB_W_SIGOUT       // 0 (diagnostics): the cold variants do not report sigma (round 3's code)
+#define QPB_W_SIGOUT 1
+#endif
 #ifndef QPB_W_ASMV         // 1 (diagnostics): every inline asm volatile (no CSE / motion of the DPP asm)
 #define QPB_W_ASMV 0
 #endif
@@ -1273,7 +1276,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #if QPB_WARM
         QPB_STS(&a.sig[q], sigma);
         if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
-#else
+#elif QPB_W_SIGOUT
         if (a.sig) QPB_STS(&a.sig[q], sigma);   // options->sigma after a cold QP_SOLVE (drop-in)
 #endif
         if (a.stats && !QPB_W_TIMING) {

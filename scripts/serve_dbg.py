@@ -14,3 +14,8 @@ for q in order:
                            ordering=int(g["ordering"]), reltol=tol, abstol=tol, maxit=maxit)
     print(json.dumps({"q": q, "flag": r["flag"], "iters": r["iters"], "g_iters": int(g["iters"][q]),
                       "dx": float(np.abs(r["x"] - g["x"][q]).max()), "dz": float(np.abs(r["z"] - g["z"][q]).max())}))
+import ctypes as C
+from apf_quadruped_amd import _lib
+st = (C.c_long * 4)()
+_lib.lib().qpb_dropin_serve_stats(st)
+print(json.dumps({"serve_requests": int(st[0]), "serve_launches": int(st[1])}))
