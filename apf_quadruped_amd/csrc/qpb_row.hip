@@ -97,6 +97,11 @@ struct qpb_args {
 #define QPB_R_RCP1 0      // 1: pivot reciprocals without the Newton step (v_rcp_f64 alone, off the chain's
                           // two dependent FMAs per pivot)
 #endif
+#ifndef QPB_R_SPLIT
+#define QPB_R_SPLIT 0     // 1: two waves per four QPs (128-thread workgroups): wave 0 factors, solves and
+                          // updates, wave 1 forms the residuals (and the exit test) while wave 0 factors;
+                          // they swap residuals and iterate through LDS, two barriers per pass
+#endif
 #ifndef QPB_R_ALIAS
 #define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
 #endif
@@ -334,13 +339,27 @@ static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, doub
 #define OFF_H0 EVEN(OFF_PR + NX * NX)
 #define LOOP_END EVEN(OFF_H0 + NX * NX)
 #define LDS_ROW (LOOP_END > STG_END ? LOOP_END : STG_END)
+// QPB_R_SPLIT: per row, the iterate wave 0 forms (x y z0 z1 s0 s1: 6 x 16) and the residuals
+// wave 1 forms (rx ry rz0 rz1 -P x: 5 x 16, the four row sums)
+#define XCH_ROW (6 * 16 + 5 * 16 + 4)
+#define LDS_ALL (WPB * 4 * LDS_ROW + (QPB_R_SPLIT ? 4 * XCH_ROW : 0))
+#if QPB_R_SPLIT && (QPB_WARM || QPB_SERVE || defined(QPB_GROUP))
+#error "the split row form is a cold batched kernel only"
+#endif
 
 // one logical block `lb` of the plan's batch (QPs 4 (lb WPB + wave) ..); qoff
 // offsets the indices the fused argmin reports (the plan's first QP in a group)
 static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, long qoff, double *qpb_lds) {
     const int lane = threadIdx.x & 63, row = lane >> 4, c = lane & 15;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if QPB_R_SPLIT
+    const int role = wv;                       // 0: factor, solves, updates; 1: residuals
+    const long q0 = lb * 4;                    // both waves of the workgroup: the same four QPs
+    double *__restrict__ Xc = qpb_lds + WPB * 4 * LDS_ROW + row * XCH_ROW;
+#else
+    constexpr int role = 0;
     const long q0 = (lb * WPB + wv) * 4;
+#endif
 #if QPB_R_TIMING == 3
     double tph[6] = {0, 0, 0, 0, 0, 0};
     long tcy = (long)__builtin_readcyclecounter();
@@ -670,38 +689,57 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         const double kd0 = isz0 ? -s0 * rzi0 : -1.0, kd1 = isz1 ? -s1 * rzi1 : -1.0;
         const double w0 = -qpb_rcp_reg(kd0), w1 = -qpb_rcp_reg(kd1);
         // residuals (Auxilary.c:745-786)
-        qpb_fence(x, y, z0, z1);
-        double tp = 0.0, ry = by, rz0 = hz0 - s0, rz1 = hz1 - s1, nPr[NX];
+        double tp, ry, rz0, rz1, rx, red[4];
+        auto residuals = [&](bool early_gwg) {
+            qpb_fence(x, y, z0, z1);
+            double nPr[NX];
+            tp = 0.0; ry = by; rz0 = hz0 - s0; rz1 = hz1 - s1;
 #pragma unroll
-        for (int j = 0; j < NX; j++) nPr[j] = QPB_R_REGH0 ? nP[j] : PR[ix * NX + j];
-        qpb_for<0, NX>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            qpb_fx<j>(rz0, x, nGl[j]);
-            if constexpr (ZH && qpb_ghmask[j]) qpb_fx<j>(rz1, x, nGh[j]);
-            if constexpr (NY > 0) qpb_fx<j>(ry, x, nAr[j]);
-            qpb_fx<j>(tp, x, nPr[j]);              // -P x
-        });
-        double ra[4] = {-cx, 0.0, 0.0, 0.0};
-        qpb_for<0, NZ>([&](auto rc) {
-            constexpr int r = decltype(rc)::value;
-            qpb_fx<(r & 15)>(ra[r & 3], r < 16 ? z0 : z1, nGc[r]);
-        });
-        qpb_for<0, NY>([&](auto lc) {
-            constexpr int l = decltype(lc)::value;
-            qpb_fx<l>(ra[(NZ + l) & 3], y, nAc[l]);
-        });
-        const double rx = ((ra[0] + ra[1]) + (ra[2] + ra[3])) + tp;
-        double red[4] = {isx ? rx * rx : 0.0, isy ? ry * ry : 0.0,
-                         (isz0 ? rz0 * rz0 : 0.0) + (isz1 ? rz1 * rz1 : 0.0),
-                         (isz0 ? s0 * z0 : 0.0) + (isz1 ? s1 * z1 : 0.0)};
-#if QPB_R_EARLYGWG && QPB_R_LATEFAC
-        gwg(w0, w1);       // independent of the residuals: issued into the reductions' latency
+            for (int j = 0; j < NX; j++) nPr[j] = QPB_R_REGH0 ? nP[j] : PR[ix * NX + j];
+            qpb_for<0, NX>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                qpb_fx<j>(rz0, x, nGl[j]);
+                if constexpr (ZH && qpb_ghmask[j]) qpb_fx<j>(rz1, x, nGh[j]);
+                if constexpr (NY > 0) qpb_fx<j>(ry, x, nAr[j]);
+                qpb_fx<j>(tp, x, nPr[j]);              // -P x
+            });
+            double ra[4] = {-cx, 0.0, 0.0, 0.0};
+            qpb_for<0, NZ>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                qpb_fx<(r & 15)>(ra[r & 3], r < 16 ? z0 : z1, nGc[r]);
+            });
+            qpb_for<0, NY>([&](auto lc) {
+                constexpr int l = decltype(lc)::value;
+                qpb_fx<l>(ra[(NZ + l) & 3], y, nAc[l]);
+            });
+            rx = ((ra[0] + ra[1]) + (ra[2] + ra[3])) + tp;
+            red[0] = isx ? rx * rx : 0.0;
+            red[1] = isy ? ry * ry : 0.0;
+            red[2] = (isz0 ? rz0 * rz0 : 0.0) + (isz1 ? rz1 * rz1 : 0.0);
+            red[3] = (isz0 ? s0 * z0 : 0.0) + (isz1 ? s1 * z1 : 0.0);
+            if (early_gwg) gwg(w0, w1);   // independent of the residuals: issued into the reductions' latency
+            qpb_rsum<4>(red);
+        };
+#if QPB_R_SPLIT
+        if (role == 1) {
+            residuals(false);
+            Xc[96 + c] = rx; Xc[112 + c] = ry; Xc[128 + c] = rz0; Xc[144 + c] = rz1; Xc[160 + c] = tp;
+            if (c == 0) { Xc[176] = red[0]; Xc[177] = red[1]; Xc[178] = red[2]; Xc[179] = red[3]; }
+        } else {
+            factor(w0, w1);              // while wave 1 forms the residuals (wasted on the last pass)
+        }
+        __syncthreads();
+        if (role == 0) {
+            rx = Xc[96 + c]; ry = Xc[112 + c]; rz0 = Xc[128 + c]; rz1 = Xc[144 + c]; tp = Xc[160 + c];
+            red[0] = Xc[176]; red[1] = Xc[177]; red[2] = Xc[178]; red[3] = Xc[179];
+        }
+#else
+        residuals(QPB_R_EARLYGWG && QPB_R_LATEFAC);
 #endif
-        qpb_rsum<4>(red);
         const double sz = red[3];
         const double rsz = qpb_rcp(sz);            // formrho's 1 / s'z, off the predictor's chain
         QPB_TM(1);
-#if !QPB_R_LATEFAC
+#if !QPB_R_LATEFAC && !QPB_R_SPLIT
         // the factor does not depend on the residuals: formed before the exit
         // test (wasted on a row's last iteration), overlapping the reductions
         factor(w0, w1);
@@ -740,7 +778,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             mu = mu_it;
             pc = sigma > a.sigma_d;
         }
-#if QPB_R_LATEFAC
+#if QPB_R_LATEFAC && !QPB_R_SPLIT
         // factor after the exit test: the wave's last pass skips it
 #if QPB_WARM
         const long tf0 = QPB_CLK();
@@ -764,9 +802,22 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             ap = bm[0] > 1e-10 ? __builtin_amdgcn_rcp(bm[0]) : 1.0;
             ad = bm[1] > 1e-10 ? __builtin_amdgcn_rcp(bm[1]) : 1.0;
         };
+#if QPB_R_SPLIT
+        // wave 0's iterate to wave 1 (its next residuals)
+        auto exchange = [&]() {
+            if (role == 0) {
+                Xc[c] = x; Xc[16 + c] = y; Xc[32 + c] = z0; Xc[48 + c] = z1; Xc[64 + c] = s0; Xc[80 + c] = s1;
+            }
+            __syncthreads();
+            if (role == 1) {
+                x = Xc[c]; y = Xc[16 + c]; z0 = Xc[32 + c]; z1 = Xc[48 + c]; s0 = Xc[64 + c]; s1 = Xc[80 + c];
+            }
+        };
+#endif
         if (!QPB_WARM && it < 0) {
             // setup solve, rhs [-c; b; h] (Auxilary.c:1010-1040): x0, y0; then
             // s0, z0 from r = h - G x0 = -dz (w = 1 exactly here)
+          if (role == 0) {
             solve(w0, w1, -cx, by, hz0, hz1, dx, dy, dz0, dz1);
             x = isx ? dx : 0.0;
             y = isy ? dy : 0.0;
@@ -781,10 +832,15 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             z1 = hi < 0 ? -zi1 : -zi1 + (1 + hi);
             if (!isz0) { s0 = 1.0; z0 = 1.0; }
             if (!isz1) { s1 = 1.0; z1 = 1.0; }
+          }
+#if QPB_R_SPLIT
+            exchange();
+#endif
             it = 0;
             QPB_TM(0);
             continue;
         }
+      if (role == 0) {
         if (qpb_any(act && pc)) {
             // predictor (kktsolve_1, Auxilary.c:471-515), ds = -s.*z
 #if QPB_WARM
@@ -837,6 +893,10 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             if (isz0) { s0 = __builtin_fma(dsl0, ap, s0); z0 = __builtin_fma(dz0, ad, z0); }
             if (isz1) { s1 = __builtin_fma(dsl1, ap, s1); z1 = __builtin_fma(dz1, ad, z1); }
         }
+      }   // role == 0
+#if QPB_R_SPLIT
+        exchange();
+#endif
         it++;
         QPB_TM(4);
     }
@@ -844,7 +904,8 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     qpb_rsum<1>(fr);
     // fused argmin first: the arrival's store -> s_waitcnt vmcnt(0) -> atomic round
     // trip then waits for the wave's partial only, not for its output stores
-    if (a.best) {
+    if (a.best && role != 0) qpb_argmin_arrive(a, __builtin_huge_val(), -1);   // QPB_R_SPLIT's wave 1
+    if (a.best && role == 0) {
         // this wave's best: rows are QPs (fval / flag uniform within a row)
         double bv = __builtin_huge_val();
         long bi = -1;
@@ -857,7 +918,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         qpb_argmin_arrive(a, bv, bi);
     }
     // ---- outputs (tiled SoA)
-    if (valid) {
+    if (valid && role == 0) {
         if (isx) QPB_STS(&a.x[tile * (NX * 64) + c * 64 + ql], x);
 #if NY > 0
         if (isy) QPB_STS(&a.y[tile * (NY * 64) + c * 64 + ql], y);
@@ -930,7 +991,7 @@ QPB_KERNEL_NAME(qpb_args a, qpb_mailbox *mb, unsigned long long last, unsigned l
 }
 #else
 extern "C" __global__ void __launch_bounds__(QPB_WG, QPB_R_WPE) QPB_KERNEL_NAME(qpb_args a) {
-    __shared__ __attribute__((aligned(16))) double qpb_lds[WPB * 4 * LDS_ROW];
+    __shared__ __attribute__((aligned(16))) double qpb_lds[LDS_ALL];
     qpb_row_body(a, qpb_xcd_block(), 0, qpb_lds);
 }
 #endif

@@ -456,6 +456,12 @@ int compile_wave(qpb_plan *plan) {
     return compile_kernel(plan->wave_kname, [plan] { return wave_source_of(plan); }, false, &plan->wave_code);
 }
 
+int compile_rowsplit(qpb_plan *plan) {
+    if (!plan->row_split) return fail(QPB_EINVAL, "plan has no split row kernel");
+    return compile_kernel(plan->rowsplit_kname, [plan] { return generate_row_kernel(plan->pl, nullptr, 1, true); },
+                          false, &plan->rowsplit_code);
+}
+
 int compile_row2(qpb_plan *plan) {
     if (plan->row_occ_batch < 0) return fail(QPB_EINVAL, "plan has no two-wave row kernel");
     return compile_kernel(plan->row2_kname, [plan] { return generate_row_kernel(plan->pl, nullptr, 2); }, false,
@@ -743,6 +749,8 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
             plan->row_occ_batch = 4096;
             if (const char *e = getenv("QPB_ROW_OCC_BATCH")) plan->row_occ_batch = atol(e);
             if (plan->row_occ_batch >= 0) qpb::generate_row_kernel(plan->pl, &plan->row2_kname, 2);
+            if (const char *e = getenv("QPB_ROW_SPLIT")) plan->row_split = atoi(e) > 0;
+            if (plan->row_split) qpb::generate_row_kernel(plan->pl, &plan->rowsplit_kname, 1, true);
         } else {
             plan->wave_wg = qpb::wave_wg_for(plan->pl);
             qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
@@ -838,7 +846,8 @@ long qpb_plan_kernel_name(const qpb_plan *plan, long B, char *buf, long cap) {
     const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
                                         (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
     const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
-    const std::string &s = wave ? (plan->row_occ_batch >= 0 && B > plan->row_occ_batch ? plan->row2_kname : plan->wave_kname)
+    const std::string &s = wave ? (plan->row_occ_batch >= 0 && B > plan->row_occ_batch ? plan->row2_kname
+                                   : plan->row_split ? plan->rowsplit_kname : plan->wave_kname)
                          : tree ? (plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch ? plan->tree2_kname : plan->tree_kname)
                                 : plan->kname;
     if (buf && cap > 0) {
@@ -888,6 +897,7 @@ int qpb_plan_compile(qpb_plan *plan) {
     if (k == 1 || (k == 0 && !plan->large_tree)) rc = qpb::compile_plan(plan);
     if (!rc && plan->wave_ok && (k == 0 || k == 2)) rc = qpb::compile_wave(plan);
     if (!rc && plan->wave_ok && (k == 0 || k == 2) && plan->row_occ_batch >= 0) rc = qpb::compile_row2(plan);
+    if (!rc && plan->wave_ok && (k == 0 || k == 2) && plan->row_split) rc = qpb::compile_rowsplit(plan);
     if (!rc && plan->tree_ok && (k == 3 || (k == 0 && plan->large_tree))) rc = qpb::compile_tree(plan);
     if (!rc && plan->tree_ok && (k == 3 || (k == 0 && plan->large_tree)) && plan->tree_occ_batch >= 0)
         rc = qpb::compile_tree2(plan);
@@ -918,11 +928,13 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
     hipFunction_t fn;
     const bool row2 = wave && plan->row_occ_batch >= 0 && B > plan->row_occ_batch;
     const bool tree2 = tree && plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch;
+    const bool split = wave && !row2 && !warm && plan->row_split;      // cold batched solves only
     int rc;
     if (!warm) {
-        rc = row2 ? qpb::compile_row2(plan) : wave ? qpb::compile_wave(plan)
+        rc = split ? qpb::compile_rowsplit(plan) : row2 ? qpb::compile_row2(plan) : wave ? qpb::compile_wave(plan)
            : tree2 ? qpb::compile_tree2(plan) : tree ? qpb::compile_tree(plan) : qpb::compile_plan(plan);
-        if (!rc) rc = row2 ? qpb::load_function(plan->row2_kname, plan->row2_code, &fn)
+        if (!rc) rc = split ? qpb::load_function(plan->rowsplit_kname, plan->rowsplit_code, &fn)
+                    : row2 ? qpb::load_function(plan->row2_kname, plan->row2_code, &fn)
                     : wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
                     : tree2 ? qpb::load_function(plan->tree2_kname, plan->tree2_code, &fn)
                     : tree ? qpb::load_function(plan->tree_kname, plan->tree_code, &fn)
@@ -964,8 +976,9 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
     // and the gap between two dependent launches; up to 4 096 waves
     bool fused = false;
     void *params[] = {&a};
-    const unsigned wg = (unsigned)(wave ? plan->wave_wg : tree2 ? plan->tree2_wg : tree ? plan->tree_wg : plan->gen.wg);
-    const long per_block = wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup
+    const unsigned wg = (unsigned)(split ? 128 : wave ? plan->wave_wg : tree2 ? plan->tree2_wg : tree ? plan->tree_wg
+                                                                  : plan->gen.wg);
+    const long per_block = split ? 4 : wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup
     unsigned grid = (unsigned)((B + per_block - 1) / per_block);
     if (wave || tree) grid = (grid + 7) & ~7u;      // XCD-aware block order (qpb_xcd_block)
     if (best && wave && plan->wave_qpw == 4 && !getenv("QPB_NO_FUSED_ARGMIN")) {

@@ -27,6 +27,11 @@ struct qpb_plan {
     std::string row2_kname;
     std::shared_ptr<std::vector<char>> row2_code;
     long row_occ_batch = -1;
+    // the split form of the one-wave row kernel (QPB_R_SPLIT: two waves per four QPs),
+    // used instead of it when row_split (QPB_ROW_SPLIT=1) for cold batched solves
+    bool row_split = false;
+    std::string rowsplit_kname;
+    std::shared_ptr<std::vector<char>> rowsplit_code;
     bool tree_ok = false;                       // tree kernel (one QP per workgroup, any pattern)
     bool large_tree = false;                    // auto: tree (not lane) kernel beyond the wave kernel's range
     int tree_wg = 256;
@@ -66,6 +71,7 @@ int strided_copy(const CopySegs &t, void *stream);
 int compile_plan(qpb_plan *plan);
 int compile_wave(qpb_plan *plan);
 int compile_row2(qpb_plan *plan);
+int compile_rowsplit(qpb_plan *plan);
 int compile_tree2(qpb_plan *plan);
 int compile_tree(qpb_plan *plan);
 int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,

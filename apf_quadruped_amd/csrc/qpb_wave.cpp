@@ -129,7 +129,9 @@ static void common_header(std::ostringstream &o, const Plan &pl, int wg, const c
         std::string kv;
         while (in >> kv) {
             const size_t eq = kv.find('=');
-            if (eq != std::string::npos) o << "#define " << kv.substr(0, eq) << " " << kv.substr(eq + 1) << "\n";
+            // QPB_R_SPLIT changes the launch shape: selected per plan by QPB_ROW_SPLIT, never here
+            if (eq != std::string::npos && kv.substr(0, eq) != "QPB_R_SPLIT")
+                o << "#define " << kv.substr(0, eq) << " " << kv.substr(eq + 1) << "\n";
         }
     }
     const long nP = pl.Pin.nnz(), nA = p ? pl.A.nnz() : 0, nG = pl.G.nnz();
@@ -195,10 +197,17 @@ static std::string row_prefix(const Plan &pl) {
     return o.str();
 }
 
-std::string generate_row_kernel(const Plan &pl, std::string *name_out, int wpe) {
+// split: the two-wave form of the one-wave kernel (QPB_R_SPLIT, 128-thread workgroups,
+// one four-QP group per workgroup: wave 0 factors while wave 1 forms the residuals)
+std::string generate_row_kernel(const Plan &pl, std::string *name_out, int wpe, bool split) {
+    std::string prefix = row_prefix(pl);
+    if (split) {
+        const std::string wg = "#define QPB_WG 64\n";
+        prefix.replace(prefix.find(wg), wg.size(), "#define QPB_WG 128\n#define QPB_R_SPLIT 1\n");
+    }
     const std::string body = (wpe > 1 ? "#define QPB_R_WPE " + std::to_string(wpe) + "\n" : std::string()) +
-                             row_prefix(pl) + kRowTemplate;
-    const std::string name = named(body, "qpb_row", pl, 64);
+                             prefix + kRowTemplate;
+    const std::string name = named(body, split ? "qpb_rowsplit" : "qpb_row", pl, split ? 128 : 64);
     if (name_out) *name_out = name;
     return "#define QPB_KERNEL_NAME " + name + "\n" + body;
 }

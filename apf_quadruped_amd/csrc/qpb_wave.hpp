@@ -28,7 +28,7 @@ std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out);
 bool row_eligible(const Plan &pl);
 // wpe: waves per SIMD the register allocation must allow (QPB_R_WPE; 2 for large
 // batches, where two waves per SIMD hide the latency the single wave exposes)
-std::string generate_row_kernel(const Plan &pl, std::string *name_out, int wpe = 1);
+std::string generate_row_kernel(const Plan &pl, std::string *name_out, int wpe = 1, bool split = false);
 // One kernel for up to QPB_GROUP_MAX row-form plans (qpb_group_*): logical
 // blocks [bend[i-1], bend[i]) run member i.
 constexpr int QPB_GROUP_MAX = 16;
