@@ -50,6 +50,13 @@ struct KernelArgs {
     // recorded, then per loop pass i < QPB_TRACE_MAX: fval, n_rx, n_ry, n_rz, n_mu
     // (before the exit test) and alpha_p, alpha_d (after the update) at [4 + 7 i ..]
     double *trace = nullptr;
+    // persistent (QPB_SERVE) warm variants, one QP: the state to continue from as one
+    // contiguous block the host writes and the kernel only reads -- x[n] y[p] z[m] s[m],
+    // {flag, iters} (two ints in one double), sigma -- instead of the output slots.  A
+    // resident wave re-reading a host-memory line it wrote itself during an earlier
+    // request was measured to get its own old bytes, not the host's later write
+    // (DESIGN §4i); NULL: read the output slots (launched kernels)
+    const double *win = nullptr;
 };
 constexpr int QPB_TRACE_MAX = 256;
 constexpr long QPB_TRACE_STRIDE = 4 + 7L * QPB_TRACE_MAX;

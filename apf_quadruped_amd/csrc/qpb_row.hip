@@ -56,6 +56,7 @@ struct qpb_args {
     double *sig;              // per-QP sigma: in (warm) / out (NULL: not tracked)
     long warm;                // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
     double *trace;            // warm variant: per-QP timers + per-iteration statistics (or NULL)
+    const double *win;        // persistent warm variants: x y z s {flag, iters} sigma to continue from (or NULL)
 };
 
 // Staging / H0 knobs.  Round 1 saw an illegal-address fault with ZF128, AADPP and
@@ -652,6 +653,20 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #if QPB_WARM
     // warm variant (qpb_solve_warm): QP_SOLVE continues from the object's iterate,
     // IterationCount and options->sigma (qpSWIFT.c:502-596 never re-initialises)
+#if QPB_SERVE
+    // the host's block (KernelArgs::win, QP 0): never a line this wave wrote
+    const double *wi = a.win;
+    if (isx) x = QPB_LDS(&wi[c]);
+#if NY > 0
+    if (isy) y = QPB_LDS(&wi[NX + c]);
+#endif
+    if (isz0) { z0 = QPB_LDS(&wi[NX + NY + c]); s0 = QPB_LDS(&wi[NX + NY + NZ + c]); }
+    if (isz1) { z1 = QPB_LDS(&wi[NX + NY + 16 + c]); s1 = QPB_LDS(&wi[NX + NY + NZ + 16 + c]); }
+    const int *wfl = reinterpret_cast<const int *>(wi + NX + NY + 2 * NZ);
+    const long it0 = QPB_LDS(&wfl[1]);
+    const int flag0 = QPB_LDS(&wfl[0]);
+    sigma = QPB_LDS(&wi[NX + NY + 2 * NZ + 1]);
+#else
     if (isx) x = QPB_LDS(&a.x[tile * (NX * 64) + c * 64 + ql]);
 #if NY > 0
     if (isy) y = QPB_LDS(&a.y[tile * (NY * 64) + c * 64 + ql]);
@@ -661,6 +676,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     const long it0 = QPB_LDS(&a.iters[qc]);   // IterationCount the QP enters with
     const int flag0 = QPB_LDS(&a.flag[qc]);   // stats->Flag it enters with (QP_FATAL after setup)
     sigma = QPB_LDS(&a.sig[qc]);
+#endif
     it = 0;
     double sigf = sigma;       // options->sigma when this row's loop ends (a frozen row's own
                                // sigma keeps being recomputed while the rest of the wave runs)

@@ -1080,9 +1080,9 @@ qpb::Server::~Server() {
 int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A, const double *G, const double *c,
                   const double *h, const double *b, const qpb_settings *st, double *x, double *y, double *z,
                   double *s, int *flag, int *iters, double *fval, double *stats, double *sig, bool warm,
-                  double *trace) {
+                  double *trace, const double *win) {
     if (!plan || !srv) return fail(QPB_EINVAL, "NULL plan or server");
-    if (warm && !sig) return fail(QPB_EINVAL, "a warm solve needs sigma");
+    if (warm && (!sig || !win)) return fail(QPB_EINVAL, "a warm solve needs sigma and the state block");
     const qpb::Plan &pl = plan->pl;
     if (!P || !G || !c || !h || !x || !z || !s || !flag || !iters || !fval) return fail(QPB_EINVAL, "NULL data pointer");
     if (pl.p > 0 && (!A || !b || !y)) return fail(QPB_EINVAL, "p > 0 needs A, b and y");
@@ -1113,6 +1113,7 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
     a.sig = sig;
     a.warm = warm ? 1 : 0;
     a.trace = warm ? trace : nullptr;
+    a.win = warm ? win : nullptr;
     if (!srv->mb) {
         void *m = nullptr;
         if (hipHostMalloc(&m, 512, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)

@@ -55,6 +55,7 @@ struct qpb_args {
     double *sig;                  // per-QP sigma: in (warm) / out (NULL: not tracked)
     long warm;                    // 1: continue from x, y, z, s, iters, flag, sig (no kkt_initialize)
     double *trace;            // warm variant: per-QP timers + per-iteration statistics (or NULL)
+    const double *win;        // persistent warm variants: x y z s {flag, iters} sigma to continue from (or NULL)
 };
 
 #ifndef QPB_WARM
@@ -1000,6 +1001,24 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #if QPB_WARM
     // warm variant (qpb_solve_warm): QP_SOLVE continues from the object's iterate,
     // IterationCount and options->sigma (qpSWIFT.c:502-596 never re-initialises)
+#if QPB_SERVE
+    // the host's block (KernelArgs::win): never a line this wave wrote
+    const double *wi = a.win;
+    if (isx) x = QPB_LDS(&wi[lane]);
+#if NY > 0
+    if (isy) y = QPB_LDS(&wi[NX + lane]);
+#endif
+#pragma unroll
+    for (int t = 0; t < ZC; t++)
+        if (isz[t]) {
+            z[t] = QPB_LDS(&wi[NX + NY + lane + 64 * t]);
+            s[t] = QPB_LDS(&wi[NX + NY + NZ + lane + 64 * t]);
+        }
+    const int *wfl = reinterpret_cast<const int *>(wi + NX + NY + 2 * NZ);
+    const long it0 = QPB_LDS(&wfl[1]);
+    const int flag0 = QPB_LDS(&wfl[0]);
+    sigma = QPB_LDS(&wi[NX + NY + 2 * NZ + 1]);
+#else
     if (isx) x = QPB_LDS(&a.x[tile * (NX * 64) + lane * 64 + ql]);
 #if NY > 0
     if (isy) y = QPB_LDS(&a.y[tile * (NY * 64) + lane * 64 + ql]);
@@ -1013,6 +1032,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     const long it0 = QPB_LDS(&a.iters[q]);   // IterationCount the QP enters with
     const int flag0 = QPB_LDS(&a.flag[q]);   // stats->Flag it enters with (QP_FATAL after setup)
     sigma = QPB_LDS(&a.sig[q]);
+#endif
     it = 0;
     // the drop-in's timers and verbose trace (KernelArgs::trace, qpb_codegen.hpp):
     // s_memrealtime ticks in the factorisations and in factor + solves, and the

@@ -92,7 +92,7 @@ struct Priv {
     double *zmem = nullptr, *zdev = nullptr;   // zero-copy slab (host / device address)
     long nP = 0, nA = 0, nG = 0, nin = 0, nout = 0;
     long oP = 0, oA = 0, oG = 0, oc = 0, oh = 0, ob = 0, ox = 0, oy = 0, oz = 0, os = 0, ost = 0, ofv = 0,
-         oin = 0, oout = 0, otr = 0, ototal = 0;
+         oin = 0, oout = 0, otr = 0, owin = 0, ototal = 0;
     // kkt_initialize's point is in x, y, z, s (QP_SETUP ran it on the device):
     // QP_SOLVE then continues from the object's state (a warm solve), as the
     // reference's QP_SOLVE always does; otherwise its first QP_SOLVE is cold
@@ -398,6 +398,10 @@ int ensure_device(Priv &v, const QP &q) {
         v.oin = take(v.nin);
         v.oout = take(v.nout + 2);              // + flag, iters (two ints in one double slot), sigma
         v.otr = take(qpb::QPB_TRACE_STRIDE);   // timers + per-iteration statistics (warm solves)
+        // the warm state the persistent solver continues from, on 128-B lines of its own
+        // that only the host writes (KernelArgs::win)
+        o = (o + 15) & ~15L;
+        v.owin = take(((q.n + q.p + 2 * q.m + 2) + 15) & ~15L);
         v.ofv = v.oout + v.nout - 1;
         v.ototal = o;
     }
@@ -555,6 +559,14 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
         const int iv[2] = {(int)v.st.Flag, (int)v.st.IterationCount};
         std::memcpy(h + ofl, iv, sizeof(iv));
         h[osg] = q.options->sigma;
+        // the same state, contiguous, for a resident wave (never read from the slots it writes)
+        double *wi = h + v.owin;
+        std::memcpy(wi, q.x, sizeof(double) * (size_t)n);
+        if (p > 0) std::memcpy(wi + n, q.y, sizeof(double) * (size_t)p);
+        std::memcpy(wi + n + p, q.z, sizeof(double) * (size_t)m);
+        std::memcpy(wi + n + p + m, q.s, sizeof(double) * (size_t)m);
+        std::memcpy(wi + n + p + 2 * m, iv, sizeof(iv));
+        wi[n + p + 2 * m + 1] = q.options->sigma;
     }
     int *dfl = reinterpret_cast<int *>(d + ofl);
     // the persistent solver answers without a launch; plans whose one-QP kernel has
@@ -563,7 +575,8 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     if (serve_enabled())
         rc = qpb::serve_ex(v.plan.get(), &v.srv[cs.warm ? 1 : 0], d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG,
                            d + v.oc, d + v.oh, p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr,
-                           d + v.oz, d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, d + osg, cs.warm, d + v.otr);
+                           d + v.oz, d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, d + osg, cs.warm, d + v.otr,
+                           d + v.owin);
     if (rc == qpb::SERVE_NONE) {
         rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
                            p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz,
