@@ -431,7 +431,10 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     for (int k = 2 * c; k < STG_END; k += 32)
         *reinterpret_cast<double2 *>(Ls + k) = double2{0.0, 0.0};   // 16-byte stores (STG_END, LDS_ROW even)
 #else
-    for (int k = c; k < STG_END; k += 16) Ls[k] = 0.0;
+    // unrolled (a compile-time trip count): the rolled loop cost ~7 instructions per store
+#pragma unroll
+    for (int i = 0; i < (STG_END + 15) / 16; i++)
+        if (c + 16 * i < STG_END) Ls[c + 16 * i] = 0.0;
 #endif
     qpb_wsync();
 #pragma unroll
@@ -750,7 +753,14 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             red[0] = Xc[176]; red[1] = Xc[177]; red[2] = Xc[178]; red[3] = Xc[179];
         }
 #else
-        residuals(QPB_R_EARLYGWG && QPB_R_LATEFAC);
+        if (QPB_WARM || it >= 0) {
+            residuals(QPB_R_EARLYGWG && QPB_R_LATEFAC);
+        } else {
+            // kkt_initialize's pass (iteration -1) has no exit test: no residuals
+            rx = ry = rz0 = rz1 = tp = 0.0;
+            red[0] = red[1] = red[2] = 0.0;
+            red[3] = 1.0;
+        }
 #endif
         const double sz = red[3];
         const double rsz = qpb_rcp(sz);            // formrho's 1 / s'z, off the predictor's chain

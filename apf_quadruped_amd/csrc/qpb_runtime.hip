@@ -1012,9 +1012,10 @@ unsigned long long serve_idle_ticks() {
 // 0 (the default): a launch answers ONE request and leaves, and the host launches the
 // next wave as soon as it has the answer, so the next call still finds a wave waiting.
 // A wave that answers request after request (QPSWIFT_HIP_SERVE_LIFE_MS > 0, then also
-// its lifetime) was measured to carry state from one request into the next in some
-// kernels -- the trot drop-in golden's warm solves went wrong from a wave's second
-// request on -- so it is a diagnostic mode only.
+// its lifetime) was measured to go wrong in some kernel builds -- the AMD-ordered trot
+// kernel's resident setup wave returned wrong initial points from its second or third
+// request on, depending on the loop's code layout -- so it is a
+// diagnostic mode only.
 // It is refused unless QPB_SERVE_DIAG=1 is set as well, so the knob alone can never
 // put wrong answers into a controller.
 unsigned long long serve_life_ticks() {
@@ -1144,8 +1145,12 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
     if (srv->running && (srv->kname != kn || std::memcmp(&srv->args, &a, sizeof a) != 0) && (rc = serve_stop(srv)))
         return rc;
     unsigned long long *req = srv->mb, *ack = srv->mb + 16;
+    // (diagnostics: QPB_SERVE_DIAG_ONLY=cold|warm keeps the other kind one-shot)
+    const char *only = getenv("QPB_SERVE_DIAG_ONLY");
+    const unsigned long long life_k =
+        (only && *only && std::strcmp(only, warm ? "warm" : "cold") != 0) ? 0ull : serve_life_ticks();
     auto launch = [&](unsigned long long last) {
-        unsigned long long idle = serve_idle_ticks(), life = serve_life_ticks();
+        unsigned long long idle = serve_idle_ticks(), life = life_k;
         void *mbd = srv->mb_dev;
         void *params[] = {&a, &mbd, &last, &idle, &life};
         const hipError_t e = hipModuleLaunchKernel(fn, 1, 1, 1, 64, 1, 1, 0, sm, params, nullptr);
@@ -1157,7 +1162,7 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
         return QPB_OK;
     };
     // a kernel that left on its own (idle) is relaunched before the request
-    if (srv->running && serve_life_ticks() != 0) {
+    if (srv->running && life_k != 0) {
         const hipError_t q = hipStreamQuery(sm);
         if (q == hipSuccess) srv->running = false;
         else if (q != hipErrorNotReady) {
@@ -1172,7 +1177,7 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
     // whatever may still be waiting and launches afresh, so a request is never posted
     // to a wave that may already have left (its idle clock starts after the previous
     // answer the host saw, within microseconds).
-    const bool oneshot = serve_life_ticks() == 0;
+    const bool oneshot = life_k == 0;
     const long long now_ns = std::chrono::duration_cast<std::chrono::nanoseconds>(
                                  std::chrono::steady_clock::now().time_since_epoch()).count();
     if (oneshot && srv->running && (double)(now_ns - srv->last_answer_ns) > 0.5e1 * (double)serve_idle_ticks() &&
@@ -1180,6 +1185,9 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
         return rc;
     if (!srv->running && (rc = launch(srv->seq))) return rc;
     const unsigned long long r = ++srv->seq;
+    // (diagnostics: QPB_SERVE_PREDELAY_US holds the request back after the inputs were written)
+    static const long predelay = getenv("QPB_SERVE_PREDELAY_US") ? atol(getenv("QPB_SERVE_PREDELAY_US")) : 0;
+    if (predelay > 0) std::this_thread::sleep_for(std::chrono::microseconds(predelay));
     mb_store(req, r);
     srv->requests++;
     if (oneshot && (rc = launch(r))) return rc;

@@ -454,7 +454,9 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #endif
     // the whole per-wave area starts zeroed (staging needs it; the transpose /
     // scratch area and the exchange vectors then never hold stale bits)
-    for (int k = lane; k < LDS_WAVE; k += 64) Ls[k] = 0.0;
+#pragma unroll
+    for (int i = 0; i < (LDS_WAVE + 63) / 64; i++)      // compile-time trip count: unrolled
+        if (lane + 64 * i < LDS_WAVE) Ls[lane + 64 * i] = 0.0;
     qpb_wsync();
 #pragma unroll
     for (int u = 0; u < NPL; u++) {

@@ -22,6 +22,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/qpSWIFT.h"
@@ -598,6 +599,21 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     get(tst, v.ost, 6);
     int iv[2];
     std::memcpy(iv, h + ofl, sizeof(iv));
+    static const bool recheck = getenv("QPB_SERVE_RECHECK") != nullptr;
+    if (recheck) {
+        // diagnostics: did any result land in the slab after the answer was seen?
+        std::this_thread::sleep_for(std::chrono::microseconds(500));
+        std::vector<double> t2(tmp.size());
+        double *ux = t2.data(), *uy = ux + n, *uz = uy + p, *us = uz + m;
+        get(ux, v.ox, n);
+        if (p > 0) get(uy, v.oy, p);
+        get(uz, v.oz, m);
+        get(us, v.os, m);
+        long nd = 0;
+        for (long i = 0; i < n + p + 2 * m; i++) nd += std::memcmp(&tmp[(size_t)i], &t2[(size_t)i], sizeof(double)) != 0;
+        if (nd) fprintf(stderr, "[recheck] %s: %ld of %ld results changed after the answer\n",
+                        setup_init ? "setup" : (cs.warm ? "warm" : "cold"), nd, n + p + 2 * m);
+    }
     take_results(v, q, tx, ty, tz, ts, tst, h[v.ofv], iv, h[osg], cs.st.maxit, setup_init);
     if (cs.warm) {
         take_timers(v, h + v.otr);

@@ -13,7 +13,7 @@ for spec in "$@"; do
     IFS=,; for kv in $vars; do export "${kv%%=*}=$(echo "${kv#*=}" | tr + ' ')"; done; unset IFS
     timeout -k 10 180 python -u scripts/serve_dbg.py > $out/$name.log 2> $out/$name.err; rc=$?
     fatal $rc $name
-    echo "$name [$vars] rc=$rc bad=$(grep -c '"iters": [^5]' $out/$name.log) n=$(grep -c '"q"' $out/$name.log)"
+    echo "$name [$vars] rc=$rc bad=$(grep -c '"ok": false' $out/$name.log) n=$(grep -c '"q"' $out/$name.log)"
     if [ "${LAT:-0}" = 1 ]; then
       for sh in c1 c30 c30_trot; do
         timeout -k 10 180 python -u scripts/dropin_latency.py --shape $sh --mode fast >> $out/$name.lat.jsonl 2>> $out/$name.err; rc=$?

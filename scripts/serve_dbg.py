@@ -10,10 +10,16 @@ n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
 tol, maxit = float(g["tol"]), int(g["maxit"])
 order = [int(v) for v in sys.argv[1].split(",")] if len(sys.argv) > 1 else list(range(g["x"].shape[0]))
 for q in order:
-    r = dropin.solve_dense(n, m, p, g["P"][q], g["A"][q], g["G"][q], g["c"][q], g["h"][q], g["b"][q],
-                           ordering=int(g["ordering"]), reltol=tol, abstol=tol, maxit=maxit)
-    print(json.dumps({"q": q, "flag": r["flag"], "iters": r["iters"], "g_iters": int(g["iters"][q]),
-                      "dx": float(np.abs(r["x"] - g["x"][q]).max()), "dz": float(np.abs(r["z"] - g["z"][q]).max())}))
+    # QP_SETUP (its initial point is the cold wave's answer), then QP_SOLVE (the warm wave)
+    qp, keep = dropin.setup_dense(n, m, p, g["P"][q], g["A"][q], g["G"][q], g["c"][q], g["h"][q], g["b"][q],
+                                  ordering=int(g["ordering"]))
+    s0 = dropin.state(qp, n, m)
+    r = dropin.solve_again(qp, n, m, reltol=tol, abstol=tol, maxit=maxit)
+    dropin._lib.lib().QP_CLEANUP_dense(qp)
+    dx = float(np.abs(r["x"] - g["x"][q]).max())
+    print(json.dumps({"q": q, "ok": bool(dx < 1e-6 and r["iters"] == int(g["iters"][q])), "flag": r["flag"], "iters": r["iters"], "g_iters": int(g["iters"][q]),
+                      "dx": dx, "dz": float(np.abs(r["z"] - g["z"][q]).max()),
+                      "init": [float(np.abs(s0[k]).sum()) for k in ("x", "y", "z", "s")] + [s0["sigma"]]}))
 import ctypes as C
 from apf_quadruped_amd import _lib
 st = (C.c_long * 4)()

@@ -4,6 +4,8 @@
 for ISA reading on the host:
 
     EXTRA="#define QPB_W_EXECDBG 1" python scripts/serve_variant_src.py out.hip
+
+COLD=1 emits the persistent cold (setup-init, QP_SETUP) variant instead.
 """
 import os, re, sys
 import numpy as np
@@ -20,4 +22,4 @@ rt = open(os.path.join(ROOT, "apf_quadruped_amd/csrc/qpb_runtime.hip")).read()
 pre = re.search(r'kServePrelude = R"QPBS\((.*?)\)QPBS"', rt, re.S).group(1)
 extra = os.environ.get("EXTRA", "")
 extra = extra + "\n" if extra else ""
-open(sys.argv[1], "w").write("#include <hip/hip_runtime.h>\n" + extra + "#define QPB_WARM 1\n#define QPB_SERVE 1\n" + pre + src)
+open(sys.argv[1], "w").write("#include <hip/hip_runtime.h>\n" + extra + ("" if os.environ.get("COLD") == "1" else "#define QPB_WARM 1\n") + "#define QPB_SERVE 1\n" + pre + src)
