@@ -290,6 +290,31 @@ std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out) 
         for (size_t k = 0; k < v.size(); k++) o << (k ? "," : "") << v[k];
         o << "};\n";
     };
+    // structure of the dense block's L: the plan's symbolic factor restricted to the
+    // dense rows (moving the leaves first leaves it unchanged -- every leaf's neighbours
+    // come after it in both orders).  qpb_lnz[j][k] = L(j, k) may be nonzero (j > k):
+    // the factor skips the updates whose broadcast H(j, k) is a structural zero.
+    {
+        std::vector<long> dpos(pl.N, -1);
+        for (long d = 0; d < nd; d++) dpos[pl.pinv[L.dense[d]]] = d;
+        std::vector<std::vector<int>> lnz(nd, std::vector<int>(nd, 0));
+        for (long c = 0; c < pl.N; c++) {
+            const long kd = dpos[c];
+            if (kd < 0) continue;
+            for (long q = pl.Lp[c]; q < pl.Lp[c + 1]; q++) {
+                const long jd = dpos[pl.Li[q]];
+                if (jd > kd) lnz[jd][kd] = 1;
+            }
+        }
+        o << "static constexpr bool qpb_lnz[" << std::max<long>(nd, 1) << "][" << std::max<long>(nd, 1) << "] = {";
+        for (long j = 0; j < nd; j++) {
+            o << (j ? "," : "") << "{";
+            for (long k = 0; k < nd; k++) o << (k ? "," : "") << lnz[j][k];
+            o << "}";
+        }
+        if (nd == 0) o << "{0}";
+        o << "};\n";
+    }
     carr("qpb_dkind", dkind);
     carr("qpb_didx", didx);
     carr("qpb_xpos", xpos);

@@ -109,6 +109,12 @@ struct qpb_args {
 #ifndef QPB_W_ABL          // cost attribution only (wrong results): skip 1 LDL' 2 G'WG 4 solve chains
 #define QPB_W_ABL 0       // 8 residual products 16 transpose (scripts/lat_bench.py, fixed iteration count)
 #endif
+#ifndef QPB_W_H0BF         // 1: the static dense-row part H0 formed branch-free (QPB_W_H0RE recomputes
+#define QPB_W_H0BF 1       // it at every factor: the divergent loads cost the AMD-ordered C30 kernel)
+#endif
+#ifndef QPB_W_LSKIP        // 1: the LDL' skips the updates whose H(j, k) is a structural zero (qpb_lnz)
+#define QPB_W_LSKIP 1
+#endif
 #ifndef QPB_W_LDSB_SYNC     // 1: a wave fence between publishing column k+1 and reading it (diagnostic)
 #define QPB_W_LDSB_SYNC 0
 #endif
@@ -508,10 +514,32 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     // (large dense blocks: recomputed from the staged matrices at every factor
     // instead of holding ND more doubles live across the iteration -- QPB_W_H0RE)
     auto h0_row = [&](double *H0) {
+#if QPB_W_H0BF
+    // branch-free: one LDS read at a selected address per entry, the leaf-y terms with
+    // the lane's own 1e7 A(l, i) (0 unless dense row i is x_i) -- no divergent loads
+    double aL[NY1];
+#pragma unroll
+    for (int l = 0; l < NY1; l++) aL[l] = (NY > 0 && qpb_yleaf[l < NY ? l : 0]) ? -RDY * dxm * Ad[dxi * LDY + l] : 0.0;
+#endif
     qpb_for<0, ND>([&](auto ec) {
         constexpr int e = decltype(ec)::value;
         constexpr int ke = qpb_dkind[e], je = qpb_didx[e];
         double v = 0.0;
+#if QPB_W_H0BF
+        if constexpr (ke == 0) {
+            const int pa = dxi <= je ? je * LDP + dxi : dxi * LDP + je;
+            const int ya = OFF_A + je * LDY + (NY > 0 ? di : 0), za = OFF_G + je * LDZ + di;
+            double vx = Ls[dk == 0 ? pa : (dk == 1 ? ya : za)];
+#pragma unroll
+            for (int l = 0; l < NY; l++)
+                if (qpb_yleaf[l]) vx = __builtin_fma(aL[l], Ad[je * LDY + l], vx);
+            v = vx;
+        } else {
+            double u = ke == 1 ? Ad[dxi * LDY + je] : Gd[dxi * LDZ + je];
+            asm volatile("" : "+v"(u));        // loaded by every lane, then selected
+            v = dk == 0 ? u : 0.0;
+        }
+#else
         if constexpr (ke == 0) {
             const double px = dxi <= je ? Pd[je * LDP + dxi] : Pd[dxi * LDP + je];
             double vx = px;
@@ -524,6 +552,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         } else {
             v = dk == 0 ? Gd[dxi * LDZ + je] : 0.0;
         }
+#endif
         H0[e] = isd ? v : 0.0;
     });
     };
@@ -716,9 +745,11 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             const double nlo = Hlo[k] * -rd, nhi = Hhi[k] * -rd;
             qpb_for<k + 1, ND>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                const double b = qpb_dpp<0x150 + (j & 15)>(j < 16 ? Hlo[k] : Hhi[k]);   // H(j, k)
-                Hlo[j] = __builtin_fma(b, nlo, Hlo[j]);
-                Hhi[j] = __builtin_fma(b, nhi, Hhi[j]);
+                if constexpr (!QPB_W_LSKIP || qpb_lnz[j][k]) {
+                    const double b = qpb_dpp<0x150 + (j & 15)>(j < 16 ? Hlo[k] : Hhi[k]);   // H(j, k)
+                    Hlo[j] = __builtin_fma(b, nlo, Hlo[j]);
+                    Hhi[j] = __builtin_fma(b, nhi, Hhi[j]);
+                }
             });
             Hlo[k] = lr > k ? nlo : 0.0;
             Hhi[k] = 16 + lr > k ? nhi : 0.0;
@@ -830,14 +861,14 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             constexpr int cb = (k & 1) * 64, nb = ((k + 1) & 1) * 64;
             qpb_for<k + 1, ND>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                H[j] = __builtin_fma(Bc[cb + j], nl, H[j]);
+                if constexpr (!QPB_W_LSKIP || qpb_lnz[j][k]) H[j] = __builtin_fma(Bc[cb + j], nl, H[j]);
                 if constexpr (j == k + 1) Bc[nb + ln] = H[j];      // column k+1 is final
             });
             if constexpr (QPB_W_LDSB_SYNC) qpb_wsync();
 #else
             qpb_for<k + 1, ND>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                H[j] = qpb_fmac_xb<j>(H[j], H[k], nl);
+                if constexpr (!QPB_W_LSKIP || qpb_lnz[j][k]) H[j] = qpb_fmac_xb<j>(H[j], H[k], nl);
             });
 #endif
             H[k] = ln > k ? nl : 0.0;       // -L(d,k) below the diagonal, 0 elsewhere
