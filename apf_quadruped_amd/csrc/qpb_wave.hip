@@ -112,6 +112,12 @@ struct qpb_args {
 #ifndef QPB_W_H0BF         // 1: the static dense-row part H0 formed branch-free (QPB_W_H0RE recomputes
 #define QPB_W_H0BF 1       // it at every factor: the divergent loads cost the AMD-ordered C30 kernel)
 #endif
+#ifndef QPB_W_TRUNM        // 1: the -L transpose stores every row unmasked, in descending column order
+#define QPB_W_TRUNM 1
+#endif
+#ifndef QPB_W_LTZS         // 1: the backward solve's -L column above the diagonal read from the zero
+#define QPB_W_LTZS 1       // slot T_SINK (an address select) instead of a value select
+#endif
 #ifndef QPB_W_LSKIP        // 1: the LDL' skips the updates whose H(j, k) is a structural zero (qpb_lnz)
 #define QPB_W_LSKIP 1
 #endif
@@ -888,9 +894,25 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             // stores: a shared sink slot would serialise the masked lanes' writes)
             const int lt = qpb_opaque(lane);
             const int base = isd ? lt * (lt - 1) / 2 : 0;
+#if QPB_W_TRUNM
+            // unmasked, in descending e: a lane's stores past the end of its row land in
+            // later rows' slots BEFORE those rows' own stores (a slot of row r is hit by
+            // a lane d < r only at e = slot - base_d, above r's own e), and one wave's LDS
+            // stores complete in program order -- the empty asm keeps the compiler from
+            // reordering them (per lane the addresses are distinct, so it otherwise may).
+            // One divergent region instead of one per store (lane 0 shares base 0 with 1).
+            if (isd && lt > 0) {
+#pragma unroll
+                for (int e = ND - 2; e >= 0; e--) {
+                    Tx[base + e] = H[e];
+                    asm volatile("" ::: "memory");
+                }
+            }
+#else
 #pragma unroll
             for (int e = 0; e < ND - 1; e++)
                 if (isd && e < lt) Tx[base + e] = H[e];
+#endif
         }
         qpb_wsync();
 #if !QPB_W_LTLDS
@@ -953,8 +975,12 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         const int ido = qpb_opaque(id);
 #pragma unroll
         for (int k = 0; k < ND; k++) {
+#if QPB_W_LTZS
+            Ltl[k] = Tx[k > ido ? k * (k - 1) / 2 + ido : T_SINK];   // T_SINK: never written, 0
+#else
             const double v = Tx[k * (k - 1) / 2 + ido];      // in the area for every k <= ND - 1, id <= ND - 1
             Ltl[k] = k > ido ? v : 0.0;
+#endif
         }
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = ND - 1 - decltype(kc)::value;
