@@ -494,10 +494,12 @@ def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
 
 def limiter_for(B):
     """What the SQ counters say bounds the row kernel at this batch
-    (profiles/r03_sq_row.json, scripts/gpu_sq.sh + scripts/sq_summary.py)."""
-    f = os.path.join(ROOT, "profiles", "r03_sq_row.json")
-    if not os.path.exists(f):
+    (profiles/r04_sq_row.json, else r03's; scripts/gpu_sq.sh + scripts/sq_summary.py)."""
+    name = next((n for n in ("r04_sq_row.json", "r03_sq_row.json")
+                 if os.path.exists(os.path.join(ROOT, "profiles", n))), None)
+    if name is None:
         return None
+    f = os.path.join(ROOT, "profiles", name)
     r = json.load(open(f)).get(f"B={B}")
     if not r:
         return None
@@ -505,7 +507,7 @@ def limiter_for(B):
     return {"kind": r.get("kind", "VALU issue + LDS/memory latency (neither HBM nor FP64 peak)"),
             "valu_active_frac": fr["valu_active"], "waitcnt_frac": fr["wait_any (s_waitcnt: LDS / memory)"],
             "waves_per_simd": r["waves_per_simd_avg"], "fp64_lane_fma_per_qp": r["per_qp"]["fma_f64_lane_ops"],
-            "source": "profiles/r03_sq_row.json"}
+            "source": "profiles/" + name}
 
 
 def controller_apf_leg(dev, K=8192, steps=20, warmup=3):

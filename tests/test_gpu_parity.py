@@ -376,6 +376,35 @@ def test_wave_two_rows_per_lane_factor_bit_identical(monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", ["amd", "own"])
+def test_wave_structure_knobs_match_plain_build(monkeypatch, order):
+    """Round 4's wave-kernel changes -- the LDL' skipping structurally zero H(j,k)
+    (QPB_W_LSKIP), the branch-free H0 (QPB_W_H0BF), the unmasked descending -L transpose
+    (QPB_W_TRUNM) and the backward solve's zero slot (QPB_W_LTZS) -- against the build
+    with all four off, on controller QPs in the drop-in's AMD order (51 dense rows) and
+    leaves first (30): the same flags and iteration counts, iterates within 1e-9
+    (the skipped terms are exact zeros; H0BF rounds the 1e7 A'A terms differently)."""
+    import torch
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan
+    B = 256
+    d = W.controller_qp(0xD06B07 + 34, np.arange(B))
+    plain = "QPB_W_LSKIP=0 QPB_W_H0BF=0 QPB_W_TRUNM=0 QPB_W_LTZS=0"
+    res = {}
+    for opt in ("", plain):
+        monkeypatch.setenv("QPB_WAVE_OPTS", opt)
+        plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], kernel="wave", order=order)
+        vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
+        res[opt] = plan.unpack(plan.solve(**vals, B=B), B)
+    np.testing.assert_array_equal(res[""]["flag"], res[plain]["flag"])
+    np.testing.assert_array_equal(res[""]["iters"], res[plain]["iters"])
+    for k in ("x", "y", "z", "s"):
+        a, b = res[""][k], res[plain][k]
+        assert np.abs(a - b).max() <= 1e-9 * max(1.0, np.abs(b).max()), (order, k)
+    assert (res[""]["flag"] == 0).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["edge_infeasible", "edge_infeasible_maxit8"])
 @pytest.mark.parametrize("own_order,kernel", [(False, "lane"), (True, "lane"), (False, "wave"), (True, "wave"),
                                               (True, "wave1"), (False, "tree"), (True, "tree")])
