@@ -333,12 +333,19 @@ static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, doub
 // area, whichever is larger) instead of both: 7.1 -> 3.6 KB for the 12/20/6 QP.
 #define EVEN(v) (((v) + 1) & ~1)
 #define OFF_A (NX * NX)
+// row stride of the per-lane rows parked in LDS (-P, H0, the -L transpose): lane c reads
+// its row at c * RS, 16-byte pieces; RS = 2 mod 4 doubles puts the 16 lanes of a row on
+// distinct bank quadruples (RS = NX = 12 pairs them up: 2-way conflicts on every read)
+#ifndef QPB_R_RS
+#define QPB_R_RS 1
+#endif
+#define RS (QPB_R_RS ? NX + ((2 - NX % 4) + 4) % 4 : NX)
 #define OFF_G (OFF_A + NY1 * NX)
 #define STG_END EVEN(OFF_G + NZ * NX)
 #define OFF_T (QPB_R_ALIAS ? 0 : STG_END)
-#define OFF_PR EVEN(OFF_T + NX * NX)
-#define OFF_H0 EVEN(OFF_PR + NX * NX)
-#define LOOP_END EVEN(OFF_H0 + NX * NX)
+#define OFF_PR EVEN(OFF_T + NX * RS)
+#define OFF_H0 EVEN(OFF_PR + NX * RS)
+#define LOOP_END EVEN(OFF_H0 + NX * RS)
 #define LDS_ROW (LOOP_END > STG_END ? LOOP_END : STG_END)
 // QPB_R_SPLIT: per row, the iterate wave 0 forms (x y z0 z1 s0 s1: 6 x 16) and the residuals
 // wave 1 forms (rx ry rz0 rz1 -P x: 5 x 16, the four row sums)
@@ -493,7 +500,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #endif
         if (!QPB_R_REGH0 && isx) {
 #pragma unroll
-            for (int j = 0; j < NX; j++) { PR[c * NX + j] = nP[j]; H0s[c * NX + j] = H0[j]; }
+            for (int j = 0; j < NX; j++) { PR[c * RS + j] = nP[j]; H0s[c * RS + j] = H0[j]; }
         }
         qpb_wsync();
     }
@@ -509,7 +516,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     // H = H0 + G' diag(w) G
     auto gwg = [&](double w0, double w1) {
 #pragma unroll
-        for (int e = 0; e < NX; e++) H[e] = QPB_R_REGH0 ? H0[e] : H0s[ix * NX + e];
+        for (int e = 0; e < NX; e++) H[e] = QPB_R_REGH0 ? H0[e] : H0s[ix * RS + e];
 #if QPB_R_GWG4
         // four rows at a time: the four products -G(r,c) w_r are formed (in their own
         // registers) before any of their DPP FMAs, so no FMA waits out the DPP operand
@@ -601,7 +608,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         // column c of -L, contiguous for lane c: Tx[c*NX + k] = -L(k, c)
         if (isx) {
 #pragma unroll
-            for (int e = 0; e < NX; e++) Tx[e * NX + c] = H[e];
+            for (int e = 0; e < NX; e++) Tx[e * RS + c] = H[e];
         }
         qpb_wsync();
     };
@@ -625,7 +632,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         t *= rDd;
         double Lt[NX];
 #pragma unroll
-        for (int k = 0; k < NX; k++) Lt[k] = Tx[ix * NX + k];
+        for (int k = 0; k < NX; k++) Lt[k] = Tx[ix * RS + k];
         qpb_for<0, NX>([&](auto kc) {
             constexpr int k = NX - 1 - decltype(kc)::value;
             qpb_fxd<k>(t, Lt[k]);
@@ -714,7 +721,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             double nPr[NX];
             tp = 0.0; ry = by; rz0 = hz0 - s0; rz1 = hz1 - s1;
 #pragma unroll
-            for (int j = 0; j < NX; j++) nPr[j] = QPB_R_REGH0 ? nP[j] : PR[ix * NX + j];
+            for (int j = 0; j < NX; j++) nPr[j] = QPB_R_REGH0 ? nP[j] : PR[ix * RS + j];
             qpb_for<0, NX>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 qpb_fx<j>(rz0, x, nGl[j]);

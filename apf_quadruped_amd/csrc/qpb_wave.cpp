@@ -63,8 +63,8 @@ static bool wave_pad() {
 }
 
 // per-wave LDS doubles (qpb_wave.hip LDS_WAVE): dense P, A, G, the L transpose
-// and the vector exchange area
-static long wave_lds_doubles(const Plan &pl, long nd) {
+// and the vector exchange area; ldg = the staged G's leading dimension
+static long wave_lds_doubles(const Plan &pl, long nd, long ldg) {
     // T: packed strictly-lower -L, or the MFMA tiles / broadcast buffers (TSZ in qpb_wave.hip)
     const long nt = (pl.n + 15) / 16;
     const bool mfma = pl.G.nnz() > 48 && pl.n <= 64;
@@ -77,20 +77,43 @@ static long wave_lds_doubles(const Plan &pl, long nd) {
     t = ((t + 1) & ~1L) + 2;
     // staged P, A, G with odd leading dimensions (LDP, LDY, LDZ)
     const long pad = wave_pad() ? 1 : 0;
-    const long stage = pl.n * (pl.n | pad) + (pl.p ? pl.n * (pl.p | pad) : 0) + pl.n * (pl.m | pad);
+    const long stage = pl.n * (pl.n | pad) + (pl.p ? pl.n * (pl.p | pad) : 0) + pl.n * ldg;
     return stage + t + 2 * pl.N + pl.m + pl.n + 8;
 }
 
-int wave_wg_for(const Plan &pl) {
-    const long nd = (long)wave_layout(pl).dense.size();
-    const long bytes = wave_lds_doubles(pl, nd) * 8;
+// workgroup size and QPs per CU for a footprint of `doubles` per QP
+static int wg_for_doubles(long doubles, int *qps_per_cu) {
+    const long bytes = doubles * 8;
     // as many QPs per CU as the 160 KiB allow (whole workgroups), ties -> larger workgroups
     int best = 0, best_qps = 0;
     for (int waves = 4; waves >= 1; waves--) {
         const long per_cu = (160L * 1024) / (bytes * waves);
         if (per_cu * waves > best_qps) { best_qps = (int)(per_cu * waves); best = waves; }
     }
+    if (qps_per_cu) *qps_per_cu = best_qps;
     return 64 * best;
+}
+
+// The staged G's leading dimension.  Its columns are read lane-strided (G(r, i) by the
+// lane of x_i: the residual's G'z, the solve's leaf elimination, the MFMA operands); a
+// stride of m doubles with m = 0 mod 4 puts those reads on 8 of the 64 LDS banks.  Padded
+// to 2 mod 4 (16-byte column alignment kept) the lanes spread over 16 bank pairs -- when
+// that costs no QP per CU (QPB_W_PADZ=0 turns it off; QPB_W_PAD=1, odd, overrides).
+static long wave_ldz(const Plan &pl, long nd) {
+    if (wave_pad()) return pl.m | 1;
+    const char *e = getenv("QPB_WAVE_OPTS");
+    if (e && strstr(e, "QPB_W_PADZ=0")) return pl.m;
+    const long padded = pl.m + ((2 - pl.m % 4) + 4) % 4;
+    if (padded == pl.m) return pl.m;
+    int q0 = 0, q1 = 0;
+    wg_for_doubles(wave_lds_doubles(pl, nd, pl.m), &q0);
+    wg_for_doubles(wave_lds_doubles(pl, nd, padded), &q1);
+    return q1 >= q0 ? padded : pl.m;
+}
+
+int wave_wg_for(const Plan &pl) {
+    const long nd = (long)wave_layout(pl).dense.size();
+    return wg_for_doubles(wave_lds_doubles(pl, nd, wave_ldz(pl, nd)), nullptr);
 }
 
 bool wave_eligible(const Plan &pl, std::string *why) {
@@ -262,11 +285,13 @@ std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out) 
     std::ostringstream o;
     std::vector<long> gcol;
     const long pad = wave_pad() ? 1 : 0;
-    common_header(o, pl, wg, "wave-cooperative", &gcol, pl.n | pad, (pl.p ? pl.p : 1) | pad, pl.m | pad);
-    const long nG = pl.G.nnz();
     // elimination layout: leaves first, the rest as a dense block in perm order
     const WaveLayout L = wave_layout(pl);
     const long nd = (long)L.dense.size();
+    const long ldz = wave_ldz(pl, nd);
+    common_header(o, pl, wg, "wave-cooperative", &gcol, pl.n | pad, (pl.p ? pl.p : 1) | pad, ldz);
+    o << "#define QPB_LDZ " << ldz << "\n";
+    const long nG = pl.G.nnz();
     std::vector<int> dkind(nd), didx(nd), xpos(n, -1);
     for (long d = 0; d < nd; d++) {
         const long k = L.dense[d];

@@ -155,7 +155,11 @@ struct qpb_args {
 #endif
 #define LDP (QPB_W_PAD ? (NX | 1) : NX)
 #define LDY (QPB_W_PAD ? (NY1 | 1) : NY1)
+#ifdef QPB_LDZ                // chosen by the host (qpb_wave.cpp wave_ldz): NZ, or NZ padded to 2 mod 4
+#define LDZ QPB_LDZ
+#else
 #define LDZ (QPB_W_PAD ? (NZ | 1) : NZ)
+#endif
 #define OFF_A (NX * LDP)
 #define OFF_G (OFF_A + (NY > 0 ? LDY : 0) * NX)
 #define OFF_C (OFF_G + LDZ * NX)
