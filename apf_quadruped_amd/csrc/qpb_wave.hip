@@ -29,12 +29,18 @@
 // line cached for an earlier one (round 3: a warm solve started from the previous
 // QP's iterate).  Batched builds keep plain loads and stores.
 #if defined(QPB_SERVE) && QPB_SERVE
+#ifndef QPB_TSTR          // (QPB_WAVE_OPTS="QPB_TSTR=64": the tiled slab, for A/B -- the host follows)
+#define QPB_TSTR 1        // the persistent (drop-in, B = 1) variants: QP 0's values packed in the slab
+#endif
 #define QPB_LDS(p) __hip_atomic_load((p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
 #define QPB_STS(p, v) __hip_atomic_store((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
 #else
 #define QPB_LDS(p) (*(p))
 #define QPB_STS(p, v) (*(p) = (v))
 #endif
+#endif
+#ifndef QPB_TSTR
+#define QPB_TSTR 64       // tiled SoA: value j of QP q at [(q / 64) * n * 64 + j * 64 + q % 64]
 #endif
 
 template <int V> struct qpb_ic { static constexpr int value = V; };
@@ -431,13 +437,13 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     double vP[NPL], vG[NGL], vA[NAL > 0 ? NAL : 1];
     int iP[NPL], iP2[NPL], iG[NGL], iA[NAL > 0 ? NAL : 1];
     {
-        const double *tP = a.P + tile * (QPB_NNZP * 64) + ql;
-        const double *tG = a.G + tile * (QPB_NNZG * 64) + ql;
+        const double *tP = a.P + tile * (QPB_NNZP * QPB_TSTR) + ql;
+        const double *tG = a.G + tile * (QPB_NNZG * QPB_TSTR) + ql;
 #pragma unroll
         for (int u = 0; u < NPL; u++) {
             const int k = lane + 64 * u;
             const bool ok = k < QPB_NNZP;
-            vP[u] = ok ? QPB_LDS(&tP[k * 64]) : 0.0;
+            vP[u] = ok ? QPB_LDS(&tP[k * QPB_TSTR]) : 0.0;
             iP[u] = ok ? qpb_scP[k] : -1;
             iP2[u] = ok ? qpb_scP2[k] : -1;
         }
@@ -445,26 +451,26 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         for (int u = 0; u < NGL; u++) {
             const int k = lane + 64 * u;
             const bool ok = k < QPB_NNZG;
-            vG[u] = ok ? QPB_LDS(&tG[k * 64]) : 0.0;
+            vG[u] = ok ? QPB_LDS(&tG[k * QPB_TSTR]) : 0.0;
             iG[u] = ok ? qpb_scG[k] : -1;
         }
 #if NY > 0
-        const double *tA = a.A + tile * (QPB_NNZA * 64) + ql;
+        const double *tA = a.A + tile * (QPB_NNZA * QPB_TSTR) + ql;
 #pragma unroll
         for (int u = 0; u < NAL; u++) {
             const int k = lane + 64 * u;
             const bool ok = k < QPB_NNZA;
-            vA[u] = ok ? QPB_LDS(&tA[k * 64]) : 0.0;
+            vA[u] = ok ? QPB_LDS(&tA[k * QPB_TSTR]) : 0.0;
             iA[u] = ok ? qpb_scA[k] : -1;
         }
 #endif
     }
-    const double cx = isx ? QPB_LDS(&a.c[tile * (NX * 64) + lane * 64 + ql]) : 0.0;
+    const double cx = isx ? QPB_LDS(&a.c[tile * (NX * QPB_TSTR) + lane * QPB_TSTR + ql]) : 0.0;
     double hz[ZC];
 #pragma unroll
-    for (int t = 0; t < ZC; t++) hz[t] = isz[t] ? QPB_LDS(&a.h[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql]) : 0.0;
+    for (int t = 0; t < ZC; t++) hz[t] = isz[t] ? QPB_LDS(&a.h[tile * (NZ * QPB_TSTR) + (lane + 64 * t) * QPB_TSTR + ql]) : 0.0;
 #if NY > 0
-    const double by = isy ? QPB_LDS(&a.b[tile * (NY * 64) + lane * 64 + ql]) : 0.0;
+    const double by = isy ? QPB_LDS(&a.b[tile * (NY * QPB_TSTR) + lane * QPB_TSTR + ql]) : 0.0;
 #else
     const double by = 0.0;
 #endif
@@ -1342,15 +1348,15 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
     QPB_TS(370);
     const double fval = qpb_rsum<ROWS_X>(fv);
     // ---- outputs (tiled SoA)
-    if (isx) QPB_STS(&a.x[tile * (NX * 64) + lane * 64 + ql], x);
+    if (isx) QPB_STS(&a.x[tile * (NX * QPB_TSTR) + lane * QPB_TSTR + ql], x);
 #if NY > 0
-    if (isy) QPB_STS(&a.y[tile * (NY * 64) + lane * 64 + ql], y);
+    if (isy) QPB_STS(&a.y[tile * (NY * QPB_TSTR) + lane * QPB_TSTR + ql], y);
 #endif
 #pragma unroll
     for (int t = 0; t < ZC; t++)
         if (isz[t]) {
-            QPB_STS(&a.z[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql], z[t]);
-            QPB_STS(&a.s[tile * (NZ * 64) + (lane + 64 * t) * 64 + ql], s[t]);
+            QPB_STS(&a.z[tile * (NZ * QPB_TSTR) + (lane + 64 * t) * QPB_TSTR + ql], z[t]);
+            QPB_STS(&a.s[tile * (NZ * QPB_TSTR) + (lane + 64 * t) * QPB_TSTR + ql], s[t]);
         }
     if (lane == 0) {
         QPB_STS(&a.flag[q], flag);
@@ -1363,8 +1369,8 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         if (a.sig) QPB_STS(&a.sig[q], sigma);   // options->sigma after a cold QP_SOLVE (drop-in)
 #endif
         if (a.stats && !QPB_W_TIMING) {
-            double *o = a.stats + tile * 384 + ql;
-            o[0] = __builtin_sqrt(st_rx2); o[64] = __builtin_sqrt(st_ry2); o[128] = __builtin_sqrt(st_rz2); o[192] = st_mu; o[256] = ap; o[320] = ad;
+            double *o = a.stats + tile * 6 * QPB_TSTR + ql;
+            o[0] = __builtin_sqrt(st_rx2); o[QPB_TSTR] = __builtin_sqrt(st_ry2); o[2 * QPB_TSTR] = __builtin_sqrt(st_rz2); o[3 * QPB_TSTR] = st_mu; o[4 * QPB_TSTR] = ap; o[5 * QPB_TSTR] = ad;
         }
     }
     QPB_TS(371);

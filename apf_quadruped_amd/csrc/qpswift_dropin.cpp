@@ -100,6 +100,7 @@ struct Priv {
     bool inited = false;
     const double *trace = nullptr;   // the last warm solve's trace (host copy, for verbose)
     qpb::Server *srv = nullptr;      // the workspace's persistent solvers (cold, warm)
+    long tstride = 64;               // slab stride of QP 0's values: 64 tiled, 1 packed (persistent solver)
 };
 
 // Public struct first so that a QP* is also a Handle*.
@@ -318,10 +319,42 @@ QP *finish_setup(Handle *hd, long *Permut, clk::time_point t0) {
     return &q;
 }
 
+// A few released QP objects' host storage per thread, reused by the next QP_SETUP:
+// the controller builds and frees a QP every tick, and a fresh object's ~40 vectors
+// reallocated and regrew every time (the mirror of the reference's QP struct).
+// A reused Priv is a freshly constructed one that took over the old vectors'
+// capacity -- every other field starts from its default.
+constexpr size_t kPrivPool = 4;
+thread_local std::vector<Priv *> t_priv_pool;
+
+void priv_put(Priv *v) {
+    if (t_priv_pool.size() >= kPrivPool) { delete v; return; }
+    Priv fresh;
+#define QPB_TAKE(f) fresh.f.swap(v->f); fresh.f.clear();
+    QPB_TAKE(Pjc) QPB_TAKE(Pir) QPB_TAKE(Ajc) QPB_TAKE(Air) QPB_TAKE(Gjc) QPB_TAKE(Gir)
+    QPB_TAKE(Ppr) QPB_TAKE(Apr) QPB_TAKE(Gpr) QPB_TAKE(Atjc) QPB_TAKE(Atir) QPB_TAKE(Gtjc) QPB_TAKE(Gtir)
+    QPB_TAKE(Atpr) QPB_TAKE(Gtpr) QPB_TAKE(Kjc) QPB_TAKE(Kir) QPB_TAKE(Kpr)
+    QPB_TAKE(perm) QPB_TAKE(pinv) QPB_TAKE(parent) QPB_TAKE(lnzc) QPB_TAKE(Lp) QPB_TAKE(Li) QPB_TAKE(Lti)
+    QPB_TAKE(Ltp) QPB_TAKE(kflag) QPB_TAKE(pattern) QPB_TAKE(upattern) QPB_TAKE(kb) QPB_TAKE(Y) QPB_TAKE(Lx)
+    QPB_TAKE(D) QPB_TAKE(x) QPB_TAKE(y) QPB_TAKE(z) QPB_TAKE(s) QPB_TAKE(rx) QPB_TAKE(ry) QPB_TAKE(rz)
+    QPB_TAKE(delta) QPB_TAKE(dx) QPB_TAKE(dy) QPB_TAKE(dz) QPB_TAKE(dsv) QPB_TAKE(ds) QPB_TAKE(lambda)
+    QPB_TAKE(temp)
+#undef QPB_TAKE
+    *v = std::move(fresh);
+    t_priv_pool.push_back(v);
+}
+
+Priv *priv_get() {
+    if (t_priv_pool.empty()) return new (std::nothrow) Priv();
+    Priv *v = t_priv_pool.back();
+    t_priv_pool.pop_back();
+    return v;
+}
+
 Handle *new_handle(long n, long m) {
     Handle *hd = static_cast<Handle *>(std::calloc(1, sizeof(Handle)));
     if (!hd) return nullptr;
-    hd->priv = new (std::nothrow) Priv();
+    hd->priv = priv_get();
     if (!hd->priv) {
         std::free(hd);
         return nullptr;
@@ -378,13 +411,27 @@ thread_local std::map<int, Workspace> t_ws;
 
 bool zero_copy(const Priv &v) { return zero_copy_enabled() && !v.plan->gen.exact; }
 
+// the plan's one-QP kernel is the row or the wave form, i.e. qpb::serve_ex answers
+// (qpb_runtime.hip serve_ex: the same condition; otherwise it returns SERVE_NONE)
+bool serves_one_qp(const qpb_plan *plan) {
+    return plan && plan->wave_ok &&
+           (plan->kernel_pref == 2 || (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || 1 <= plan->wave_max_batch)));
+}
+
 int ensure_device(Priv &v, const QP &q) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return qpb::set_error(QPB_EHIP, "QP_SOLVE: no HIP device available (the drop-in has no CPU path)");
     if (v.dev < 0 && hipGetDevice(&v.dev) != hipSuccess) return qpb::set_error(QPB_EHIP, "hipGetDevice failed");
     if (v.ototal == 0) {   // layout of this QP in the slab (tile of 64, QP in lane 0)
-        const long T = 64;
+        // the persistent solver's variants read QP 0 packed (QPB_TSTR = 1): a zero-copy
+        // slab it serves holds every vector contiguous -- 8 values per 64-byte line over
+        // the host link instead of one; launched kernels read the tiled layout
+        const char *wo = std::getenv("QPB_WAVE_OPTS");
+        const bool packed = zero_copy(v) && serve_enabled() && serves_one_qp(v.plan.get()) &&
+                            !(wo && std::strstr(wo, "QPB_TSTR=64"));
+        const long T = packed ? 1 : 64;
+        v.tstride = T;
         v.nP = q.P->nnz;
         v.nA = q.p > 0 ? q.A->nnz : 0;
         v.nG = q.G->nnz;
@@ -541,8 +588,9 @@ void take_results(Priv &v, QP &q, const double *x, const double *y, const double
 int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     const long n = q.n, m = q.m, p = q.p;
     double *h = v.zmem, *d = v.zdev;
-    auto put = [h](long off, const double *src, long k) {
-        for (long i = 0; i < k; i++) h[off + 64 * i] = src[i];
+    const long T = v.tstride;
+    auto put = [h, T](long off, const double *src, long k) {
+        for (long i = 0; i < k; i++) h[off + T * i] = src[i];
     };
     put(v.oP, q.P->pr, v.nP);
     if (p > 0) put(v.oA, q.A->pr, v.nA);
@@ -589,8 +637,8 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
     if (rc) return rc;
     std::vector<double> tmp((size_t)(n + p + 2 * m + 6));
     double *tx = tmp.data(), *ty = tx + n, *tz = ty + p, *ts = tz + m, *tst = ts + m;
-    auto get = [h](double *dst, long off, long k) {
-        for (long i = 0; i < k; i++) dst[i] = h[off + 64 * i];
+    auto get = [h, T](double *dst, long off, long k) {
+        for (long i = 0; i < k; i++) dst[i] = h[off + T * i];
     };
     get(tx, v.ox, n);
     if (p > 0) get(ty, v.oy, p);
@@ -773,7 +821,7 @@ QP *setup_init(QP *q, clk::time_point t0) {
 void release(QP *q) {
     if (!q) return;
     Handle *hd = handle_of(q);
-    delete hd->priv;      // device buffers belong to the thread workspace, not the QP
+    priv_put(hd->priv);   // device buffers belong to the thread workspace, not the QP
     std::free(hd);
 }
 
