@@ -1081,7 +1081,7 @@ qpb::Server::~Server() {
 int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A, const double *G, const double *c,
                   const double *h, const double *b, const qpb_settings *st, double *x, double *y, double *z,
                   double *s, int *flag, int *iters, double *fval, double *stats, double *sig, bool warm,
-                  double *trace, const double *win) {
+                  double *trace, const double *win, const std::function<void()> &while_waiting) {
     if (!plan || !srv) return fail(QPB_EINVAL, "NULL plan or server");
     if (warm && (!sig || !win)) return fail(QPB_EINVAL, "a warm solve needs sigma and the state block");
     const qpb::Plan &pl = plan->pl;
@@ -1191,6 +1191,9 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
     mb_store(req, r);
     srv->requests++;
     if (oneshot && (rc = launch(r))) return rc;
+    // host work that does not need the answer (the drop-in's struct mirror) runs while
+    // the wave solves
+    if (while_waiting) while_waiting();
     auto answered = [&]() {
         srv->dev_ticks = srv->mb[32];
         if (getenv("QPB_SERVE_DEBUG"))

@@ -122,7 +122,7 @@ constexpr int SERVE_NONE = 1;            // serve_ex: this plan's one-QP kernel 
 int serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A, const double *G, const double *c,
              const double *h, const double *b, const qpb_settings *st, double *x, double *y, double *z, double *s,
              int *flag, int *iters, double *fval, double *stats, double *sig, bool warm, double *trace,
-             const double *win);
+             const double *win, const std::function<void()> &while_waiting = {});
 // Stop the kernel (if running) and wait for it to leave; the mailbox stays.
 int serve_stop(Server *srv);
 // Post the stop word to every running server of the calling thread without

@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -101,6 +102,8 @@ struct Priv {
     const double *trace = nullptr;   // the last warm solve's trace (host copy, for verbose)
     qpb::Server *srv = nullptr;      // the workspace's persistent solvers (cold, warm)
     long tstride = 64;               // slab stride of QP 0's values: 64 tiled, 1 packed (persistent solver)
+    bool mirror_pending = false;     // finish_mirror not run yet (QP_SETUP runs it while the device works)
+    long *permut = nullptr;          // the caller's Permut (kkt.P points to it when given)
 };
 
 // Public struct first so that a QP* is also a Handle*.
@@ -219,10 +222,10 @@ PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const
 
 // Everything of setup except the input conversion: transposes, plan, KKT
 // mirror, work vectors, public pointers.
-QP *finish_setup(Handle *hd, long *Permut, clk::time_point t0) {
+QP *finish_setup(Handle *hd, long *Permut) {
     QP &q = hd->qp;
     Priv &v = *hd->priv;
-    const long n = q.n, m = q.m, p = q.p, N = n + m + p;
+    const long n = q.n, m = q.m, p = q.p;
 
     q.options = &v.opt;
     q.stats = &v.st;
@@ -233,15 +236,6 @@ QP *finish_setup(Handle *hd, long *Permut, clk::time_point t0) {
     v.opt.verbose = VERBOSE;
     v.st.Flag = QP_FATAL;
 
-    csc_transpose(m, n, q.G->jc, q.G->ir, q.G->pr, v.Gtjc, v.Gtir, v.Gtpr);
-    set_smat(v.Gts, n, m, v.Gtjc.data(), v.Gtir.data(), v.Gtpr.data());
-    q.Gt = &v.Gts;
-    if (p > 0) {
-        csc_transpose(p, n, q.A->jc, q.A->ir, q.A->pr, v.Atjc, v.Atir, v.Atpr);
-        set_smat(v.Ats, n, p, v.Atjc.data(), v.Atir.data(), v.Atpr.data());
-        q.At = &v.Ats;
-    }
-
     auto vec = [](std::vector<double> &b, long k) {
         b.assign((size_t)std::max(k, 1L), 0.0);
         return b.data();
@@ -250,6 +244,42 @@ QP *finish_setup(Handle *hd, long *Permut, clk::time_point t0) {
     q.y = p > 0 ? vec(v.y, p) : nullptr;
     q.z = vec(v.z, m);
     q.s = vec(v.s, m);
+
+    // default: fast arithmetic (the wave kernel where eligible: ~50 us per C1
+    // tick instead of ~250 us); QPSWIFT_HIP_EXACT=1 selects the bit-faithful
+    // lane kernel (bit-identical to qpSWIFT given the same permutation)
+    const char *ex = getenv("QPSWIFT_HIP_EXACT");
+    const bool exact = ex && *ex && *ex != '0';
+    v.plan = get_plan(n, m, p, q.P->jc, q.P->ir, p > 0 ? q.A->jc : nullptr, p > 0 ? q.A->ir : nullptr, q.G->jc,
+                      q.G->ir, Permut, exact, v.err);
+    // the rest mirrors the reference's structs for callers that read them; the
+    // device's initial point does not need it, so setup_init runs it while the
+    // device computes (finish_mirror)
+    v.permut = Permut;
+    v.mirror_pending = true;
+    return &q;
+}
+
+// The reference's QP struct contents that no device solve reads: G' and A', the work
+// vectors, the KKT (values as assembled), its ordering and symbolic factor, and the
+// LDL' workspace (qpSWIFT.c:60-456 fill them in QP_SETUP).
+void finish_mirror(Priv &v, QP &q) {
+    if (!v.mirror_pending) return;
+    v.mirror_pending = false;
+    const long n = q.n, m = q.m, p = q.p, N = n + m + p;
+    long *Permut = v.permut;
+    csc_transpose(m, n, q.G->jc, q.G->ir, q.G->pr, v.Gtjc, v.Gtir, v.Gtpr);
+    set_smat(v.Gts, n, m, v.Gtjc.data(), v.Gtir.data(), v.Gtpr.data());
+    q.Gt = &v.Gts;
+    if (p > 0) {
+        csc_transpose(p, n, q.A->jc, q.A->ir, q.A->pr, v.Atjc, v.Atir, v.Atpr);
+        set_smat(v.Ats, n, p, v.Atjc.data(), v.Atir.data(), v.Atpr.data());
+        q.At = &v.Ats;
+    }
+    auto vec = [](std::vector<double> &b, long k) {
+        b.assign((size_t)std::max(k, 1L), 0.0);
+        return b.data();
+    };
     q.rx = vec(v.rx, n);
     q.ry = p > 0 ? vec(v.ry, p) : nullptr;
     q.rz = vec(v.rz, m);
@@ -261,14 +291,6 @@ QP *finish_setup(Handle *hd, long *Permut, clk::time_point t0) {
     q.ds = vec(v.ds, m);
     q.lambda = vec(v.lambda, m);
     q.temp = vec(v.temp, n);
-
-    // default: fast arithmetic (the wave kernel where eligible: ~50 us per C1
-    // tick instead of ~250 us); QPSWIFT_HIP_EXACT=1 selects the bit-faithful
-    // lane kernel (bit-identical to qpSWIFT given the same permutation)
-    const char *ex = getenv("QPSWIFT_HIP_EXACT");
-    const bool exact = ex && *ex && *ex != '0';
-    v.plan = get_plan(n, m, p, q.P->jc, q.P->ir, p > 0 ? q.A->jc : nullptr, p > 0 ? q.A->ir : nullptr, q.G->jc,
-                      q.G->ir, Permut, exact, v.err);
 
     q.kkt = &v.K;
     v.st.AMD_RESULT = Permut ? -3 : 0;
@@ -315,8 +337,6 @@ QP *finish_setup(Handle *hd, long *Permut, clk::time_point t0) {
     v.K.Flag = v.kflag.data();
     v.K.Pattern = v.pattern.data();
     v.K.UPattern = v.upattern.data();
-    v.st.tsetup = seconds_since(t0);
-    return &q;
 }
 
 // A few released QP objects' host storage per thread, reused by the next QP_SETUP:
@@ -585,7 +605,7 @@ void take_results(Priv &v, QP &q, const double *x, const double *y, const double
 // tiled slot of QP 0 (stride 64) of the mapped pinned slab, one launch reads
 // them over the host link and writes x, y, z, s, stats, flag, iterations, fval
 // and sigma back into it.
-int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
+int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init, const std::function<void()> &overlap) {
     const long n = q.n, m = q.m, p = q.p;
     double *h = v.zmem, *d = v.zdev;
     const long T = v.tstride;
@@ -625,8 +645,9 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init) {
         rc = qpb::serve_ex(v.plan.get(), &v.srv[cs.warm ? 1 : 0], d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG,
                            d + v.oc, d + v.oh, p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr,
                            d + v.oz, d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, d + osg, cs.warm, d + v.otr,
-                           d + v.owin);
+                           d + v.owin, overlap);
     if (rc == qpb::SERVE_NONE) {
+        if (overlap) overlap();       // (no persistent solver: nothing to overlap with)
         rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
                            p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz,
                            d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, nullptr, v.stream, d + osg, cs.warm,
@@ -688,7 +709,8 @@ void mirror_kkt(Priv &v, QP &q) {
 // so ONE host-to-device copy carries the inputs and (warm) the QP's state, a
 // scatter kernel spreads them to the tiled slots, the solve runs, a gather kernel
 // packs the results and ONE device-to-host copy brings them back.
-int solve_staged(Priv &v, QP &q, const CallState &cs, bool setup_init) {
+int solve_staged(Priv &v, QP &q, const CallState &cs, bool setup_init, const std::function<void()> &overlap) {
+    if (overlap) overlap();
     const long n = q.n, m = q.m, p = q.p;
     double *hin = v.hmem, *hout = v.hmem + v.nin;
     double *w = hin;
@@ -783,7 +805,7 @@ int solve_staged(Priv &v, QP &q, const CallState &cs, bool setup_init) {
 
 // One launch for this QP: QP_SETUP's kkt_initialize (setup_init: maxit = 0,
 // cold) or a QP_SOLVE (warm once the initial point is in the object).
-int solve_on_device(Priv &v, QP &q, bool setup_init) {
+int solve_on_device(Priv &v, QP &q, bool setup_init, const std::function<void()> &overlap = {}) {
     int rc = ensure_device(v, q);
     if (rc) return rc;
     int cur = -1;
@@ -791,7 +813,7 @@ int solve_on_device(Priv &v, QP &q, bool setup_init) {
     if (cur != v.dev) (void)hipSetDevice(v.dev);
     CallState cs = call_state(v, q, setup_init ? 0 : q.options->maxit);
     if (setup_init) cs.warm = false;
-    rc = zero_copy(v) ? solve_zero_copy(v, q, cs, setup_init) : solve_staged(v, q, cs, setup_init);
+    rc = zero_copy(v) ? solve_zero_copy(v, q, cs, setup_init, overlap) : solve_staged(v, q, cs, setup_init, overlap);
     if (cur != v.dev && cur >= 0) (void)hipSetDevice(cur);
     if (rc) return rc;
     if (setup_init) v.inited = true;
@@ -812,8 +834,10 @@ QP *setup_init(QP *q, clk::time_point t0) {
     const char *e = std::getenv("QPSWIFT_HIP_SETUP_INIT");
     int ndev = 0;
     if (v.plan && !(e && e[0] == '0') && hipGetDeviceCount(&ndev) == hipSuccess && ndev > 0) {
-        if (solve_on_device(v, *q, true) != QPB_OK) v.err = qpb_last_error();
+        // the reference's struct mirror is filled while the device computes the point
+        if (solve_on_device(v, *q, true, [&v, q] { finish_mirror(v, *q); }) != QPB_OK) v.err = qpb_last_error();
     }
+    finish_mirror(v, *q);    // (no device init, or it failed before posting)
     v.st.tsetup = seconds_since(t0);
     return q;
 }
@@ -851,7 +875,7 @@ QP *QP_SETUP(qp_int n, qp_int m, qp_int p, qp_int *Pjc, qp_int *Pir, qp_real *Pp
     q.c = c;
     q.h = h;
     q.sigma_d = sigma_d;
-    return setup_init(finish_setup(hd, Permut, t0), t0);
+    return setup_init(finish_setup(hd, Permut), t0);
 }
 
 QP *QP_SETUP_dense(qp_int n, qp_int m, qp_int p, qp_real *Ppr, qp_real *Apr, qp_real *Gpr, qp_real *c,
@@ -879,7 +903,7 @@ QP *QP_SETUP_dense(qp_int n, qp_int m, qp_int p, qp_real *Ppr, qp_real *Apr, qp_
     q.c = c;
     q.h = h;
     q.sigma_d = 0.0;   // qpSWIFT.c:334
-    return setup_init(finish_setup(hd, Permut, t0), t0);
+    return setup_init(finish_setup(hd, Permut), t0);
 }
 
 qp_int QP_SOLVE(QP *myQP) {
