@@ -22,7 +22,7 @@ SIMDS = 256 * 4
 FP64_PEAK_FLOP_PER_CYC_SIMD = 32      # 78.6 TF / (1 024 SIMDs x 2.4 GHz)
 
 
-def load(d, prefix="qpb_row"):
+def load(d, prefix="qpb_row", by_name=False):
     vals = defaultdict(list)
     dur = defaultdict(list)
     wgs = {}
@@ -30,7 +30,7 @@ def load(d, prefix="qpb_row"):
         for r in csv.DictReader(open(f)):
             if not r["Kernel_Name"].startswith(prefix):
                 continue
-            key = int(r["Grid_Size"])
+            key = (r["Kernel_Name"].split("(")[0], int(r["Grid_Size"])) if by_name else int(r["Grid_Size"])
             wgs[key] = int(r["Workgroup_Size"])
             vals[(key, r["Counter_Name"])].append(float(r["Counter_Value"]))
             dur[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
@@ -40,11 +40,14 @@ def load(d, prefix="qpb_row"):
 def main():
     src, out = sys.argv[1], sys.argv[2]
     tree = len(sys.argv) > 3 and sys.argv[3] == "tree"
-    vals, dur, wgs = load(src, "qpb_tree" if tree else "qpb_row")
+    wave = len(sys.argv) > 3 and sys.argv[3] == "wave"      # one QP per wavefront (controller shapes)
+    vals, dur, wgs = load(src, "qpb_tree" if tree else ("qpb_wave" if wave else "qpb_row"), by_name=wave)
     res = {}
     for grid in sorted({g for g, _ in vals}):
         c = {n: sum(v) / len(v) for (g, n), v in vals.items() if g == grid}
-        if tree:
+        if wave:
+            B = grid[1] // 64
+        elif tree:
             B = grid // wgs[grid]
             B = 1 if B == 8 else B          # one QP: the grid is padded to 8 blocks (one per XCD)
         else:
@@ -62,10 +65,13 @@ def main():
                     f"{c['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * cyc):.0%}, a wave waits {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.0%} "
                     f"of its cycles (LDS / descriptor loads / barriers)")
         simd_valu = c["SQ_ACTIVE_INST_VALU"] * 4 / (SIMDS * cyc)       # VALU-issue cycles per SIMD cycle
-        kind = kind if tree else (f"VALU issue at {wps:.1f} waves per SIMD (SIMD VALU busy {simd_valu:.0%}; neither HBM nor FP64 peak)"
+        if wave:
+            kind = (f"one QP per wavefront: {wps:.2f} waves per SIMD on average, SIMD VALU busy {c['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * cyc):.0%}, "
+                    f"a wave waits {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.0%} of its cycles (LDS / memory)")
+        kind = kind if (tree or wave) else (f"VALU issue at {wps:.1f} waves per SIMD (SIMD VALU busy {simd_valu:.0%}; neither HBM nor FP64 peak)"
                 if wps > 1.5 else
                 f"latency: one wave on {wps:.0%} of the SIMDs, VALU issue + LDS/memory waits (neither HBM nor FP64 peak)")
-        res[f"B={B}"] = {
+        res[f"{grid[0]} B={B}" if wave else f"B={B}"] = {
             "kind": kind, "simd_valu_busy": simd_valu,
             "kernel_s": t, "clock_ghz": clock / 1e9, "waves": waves,
             "waves_per_simd_avg": wc / (SIMDS * cyc),
@@ -81,7 +87,8 @@ def main():
             "fp64_issue_frac_of_peak": flops_issued / (FP64_PEAK_FLOP_PER_CYC_SIMD * SIMDS * cyc),
             "counters": c,
         }
-    res["reading"] = ("MPC (N = 380): one QP alone runs 6 passes of ~118 gather / panel steps each (~1 us per "
+    res["reading"] = ("controller-shape QPs (30 variables), one QP per wavefront: the dense LDL' and the "
+                      "triangular solves are one wave's dependency chain; see DESIGN §4b") if wave else ("MPC (N = 380): one QP alone runs 6 passes of ~118 gather / panel steps each (~1 us per "
                       "step: descriptor wait, LDS terms, butterfly, epilogue, barrier); at 1 024 QPs (4 per CU) the "
                       "average wave lives ~0.98 ms of the 1.65 ms launch -- the launch is as long as the slowest QP "
                       "(10-11 iterations vs a mean of 5.7), which runs alone at the end: latency, not throughput"
