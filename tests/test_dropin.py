@@ -128,6 +128,32 @@ def test_setup_mirror_equals_reference_setup(name, null_perm):
         assert np.array_equal(np.asarray(ref[key]), np.asarray(ours[key])), key
 
 
+def test_setup_mirror_unchanged_by_reused_storage():
+    """Released QP objects' host storage is pooled per thread and taken over by the
+    next QP_SETUP (qpswift_dropin.cpp priv_put / priv_get): a C1 setup made after a
+    larger 30/68/18 object (and an MPC one) was released must mirror exactly what the
+    first C1 setup of the process did -- no size, value or field carried over."""
+    L = _lib.lib()
+
+    def mirror(name):
+        g = golden(name)
+        args = _golden_dense_args(g, 0)
+        n, m, p = args[:3]
+        keep = [None if a is None else np.ascontiguousarray(a, dtype=np.float64) for a in args[3:]]
+        qp = L.QP_SETUP_dense(n, m, p, *[abi.dptr(a) for a in keep], abi.lptr(None), int(g["ordering"]))
+        out = _setup_mirror(L, qp, n, m, p)
+        L.QP_CLEANUP_dense(qp)
+        return out
+
+    first = mirror("c1_tol1e-6")
+    for other in ("c30_tol1e-2", "mpc_h10", "c30_trot_tol1e-2"):
+        mirror(other)
+        again = mirror("c1_tol1e-6")
+        assert first.keys() == again.keys()
+        for key in first:
+            assert np.array_equal(np.asarray(first[key]), np.asarray(again[key])), (other, key)
+
+
 def test_setup_null_permut_fills_reference_perm_and_amd_result():
     g = golden("c1_tol1e-6")
     qp, keep = dropin.setup_dense(*_golden_dense_args(g, 0))
