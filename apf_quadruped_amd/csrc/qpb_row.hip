@@ -66,12 +66,14 @@ struct qpb_args {
 };
 
 // Staging / H0 knobs.  Round 1 saw an illegal-address fault with ZF128, AADPP and
-// LATEFAC all on.  Until its cause is named ZF128 and AADPP ship off.
+// LATEFAC all on; round 3 found no faulting instruction in today's objects.
+// ZF128 stays off (the unrolled zero-fill replaced it); AADPP is on since round 4
+// (+2 % at 1 024 and 2^20 QPs, profiles/r04_aadpp_ab.jsonl, the GPU suite green).
 #ifndef QPB_R_ZF128
 #define QPB_R_ZF128 0     // zero-fill the staging area with 16-byte LDS stores
 #endif
 #ifndef QPB_R_AADPP
-#define QPB_R_AADPP 0     // 1e7 A'A of H0 by DPP broadcasts (1) or LDS reads (0)
+#define QPB_R_AADPP 1     // 1e7 A'A of H0 by DPP broadcasts (1) or LDS reads (0)
 #endif
 #ifndef QPB_R_LATEFAC
 #define QPB_R_LATEFAC 1   // factor after the exit test (0: before it, overlapping the reductions)
