@@ -3,7 +3,11 @@ does (QP_SETUP_dense -> options -> QP_SOLVE -> read x -> QP_CLEANUP_dense,
 main.cpp:1649-1663), next to the reference qpSWIFT on the host CPU (oracle/_ref,
 when present).
 
-    python scripts/dropin_latency.py [--ticks N] [--shape c1|c30] [--mode exact|fast]
+    python scripts/dropin_latency.py [--ticks N] [--shape c1|c30] [--mode exact|fast] [--permut amd|leaves]
+
+--permut leaves passes the leaves-first KKT ordering (z rows, y rows, then x) through
+QP_SETUP_dense's own Permut argument (qpSWIFT.c:296-303) to both the drop-in and the CPU
+reference, instead of NULL (-> AMD, what the controller passes).
 """
 import argparse
 import ctypes as C
@@ -25,6 +29,7 @@ def main():
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--tol", type=float, default=1e-2)        # the controller's (main.cpp:1651)
     ap.add_argument("--setup-init", type=int, default=1, help="QPSWIFT_HIP_SETUP_INIT (recorded only)")
+    ap.add_argument("--permut", default="amd", choices=["amd", "leaves"])
     a = ap.parse_args()
     from apf_quadruped_amd import _lib, plans, qpswift_abi as abi, workloads as W
     if a.mode == "exact":
@@ -45,13 +50,17 @@ def main():
     args = [tuple(abi.dptr(X[t]) for X in (P, A, G, c, h, b)) for t in range(a.ticks)]
 
     serve = (C.c_long * 4)()
+    permut = None
+    if a.permut == "leaves":
+        perm = np.concatenate([np.arange(n + p, n + p + m), np.arange(n, n + p), np.arange(n)]).astype(np.int64)
+        permut = perm.ctypes.data_as(C.POINTER(C.c_long))
 
     def run(lib):
         lat, flags, xs, seg, dev = [], [], [], [], []
         for t in range(a.ticks):
             Pt, At, Gt, ct, ht, bt = args[t]
             t0 = time.perf_counter()
-            qp = lib.QP_SETUP_dense(n, m, p, Pt, At, Gt, ct, ht, bt, None, abi.COLUMN_MAJOR_ORDERING)
+            qp = lib.QP_SETUP_dense(n, m, p, Pt, At, Gt, ct, ht, bt, permut, abi.COLUMN_MAJOR_ORDERING)
             t1 = time.perf_counter()
             o = qp.contents.options.contents
             o.reltol = a.tol
@@ -73,7 +82,7 @@ def main():
     L = _lib.lib()
     run(L)                                   # first ticks: plan + kernel (cache) + device buffers
     lat, flags, xs = run(L)
-    out = dict(shape=a.shape, mode=a.mode, tol=a.tol, ticks=a.ticks, setup_init=a.setup_init, optimal=float((flags == 0).mean()),
+    out = dict(shape=a.shape, mode=a.mode, permut=a.permut, tol=a.tol, ticks=a.ticks, setup_init=a.setup_init, optimal=float((flags == 0).mean()),
                gpu_us_median=float(np.median(lat) * 1e6), gpu_us_p99=float(np.percentile(lat, 99) * 1e6),
                gpu_setup_us=float(run.seg[0]), gpu_solve_us=float(run.seg[1]))
     L.qpb_dropin_serve_stats(serve)

@@ -202,6 +202,35 @@ def test_dropin_fast_default_with_reference_permutation(name):
             scale = max(1.0, float(np.abs(g[k][q]).max()))
             assert np.abs(r[k] - g[k][q]).max() <= 1e-6 * scale, (name, q, k)
 
+def _leaves_perm(n, m, p):
+    """The leaves-first KKT ordering (z rows, y rows, then x in natural order), as a
+    caller would pass it through QP_SETUP_dense's Permut (qpSWIFT.c:296-303)."""
+    return np.concatenate([np.arange(n + p, n + p + m), np.arange(n, n + p), np.arange(n)]).astype(np.int64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c30_tol1e-2", "c30_trot_tol1e-2", "c30_crawl_tol1e-2", "c1_tol1e-2"])
+def test_dropin_leaves_first_permut_matches_oracle(name, oracle):
+    """A caller-supplied leaves-first Permut (the faster one-row-per-lane factor on the
+    device, scripts/dropin_latency.py --permut leaves): the drop-in against the oracle
+    run in the same order -- flag and iterations equal, x, y, z, s within 1e-6 -- and
+    AMD_RESULT = -3 (a given permutation, qpSWIFT.c:296-303)."""
+    g = golden(name)
+    n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    perm = _leaves_perm(n, m, p)
+    for q in range(0, g["x"].shape[0], 2):
+        r = dropin.solve_dense(*_golden_dense_args(g, q), perm=perm, ordering=int(g["ordering"]),
+                               reltol=tol, abstol=tol, maxit=maxit)
+        o = oracle.solve_dense(n, m, p, g["P"][q], g["A"][q] if p else None, g["G"][q], g["c"][q], g["h"][q],
+                               g["b"][q], perm=perm, ordering=int(g["ordering"]), reltol=tol, abstol=tol, maxit=maxit)
+        assert r["amd_result"] == -3
+        assert r["flag"] == o["flag"] and r["iters"] == o["iters"], (name, q)
+        for k in ("x", "z", "s") + (("y",) if p else ()):
+            scale = max(1.0, float(np.abs(o[k]).max()))
+            assert np.abs(r[k] - o[k]).max() <= 1e-6 * scale, (name, q, k)
+
+
 DENSE = ["c1_tol1e-6", "c1_tol1e-2", "c1_rowmajor", "c1_noeq", "edge_zero_g_row", "mixed_stance4",
          "mixed_trot_blfr", "mixed_crawl_blflfr", "c1_maxit0", "c1_maxit2", "c1_maxit5", "edge_infeasible",
          "edge_infeasible_maxit8"]
