@@ -84,11 +84,20 @@ static long wave_lds_doubles(const Plan &pl, long nd, long ldg) {
 // workgroup size and QPs per CU for a footprint of `doubles` per QP
 static int wg_for_doubles(long doubles, int *qps_per_cu) {
     const long bytes = doubles * 8;
-    // as many QPs per CU as the 160 KiB allow (whole workgroups), ties -> larger workgroups
+    // as many QPs per CU as the 160 KiB allow (whole workgroups), ties -> larger
+    // workgroups; except where the LDS holds a CU to at most 16 QPs: there the smallest
+    // size that reaches the same count, since a workgroup's LDS is freed only when its
+    // slowest QP finishes and one-wave workgroups refill the CU QP by QP (8 192
+    // AMD-ordered 30/68/18 QPs 2.33 -> 2.24 ms against four-wave workgroups,
+    // profiles/r04_wave_wg_ab.log; 1 024 QPs unchanged)
     int best = 0, best_qps = 0;
     for (int waves = 4; waves >= 1; waves--) {
         const long per_cu = (160L * 1024) / (bytes * waves);
         if (per_cu * waves > best_qps) { best_qps = (int)(per_cu * waves); best = waves; }
+    }
+    for (int waves = 1; waves < best && best_qps <= 16; waves++) {
+        const long per_cu = (160L * 1024) / (bytes * waves);
+        if (per_cu * waves == best_qps) { best = waves; break; }
     }
     if (qps_per_cu) *qps_per_cu = best_qps;
     return 64 * best;
@@ -113,7 +122,16 @@ static long wave_ldz(const Plan &pl, long nd) {
 
 int wave_wg_for(const Plan &pl) {
     const long nd = (long)wave_layout(pl).dense.size();
-    return wg_for_doubles(wave_lds_doubles(pl, nd, wave_ldz(pl, nd)), nullptr);
+    const long doubles = wave_lds_doubles(pl, nd, wave_ldz(pl, nd));
+    const int wg = wg_for_doubles(doubles, nullptr);
+    // QPB_WAVE_OPTS="QPB_W_WG=64|128|192|256": a smaller workgroup with the same QPs per CU
+    // (a workgroup's LDS is freed only when its slowest QP finishes)
+    if (const char *e = getenv("QPB_WAVE_OPTS"))
+        if (const char *k = strstr(e, "QPB_W_WG=")) {
+            const int w = atoi(k + 9);
+            if (w >= 64 && w <= wg && w % 64 == 0) return w;
+        }
+    return wg;
 }
 
 bool wave_eligible(const Plan &pl, std::string *why) {
