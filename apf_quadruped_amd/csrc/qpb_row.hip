@@ -186,10 +186,14 @@ template <int CTRL> static __device__ __forceinline__ double qpb_dpp(double v) {
 //  - qpb_fxs: static sources (prologue slices) and the factor's columns;
 //  - qpb_fx:  dynamic sources, volatile so a phase keeps its order;
 //  - qpb_fxd: the chained triangular solves (src is the accumulator itself).
-#ifndef QPB_DPP_NOP
-#define QPB_DPP_NOP 0
-#endif
-#if QPB_DPP_NOP >= 2
+#ifndef QPB_DPP_NOP           // -1: no wait states in the asm text, the post-assembly pass places each one
+#define QPB_DPP_NOP -1         // (0: a fixed s_nop 1 in the chained asm, on top of the s_nop 0 LLVM puts
+#endif                         // between dependent inline asm on gfx950 -- 3 wait states for 2; -2 % per
+                               // headline launch, profiles/r04_dpp_nop_ab.log)
+#if QPB_DPP_NOP < 0           // every wait state placed by the post-assembly pass (qpb_hazard asm_fixup)
+#define QPB_DPP_PRE ""
+#define QPB_DPP_DEP ""
+#elif QPB_DPP_NOP >= 2
 #define QPB_DPP_PRE "s_nop 4\n\t"
 #define QPB_DPP_DEP "s_nop 4\n\t"
 #elif QPB_DPP_NOP

@@ -230,10 +230,14 @@ template <int J> static __device__ __forceinline__ double qpb_xb(double v) {
 // out from the source: the runtime audits every compiled code object
 // (qpb_runtime.hip, dpp_audit) and rebuilds with QPB_DPP_NOP = 2 (wait states
 // inside every DPP asm) should it find a hazard.
-#ifndef QPB_DPP_NOP
-#define QPB_DPP_NOP 0
-#endif
-#if QPB_DPP_NOP >= 2
+#ifndef QPB_DPP_NOP           // -1: no wait states in the asm text, the post-assembly pass places each one
+#define QPB_DPP_NOP -1         // (0: a fixed s_nop 1 in the chained asm, on top of the s_nop 0 LLVM puts
+#endif                         // between dependent inline asm on gfx950 -- 3 wait states for 2; -2 % per
+                               // headline launch, profiles/r04_dpp_nop_ab.log)
+#if QPB_DPP_NOP < 0           // every wait state placed by the post-assembly pass (qpb_hazard asm_fixup)
+#define QPB_DPP_PRE ""
+#define QPB_DPP_DEP ""
+#elif QPB_DPP_NOP >= 2
 #define QPB_DPP_PRE "s_nop 4\n\t"
 #define QPB_DPP_DEP "s_nop 4\n\t"
 #elif QPB_DPP_NOP
