@@ -86,10 +86,12 @@ struct qpb_args {
                           // round trip at the start of every factor and residual pass)
 #endif
 #endif
-#ifndef QPB_R_LAZYREG
-#define QPB_R_LAZYREG 0   // 1: pivot regularisation checked once per factor, the factor redone only
-                          // when needed (measured: 1 024 QPs 32.7 vs 32.9 us, no gain; the two-wave
-                          // form spills 34 more registers with it)
+#ifndef QPB_R_LAZYREG     // 1: pivot regularisation checked once per factor, the factor redone only
+#if defined(QPB_R_WPE) && QPB_R_WPE > 1   // when needed (same bits).  The two-wave form spills 34
+#define QPB_R_LAZYREG 0   // more registers with it (2^20 QPs 3.59 -> 3.82 ms); the one-wave kernel
+#else                     // gains since the DPP wait states moved to the hazard pass (1 024 QPs
+#define QPB_R_LAZYREG 1   // 30.3 -> 29.8 us, profiles/r04_row_knobs2_ab.jsonl; round 3: no gain)
+#endif
 #endif
 #ifndef QPB_R_GWG4
 #define QPB_R_GWG4 1      // G'WG four rows at a time, products formed before their DPP FMAs
