@@ -420,3 +420,41 @@ def test_infeasible_runs_to_maxit(name, own_order, kernel):
     for k in ("x", "y", "z", "s"):
         assert np.isfinite(r[k]).all(), (name, kernel, k)
 
+
+
+@pytest.mark.gpu
+def test_row_kernel_zero_pivot_refactor_matches_oracle(oracle, monkeypatch):
+    """The one-wave row kernel checks the pivot regularisation once per factor
+    (QPB_R_LAZYREG) and redoes the factor with the regularised reciprocals
+    (ldl.c:318-319) only when some pivot is <= 1e-14.  Force that path: variable 0 of
+    the contact QPs decoupled (its P row / column, G and A columns and c entry zeroed),
+    so its pivot is exactly 0 in every factor; the kernel vs the oracle in the plan's
+    order, flags and iterations equal, x / y / z / s within 1e-9, and the two-wave
+    kernel (which regularises every pivot inline) bit-identical."""
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan
+    B = 200
+    d = {k: np.array(v, copy=True) if isinstance(v, np.ndarray) else v
+         for k, v in W.contact_force_qp(0xD06B07 + 23, np.arange(B)).items()}
+    d["P"][:, 0, :] = 0.0
+    d["P"][:, :, 0] = 0.0
+    d["G"][:, :, 0] = 0.0
+    d["A"][:, :, 0] = 0.0
+    d["c"][:, 0] = 0.0
+    plan = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0], kernel="wave")
+    assert plan.kernel_name(B).startswith("qpb_row")
+    r = plan.unpack(plan.solve(**plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]), B=B), B)
+    Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    for q in (0, 1, B // 2, B - 1):
+        o = oracle.solve_dense(12, 20, 6, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm)
+        assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], q
+        for k in ("x", "y", "z", "s"):
+            scale = max(1.0, float(np.abs(o[k]).max()))
+            assert np.abs(r[k][q] - o[k]).max() <= 1e-9 * scale, (q, k)
+        assert r["x"][q][0] == 0.0
+    monkeypatch.setenv("QPB_ROW_OCC_BATCH", "100")       # B = 200 on the two-wave kernel
+    plan2 = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0], kernel="wave")
+    assert plan2.kernel_name(B) != plan.kernel_name(B)
+    r2 = plan2.unpack(plan2.solve(**plan2.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]), B=B), B)
+    for k in ("x", "y", "z", "s", "fval", "iters", "flag"):
+        np.testing.assert_array_equal(r[k], r2[k])
