@@ -101,6 +101,8 @@ def lib() -> C.CDLL:
     L.qpb_plan_compile_warm.argtypes = [vp, C.c_long]
     L.qpb_plan_compile_serve.argtypes = [vp]
     L.qpb_dropin_serve_stats.argtypes = [C.POINTER(C.c_long)]
+    L.qpb_serve_config.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    L.qpb_serve_config.restype = C.c_int
     L.qpb_solve.restype = C.c_int
     L.qpb_solve.argtypes = [vp, C.c_long] + [vp] * 6 + [C.POINTER(QpbSettings)] + [vp] * 7 + [vp, vp]
     L.qpb_solve_warm.restype = C.c_int

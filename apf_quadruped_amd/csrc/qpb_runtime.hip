@@ -880,9 +880,7 @@ int qpb_plan_compile_warm(qpb_plan *plan, long B) {
 
 int qpb_plan_compile_serve(qpb_plan *plan) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
-    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
-                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || 1 <= plan->wave_max_batch)));
-    if (!wave) return qpb::SERVE_NONE;
+    if (!qpb::serve_eligible(plan)) return qpb::SERVE_NONE;
     std::shared_ptr<std::vector<char>> *slot = nullptr;
     auto gen = [plan] { return qpb::wave_source_of(plan); };
     int rc = qpb::compile_variant(plan, plan->wave_kname, gen, false, false, true, &slot);
@@ -1033,11 +1031,21 @@ unsigned long long serve_life_ticks() {
     return t;
 }
 // the calling thread's servers, for serve_retire_thread (a server belongs to the
-// workspace of the thread that solves through it)
-thread_local std::vector<qpb::Server *> t_servers;
+// workspace of the thread that solves through it).  A plain pointer, not a vector:
+// thread_local objects are destroyed in reverse order of construction, and the
+// drop-in's workspaces (which own Servers) are constructed before this list is first
+// used -- so at thread exit ~Server runs after a thread_local vector would already be
+// gone.  A trivially destructible pointer stays readable through the whole teardown;
+// the list itself is freed by the last ~Server that empties it.
+thread_local std::vector<qpb::Server *> *t_servers = nullptr;
 unsigned long long mb_load(const unsigned long long *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 void mb_store(unsigned long long *p, unsigned long long v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
 }  // namespace
+
+bool qpb::serve_eligible(const qpb_plan *plan) {
+    return plan && plan->wave_ok &&
+           (plan->kernel_pref == 2 || (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || 1 <= plan->wave_max_batch)));
+}
 
 // A retired server's wave saw the stop word (or will, the moment it starts): wait for
 // it to leave and re-arm the mailbox before the next launch.
@@ -1050,7 +1058,8 @@ static int serve_settle(qpb::Server *srv) {
 }
 
 void qpb::serve_retire_thread() {
-    for (Server *srv : t_servers) {
+    if (!t_servers) return;
+    for (Server *srv : *t_servers) {
         if (!srv->running) continue;
         mb_store(srv->mb, kStop);        // the queued wave leaves at its next poll (~0.1 us)
         srv->running = false;
@@ -1072,8 +1081,12 @@ int qpb::serve_stop(Server *srv) {
 
 qpb::Server::~Server() {
     (void)serve_stop(this);
-    for (size_t i = 0; i < t_servers.size(); i++)
-        if (t_servers[i] == this) { t_servers.erase(t_servers.begin() + (long)i); break; }
+    if (registered && t_servers) {
+        auto &v = *t_servers;
+        for (size_t i = 0; i < v.size(); i++)
+            if (v[i] == this) { v.erase(v.begin() + (long)i); break; }
+        if (v.empty()) { delete t_servers; t_servers = nullptr; }
+    }
     if (stream) (void)hipStreamDestroy((hipStream_t)stream);
     if (mb) (void)hipHostFree(mb);
 }
@@ -1088,9 +1101,7 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
     if (!P || !G || !c || !h || !x || !z || !s || !flag || !iters || !fval) return fail(QPB_EINVAL, "NULL data pointer");
     if (pl.p > 0 && (!A || !b || !y)) return fail(QPB_EINVAL, "p > 0 needs A, b and y");
     // the kernel solve_ex would launch for one QP must be the row or the wave form
-    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
-                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || 1 <= plan->wave_max_batch)));
-    if (!wave) return SERVE_NONE;
+    if (!serve_eligible(plan)) return SERVE_NONE;
     std::shared_ptr<std::vector<char>> *slot = nullptr;
     int rc = compile_variant(plan, plan->wave_kname, [plan] { return qpb::wave_source_of(plan); }, false, warm, true,
                              &slot);
@@ -1137,7 +1148,8 @@ int qpb::serve_ex(qpb_plan *plan, Server *srv, const double *P, const double *A,
     }
     hipStream_t sm = (hipStream_t)srv->stream;
     if (!srv->registered) {
-        t_servers.push_back(srv);
+        if (!t_servers) t_servers = new std::vector<Server *>();
+        t_servers->push_back(srv);
         srv->registered = true;
     }
     if ((rc = serve_settle(srv))) return rc;
@@ -1242,6 +1254,12 @@ extern "C" {
  * call it themselves; the next QP_SOLVE relaunches. */
 int qpb_dropin_quiesce(void) {
     qpb::serve_retire_thread();
+    return QPB_OK;
+}
+
+int qpb_serve_config(double *idle_ms, double *life_ms) {
+    if (idle_ms) *idle_ms = (double)serve_idle_ticks() * 1e-5;    // 100 MHz ticks -> ms
+    if (life_ms) *life_ms = (double)serve_life_ticks() * 1e-5;
     return QPB_OK;
 }
 

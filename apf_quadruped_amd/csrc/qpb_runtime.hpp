@@ -116,6 +116,10 @@ struct Server {
     ~Server();                           // stops the kernel, frees the mailbox and stream
 };
 constexpr int SERVE_NONE = 1;            // serve_ex: this plan's one-QP kernel has no persistent form
+// The one predicate for "serve_ex answers this plan" (its one-QP kernel is the row or the
+// wave form): serve_ex, qpb_plan_compile_serve and the drop-in's packed-slab choice all
+// use it, so they cannot disagree (a packed slab read by a launched kernel would be wrong).
+bool serve_eligible(const qpb_plan *plan);
 // One QP (B = 1, the tiled slot of QP 0) through `srv`: returns once the results are
 // in x .. trace.  SERVE_NONE when the plan's kernel for one QP is neither the row
 // nor the wave form (the caller launches instead).

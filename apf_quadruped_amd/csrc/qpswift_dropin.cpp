@@ -345,10 +345,26 @@ void finish_mirror(Priv &v, QP &q) {
 // A reused Priv is a freshly constructed one that took over the old vectors'
 // capacity -- every other field starts from its default.
 constexpr size_t kPrivPool = 4;
-thread_local std::vector<Priv *> t_priv_pool;
+// The pool owns what it holds: its destructor deletes the pooled objects when the
+// thread exits (a controller on short-lived threads must not leak them).  A QP
+// released after that (from another thread_local's destructor) is deleted outright.
+struct PrivPool {
+    std::vector<Priv *> v;
+    PrivPool() = default;
+    PrivPool(const PrivPool &) = delete;
+    PrivPool &operator=(const PrivPool &) = delete;
+    ~PrivPool();
+};
+thread_local PrivPool t_priv_pool;
+thread_local bool t_priv_pool_gone = false;      // trivially destructible: readable at teardown
+PrivPool::~PrivPool() {
+    for (Priv *p : v) delete p;
+    v.clear();
+    t_priv_pool_gone = true;
+}
 
 void priv_put(Priv *v) {
-    if (t_priv_pool.size() >= kPrivPool) { delete v; return; }
+    if (t_priv_pool_gone || t_priv_pool.v.size() >= kPrivPool) { delete v; return; }
     Priv fresh;
 #define QPB_TAKE(f) fresh.f.swap(v->f); fresh.f.clear();
     QPB_TAKE(Pjc) QPB_TAKE(Pir) QPB_TAKE(Ajc) QPB_TAKE(Air) QPB_TAKE(Gjc) QPB_TAKE(Gir)
@@ -361,13 +377,13 @@ void priv_put(Priv *v) {
     QPB_TAKE(temp)
 #undef QPB_TAKE
     *v = std::move(fresh);
-    t_priv_pool.push_back(v);
+    t_priv_pool.v.push_back(v);
 }
 
 Priv *priv_get() {
-    if (t_priv_pool.empty()) return new (std::nothrow) Priv();
-    Priv *v = t_priv_pool.back();
-    t_priv_pool.pop_back();
+    if (t_priv_pool_gone || t_priv_pool.v.empty()) return new (std::nothrow) Priv();
+    Priv *v = t_priv_pool.v.back();
+    t_priv_pool.v.pop_back();
     return v;
 }
 
@@ -431,12 +447,6 @@ thread_local std::map<int, Workspace> t_ws;
 
 bool zero_copy(const Priv &v) { return zero_copy_enabled() && !v.plan->gen.exact; }
 
-// the plan's one-QP kernel is the row or the wave form, i.e. qpb::serve_ex answers
-// (qpb_runtime.hip serve_ex: the same condition; otherwise it returns SERVE_NONE)
-bool serves_one_qp(const qpb_plan *plan) {
-    return plan && plan->wave_ok &&
-           (plan->kernel_pref == 2 || (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || 1 <= plan->wave_max_batch)));
-}
 
 int ensure_device(Priv &v, const QP &q) {
     int ndev = 0;
@@ -448,7 +458,7 @@ int ensure_device(Priv &v, const QP &q) {
         // slab it serves holds every vector contiguous -- 8 values per 64-byte line over
         // the host link instead of one; launched kernels read the tiled layout
         const char *wo = std::getenv("QPB_WAVE_OPTS");
-        const bool packed = zero_copy(v) && serve_enabled() && serves_one_qp(v.plan.get()) &&
+        const bool packed = zero_copy(v) && serve_enabled() && qpb::serve_eligible(v.plan.get()) &&
                             !(wo && std::strstr(wo, "QPB_TSTR=64"));
         const long T = packed ? 1 : 64;
         v.tstride = T;
@@ -647,6 +657,10 @@ int solve_zero_copy(Priv &v, QP &q, const CallState &cs, bool setup_init, const 
                            d + v.oz, d + v.os, dfl, dfl + 1, d + v.ofv, d + v.ost, d + osg, cs.warm, d + v.otr,
                            d + v.owin, overlap);
     if (rc == qpb::SERVE_NONE) {
+        // a launched kernel reads the tiled slot (stride 64): a packed slab here would be
+        // read wrongly without any error -- refuse instead (serve_eligible decides both)
+        if (T != 64)
+            return qpb::set_error(QPB_EHIP, "QP_SOLVE: packed slab but no persistent solver answered (internal)");
         if (overlap) overlap();       // (no persistent solver: nothing to overlap with)
         rc = qpb::solve_ex(v.plan.get(), 1, d + v.oP, p > 0 ? d + v.oA : nullptr, d + v.oG, d + v.oc, d + v.oh,
                            p > 0 ? d + v.ob : nullptr, &cs.st, d + v.ox, p > 0 ? d + v.oy : nullptr, d + v.oz,

@@ -71,18 +71,48 @@ def _free_port() -> int:
     return port
 
 
+def count_gpus_in_child() -> int:
+    """Visible GPUs, counted by a throwaway child process: whatever HIP (or amdsmi)
+    initialisation the count needs happens there, so the launcher itself never loads
+    the HIP runtime -- a parent that touched the GPU and then spawns ranks is the
+    pattern this pool refuses.  -1 when the child fails."""
+    import subprocess
+    try:
+        r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=600)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else -1
+    except Exception:
+        return -1
+
+
+def _parent_maps_report():
+    """QPB_BENCH_PARENT_MAPS=<file>: the launcher writes the shared objects mapped into
+    its own process (tests/test_multi.py checks that no HIP runtime is among them)."""
+    out = os.environ.get("QPB_BENCH_PARENT_MAPS")
+    if not out:
+        return
+    libs = set()
+    with open("/proc/self/maps") as f:
+        for ln in f:
+            parts = ln.split()
+            if len(parts) >= 6 and ".so" in parts[-1]:
+                libs.add(os.path.basename(parts[-1]))
+    with open(out, "w") as f:
+        json.dump({"pid": os.getpid(), "libs": sorted(libs),
+                   "torch_imported": "torch" in sys.modules}, f)
+
+
 def launch_ranks(args) -> int:
     """`python bench.py --gpus N` without a launcher: start N rank processes of this
     script (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT
     set as torch.distributed.run sets them) and return the worst exit code.  This
-    process never touches the GPU: it only counts devices (torch.cuda.device_count
-    does not initialise HIP on this image), and refuses to run fewer ranks than asked.
-    Rank 0 prints the JSON line; every rank's stderr passes through."""
+    process never touches the GPU and never imports torch: the device count comes from
+    a throwaway child (count_gpus_in_child), and it refuses to run fewer ranks than
+    asked.  Rank 0 prints the JSON line; every rank's stderr passes through."""
     import subprocess
     n = args.gpus
     if not args.dry_run:
-        import torch
-        have = torch.cuda.device_count()
+        have = count_gpus_in_child()
         if have < n:
             print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}", file=sys.stderr)
             return 2
@@ -93,6 +123,7 @@ def launch_ranks(args) -> int:
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     codes = [p.wait() for p in procs]
+    _parent_maps_report()
     bad = [c for c in codes if c != 0]
     if bad:
         print(f"bench.py: rank exit codes {codes}", file=sys.stderr)
@@ -233,7 +264,8 @@ def shape_leg(name, gen, B, tol, dev, steps=50, warmup=5, cpu=None):
     res = {"workload": name, "batch": B, "value": B * steps / el, "unit": "QP solves/s",
            "ms_per_step": el * 1e3 / steps, "kernel": kn, "kernel_ms": km, "kernel_qps": B / (km * 1e-3),
            "kkt_N": plan.info.N, "nnz_L": plan.info.lnz,
-           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "roofline": {"bound": measured_bound(kn, B), "roofline_ref": "hbm", "achieved": ach,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ach / HBM_PEAK_GBS, "traffic": traffic_for(kn, B), "bytes_per_qp": bpq},
            "mean_iters": float(out["iters"].float().mean().item()),
            "optimal_frac": float((out["flag"] == 0).float().mean().item())}
@@ -492,6 +524,48 @@ def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
             "optimal_frac": float((out["flag"] == 0).float().mean().item())}
 
 
+def _sq_record(kname, B):
+    """The newest SQ-counter summary for this kernel at this batch (profiles/r0N_sq_*.json,
+    scripts/gpu_sq*.sh + scripts/sq_summary.py): row-kernel files key "B=<B>", the tree
+    file "B=<B>", the wave file "<kernel> B=<B>"."""
+    kind = "row" if kname.startswith("qpb_row") else ("tree" if kname.startswith("qpb_tree") else
+                                                      ("wave" if kname.startswith("qpb_wave") else None))
+    if kind is None:
+        return None, None
+    for rnd in ("r05", "r04", "r03"):
+        name = f"{rnd}_sq_{kind}.json"
+        f = os.path.join(ROOT, "profiles", name)
+        if not os.path.exists(f):
+            continue
+        d = json.load(open(f))
+        r = d.get(f"{kname} B={B}") or (d.get(f"B={B}") if kind != "wave" else None)
+        if r:
+            return r, "profiles/" + name
+    return None, None
+
+
+def fp64_issued(kname, B):
+    """FP64 actually issued (SQ_INSTS_VALU_FMA_F64 lane-ops, from the same SQ summary) next
+    to the algorithmic fraction, so the lanes' redundant work is visible in the line."""
+    r, src = _sq_record(kname, B)
+    if not r or "fp64_issue_frac_of_peak" not in r:
+        return {"issued_frac": None}
+    return {"issued_frac": r["fp64_issue_frac_of_peak"],
+            "issued_lane_fma_per_qp": r.get("per_qp", {}).get("fma_f64_lane_ops"), "issued_source": src}
+
+
+def measured_bound(kname, B):
+    """roofline.bound from the measured limiter, not from the roofline the fraction is
+    quoted against: "valu_issue" when the SIMDs' VALU is busy >= 60 % of the launch,
+    "latency" when it is not (a wave's dependency chain, few waves per SIMD),
+    "unmeasured" without counters for this kernel and batch.  (HBM never binds here:
+    traffic is <= 1.6x the algorithmic bytes at <= 10 % of peak.)"""
+    r, _ = _sq_record(kname, B)
+    if not r or r.get("simd_valu_busy") is None:
+        return "unmeasured"
+    return "valu_issue" if r["simd_valu_busy"] >= 0.6 else "latency"
+
+
 def limiter_for(B):
     """What the SQ counters say bounds the row kernel at this batch
     (profiles/r04_sq_row.json, else r03's; scripts/gpu_sq.sh + scripts/sq_summary.py)."""
@@ -627,7 +701,8 @@ def main():
         achl = bpq * BL / (km * 1e-3) / 1e9
         large = {"batch": BL, "value": BL * 10 / el, "ms_per_step": el * 1e3 / 10, "kernel": kl,
                  "kernel_ms": km, "kernel_qps": BL / (km * 1e-3),
-                 "roofline": {"bound": "hbm", "achieved": achl, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "roofline": {"bound": measured_bound(kl, BL), "roofline_ref": "hbm", "achieved": achl,
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": achl / HBM_PEAK_GBS, "traffic": traffic_for(kl, BL),
                               "limiter": limiter_for(BL) if kl.startswith("qpb_row") else None},
                  "fp64_tflops": flops_per_qp(plan.info, itl) * BL / (km * 1e-3) / 1e12,
@@ -685,13 +760,14 @@ def main():
                        "qps_per_gpu": B, "global_batch": B * world, "tol": args.tol,
                        "kernel": kname, "arith": "exact" if args.exact else "fast",
                        "kkt_N": plan.info.N, "nnz_L": plan.info.lnz, "parallelism": f"shard{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": measured_bound(kname, B), "roofline_ref": "hbm", "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(kname, B),
                          "algorithmic_bytes_per_launch": bpq * B, "bytes_per_qp": bpq,
                          "kernel_ms": kern_ms, "kernel": kname,
                          "limiter": limiter_for(B) if kname.startswith("qpb_row") else None},
-            "fp64": {"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
-                     "frac": fp64_tf / FP64_PEAK_TFLOPS, "flops_per_qp": fpq},
+            "fp64": dict({"achieved_tflops": fp64_tf, "peak_tflops": FP64_PEAK_TFLOPS,
+                          "frac": fp64_tf / FP64_PEAK_TFLOPS, "flops_per_qp": fpq}, **fp64_issued(kname, B)),
             "mean_iters": mean_it,
             "optimal_frac": float((flags == 0).mean()),
             "large_batch": large,

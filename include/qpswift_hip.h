@@ -319,6 +319,12 @@ int qpb_dropin_serve_stats(long out[4]);
  * QPSWIFT_HIP_SERVE_IDLE_MS.  qpb_solve / qpb_solve_best / qpb_solve_warm /
  * qpb_group_solve do this themselves.  The next QP_SOLVE relaunches (~20 us). */
 int qpb_dropin_quiesce(void);
+/* The persistent solver's effective settings for this process (read once from the
+ * environment): idle_ms = QPSWIFT_HIP_SERVE_IDLE_MS (default 20), life_ms = the
+ * multi-request lifetime -- 0 (one request per wave, the shipped mode) unless
+ * QPSWIFT_HIP_SERVE_LIFE_MS > 0 AND QPB_SERVE_DIAG=1 (a diagnostics-only mode with an
+ * open defect).  Needs no GPU. */
+int qpb_serve_config(double *idle_ms, double *life_ms);
 
 #ifdef __cplusplus
 }

@@ -6,6 +6,7 @@ checker), reduces it to (fval, local index) with the qpb_argmin rule, and the
 ranks exchange their payload (fval, local index, x*[12]: 16 + 96 B each, as
 qpb_winner builds it on the GPU); the gathered winner and its x* must equal the
 single-process argmin over the whole batch."""
+import json
 import os
 import socket
 
@@ -187,6 +188,21 @@ def test_bench_gpus_n_launches_n_ranks(n):
     assert [(d["rank"], d["local_rank"], d["world"]) for d in line["ranks"]] == [(r, r, n) for r in range(n)]
     assert [(d["lo"], d["hi"]) for d in line["ranks"]] == [(r * 8192, (r + 1) * 8192) for r in range(n)]
     assert line["master"][0] == "127.0.0.1"
+
+
+def test_bench_launcher_parent_never_loads_hip(tmp_path):
+    """The `--gpus N` launcher process itself loads no HIP runtime and does not import
+    torch (its device count comes from a throwaway child): checked from the parent's
+    own /proc/self/maps after its ranks have run."""
+    maps = tmp_path / "maps.json"
+    rc, line, err = _bench(["--gpus", "2", "--batch", "1024", "--dry-run"], {"QPB_BENCH_PARENT_MAPS": str(maps)})
+    assert rc == 0, err
+    rep = json.loads(maps.read_text())
+    assert rep["libs"], "no shared objects read from /proc/self/maps"
+    assert not rep["torch_imported"]
+    bad = [lib for lib in rep["libs"] if "amdhip" in lib or "hsa-runtime" in lib or "libtorch" in lib
+           or "rccl" in lib]
+    assert not bad, bad
 
 
 def test_bench_refuses_rank_count_mismatch():
