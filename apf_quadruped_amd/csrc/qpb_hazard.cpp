@@ -10,6 +10,16 @@
 //   * 5 after a VALU write of EXEC (v_cmpx);
 //   * kMfmaWs after an MFMA writes such a VGPR (its result lands late; the value
 //     is generous for every gfx950 MFMA shape, none of ours feeds DPP directly).
+// The audit over the whole code object checks two more gfx950 hazard classes, on every
+// instruction (compiler-generated code included -- a finding there would be a backend
+// gap; none exists in any kernel of this repository):
+//   * trans forwarding: a VALU instruction reading a VGPR written by a transcendental
+//     (v_rcp / v_rsq / v_sqrt / v_exp / v_log / v_sin / v_cos) needs 1 wait state --
+//     an inline-asm consumer of a v_rcp_f64 result gets none from the compiler;
+//   * a VMEM instruction reading an SGPR (its saddr / soffset) that a VALU wrote
+//     (v_readlane, v_readfirstlane, v_cmp into an SGPR pair, carry-outs) needs 5 -- a
+//     stale base would be a wrong (possibly illegal) address.
+// asm_fixup pads the inline-asm DPP instructions for the trans rule as well.
 // Two users of one scan:
 //   * asm_fixup: compiling a kernel with DPP asm goes through assembly (clang -S);
 //     every DPP instruction inside an inline-asm region gets exactly the s_nop it
@@ -29,11 +39,16 @@
 namespace qpb {
 namespace {
 
-constexpr int kDppVgprWs = 2, kDppExecWs = 5, kMfmaWs = 19, kMaxWs = kMfmaWs;
+constexpr int kDppVgprWs = 2, kDppExecWs = 5, kMfmaWs = 19, kTransWs = 1, kSgprVmemWs = 5, kMaxWs = kMfmaWs;
+enum Rules { R_DPP = 1, R_TRANS = 2, R_SGPR_VMEM = 4 };
 
 struct Insn {
     std::string mn;
     std::vector<std::pair<int, int>> vregs;   // every v register operand, [lo, hi], in operand order
+    std::vector<std::pair<int, int>> vreads;  // the VGPRs it reads (operand 0 only for mac / fmac / DPP)
+    std::vector<std::pair<int, int>> sregs;   // every s register operand (vcc as s1000:1001)
+    std::vector<std::pair<int, int>> sdefs;   // SGPRs a VALU instruction writes
+    bool valu = false, trans = false, vmem = false;
     bool vdef0 = false;                       // first operand is a VGPR the instruction writes (VALU)
     bool mfma = false;
     bool exec_valu_def = false;               // v_cmpx*: VALU write of EXEC
@@ -48,6 +63,23 @@ bool parse_vreg(const std::string &t, std::pair<int, int> &r) {
     size_t i = 0;
     while (i < t.size() && (t[i] == ' ' || t[i] == '\t' || t[i] == '-' || t[i] == '|')) i++;
     if (i + 1 >= t.size() || t[i] != 'v') return false;
+    if (t[i + 1] == '[') {
+        int a = 0, b = 0;
+        if (sscanf(t.c_str() + i + 2, "%d:%d]", &a, &b) != 2) return false;
+        r = {a, b};
+        return true;
+    }
+    if (!isdigit((unsigned char)t[i + 1])) return false;
+    const int a = atoi(t.c_str() + i + 1);
+    r = {a, a};
+    return true;
+}
+
+bool parse_sreg(const std::string &t, std::pair<int, int> &r) {
+    size_t i = 0;
+    while (i < t.size() && (t[i] == ' ' || t[i] == '\t' || t[i] == '-' || t[i] == '|')) i++;
+    if (t.compare(i, 3, "vcc") == 0) { r = {1000, 1001}; return true; }
+    if (i + 1 >= t.size() || t[i] != 's') return false;
     if (t[i + 1] == '[') {
         int a = 0, b = 0;
         if (sscanf(t.c_str() + i + 2, "%d:%d]", &a, &b) != 2) return false;
@@ -81,11 +113,17 @@ Insn parse_insn(const std::string &text) {
             ops.push_back(first);
         }
     }
-    for (auto &o : ops) {
-        std::pair<int, int> r;
-        if (parse_vreg(o, r)) a.vregs.push_back(r);
-    }
     const std::string &m = a.mn;
+    const bool reads_dst = m.find("mac") != std::string::npos || m.find("_dpp") != std::string::npos;
+    for (size_t k = 0; k < ops.size(); k++) {
+        std::pair<int, int> r;
+        if (parse_vreg(ops[k], r)) {
+            a.vregs.push_back(r);
+            if (k > 0 || reads_dst) a.vreads.push_back(r);
+        } else if (parse_sreg(ops[k], r)) {
+            a.sregs.push_back(r);
+        }
+    }
     a.dpp = m.find("_dpp") != std::string::npos;
     a.mfma = m.rfind("v_mfma", 0) == 0;
     const bool valu = m.rfind("v_", 0) == 0 && m.rfind("v_cmp", 0) != 0 && m.rfind("v_readlane", 0) != 0 &&
@@ -93,6 +131,16 @@ Insn parse_insn(const std::string &text) {
     std::pair<int, int> r0;
     a.vdef0 = valu && !ops.empty() && parse_vreg(ops[0], r0);
     a.exec_valu_def = m.rfind("v_cmpx", 0) == 0;
+    a.valu = m.rfind("v_", 0) == 0;
+    for (const char *t : {"v_rcp_", "v_rsq_", "v_sqrt_", "v_exp_", "v_log_", "v_sin_", "v_cos_"})
+        if (m.rfind(t, 0) == 0) a.trans = true;
+    a.vmem = m.rfind("global_", 0) == 0 || m.rfind("buffer_", 0) == 0 || m.rfind("flat_", 0) == 0 ||
+             m.rfind("scratch_", 0) == 0;
+    if (a.valu) {                                   // SGPRs a VALU instruction writes
+        std::pair<int, int> r;
+        if (!ops.empty() && parse_sreg(ops[0], r)) a.sdefs.push_back(r);                      // v_cmp sdst, readlane
+        if (m.find("_co_") != std::string::npos && ops.size() > 1 && parse_sreg(ops[1], r)) a.sdefs.push_back(r);
+    }
     if (m == "s_nop") a.ws = 1 + (int)strtol(rest.c_str(), nullptr, 0);
     a.uncond = m == "s_branch" || m == "s_endpgm" || m.rfind("s_setpc", 0) == 0;
     return a;
@@ -106,7 +154,7 @@ bool overlap(const std::pair<int, int> &a, const std::pair<int, int> &b) {
 // (backward walk over fall-through and branch predecessors) of what a hazardous
 // producer within its window demands.  `where` receives the worst producer.
 int need_ws(const std::vector<Insn> &ins, const std::map<std::string, std::vector<size_t>> &preds_of,
-            const std::map<size_t, std::string> &label_at, size_t d, std::string *where) {
+            const std::map<size_t, std::string> &label_at, size_t d, std::string *where, int rules = R_DPP | R_TRANS) {
     const Insn &D = ins[d];
     int need = 0;
     std::vector<std::pair<size_t, int>> stack;
@@ -126,10 +174,17 @@ int need_ws(const std::vector<Insn> &ins, const std::map<std::string, std::vecto
         stack.pop_back();
         const Insn &P = ins[p];
         int n = 0;
-        if (P.vdef0 && !P.vregs.empty())
+        if ((rules & R_DPP) && P.vdef0 && !P.vregs.empty())
             for (auto &u : D.vregs)
                 if (overlap(P.vregs[0], u)) n = std::max(n, (P.mfma ? kMfmaWs : kDppVgprWs) - ws);
-        if (P.exec_valu_def) n = std::max(n, kDppExecWs - ws);
+        if ((rules & R_DPP) && P.exec_valu_def) n = std::max(n, kDppExecWs - ws);
+        if ((rules & R_TRANS) && P.trans && P.vdef0 && D.valu && !D.trans)
+            for (auto &u : D.vreads)
+                if (overlap(P.vregs[0], u)) n = std::max(n, kTransWs - ws);
+        if ((rules & R_SGPR_VMEM) && D.vmem && P.valu)
+            for (auto &sd : P.sdefs)
+                for (auto &u : D.sregs)
+                    if (overlap(sd, u)) n = std::max(n, kSgprVmemWs - ws);
         if (n > need) {
             need = n;
             if (where) *where = P.mn + " (" + std::to_string(ws) + " wait states before)";
@@ -276,16 +331,26 @@ int audit_disassembly(const std::string &dis, std::string *report) {
         label_at[it->second] = name;
         preds_of[name].push_back(i);
     }
-    int hazards = 0;
+    int hazards = 0, other = 0;
     std::ostringstream rep;
     for (size_t d = 0; d < ins.size(); d++) {
-        if (!ins[d].dpp) continue;
+        const Insn &D = ins[d];
+        int rules = 0;
+        if (D.dpp) rules |= R_DPP;
+        if (D.valu && !D.trans) rules |= R_TRANS;
+        if (D.vmem) rules |= R_SGPR_VMEM;
+        if (!rules) continue;
         std::string where;
-        const int n = need_ws(ins, preds_of, label_at, d, &where);
-        if (n > 0 && hazards++ < 8) rep << ins[d].mn << " needs " << n << " more wait state(s) after " << where << "; ";
+        const int n = need_ws(ins, preds_of, label_at, d, &where, rules);
+        if (n <= 0) continue;
+        if (D.dpp) hazards++;
+        else other++;
+        if (hazards + other <= 8) rep << D.mn << " needs " << n << " more wait state(s) after " << where << "; ";
     }
-    *report = hazards ? std::to_string(hazards) + " DPP hazard(s): " + rep.str() : "clean";
-    return hazards ? 0 : 1;
+    *report = (hazards || other) ? std::to_string(hazards) + " DPP hazard(s), " + std::to_string(other) +
+                                       " trans-forwarding / SGPR->VMEM hazard(s): " + rep.str()
+                                 : "clean (DPP, trans forwarding, VALU SGPR -> VMEM)";
+    return (hazards || other) ? 0 : 1;
 }
 
 }  // namespace qpb

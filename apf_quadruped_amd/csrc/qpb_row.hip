@@ -116,6 +116,27 @@ struct qpb_args {
 #ifndef QPB_R_ALIAS
 #define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
 #endif
+#ifndef QPB_R_GATHER
+#define QPB_R_GATHER 15   // sparse products with G (and A') as per-lane gathers from the row's LDS vector
+                          // area (one ds_read + one FMA per term of the lane's own row / column) instead
+                          // of one DPP broadcast per column of the pattern's union (qpb_wave.cpp
+                          // row_gather_tables).  Bit mask: 1 the residual products, 2 G'WG's sources,
+                          // 4 the solves' leaf eliminations (G'v, A'yr), 8 the solves' G dx / A dx
+#endif
+#define GR_RES ((QPB_R_GATHER) & 1)
+#define GR_GWG ((QPB_R_GATHER) & 2)
+#define GR_SLV ((QPB_R_GATHER) & 4)
+#define GR_SLX ((QPB_R_GATHER) & 8)
+#ifndef QPB_R_PIVLDS
+#define QPB_R_PIVLDS 1    // the factor keeps no zeroed triangle and no 1/D select per pivot: each
+                          // pivot goes to an LDS slot (1/D re-formed per lane afterwards, the same bits),
+                          // -L goes to LDS under an address mask (strict lower part only; the rest of the
+                          // area stays zero), and both triangular solves read their multipliers there
+#endif
+#ifndef QPB_R_H2
+#define QPB_R_H2 1        // the lookahead pivot D_{k+1} = H(k+1,k+1) - H(k+1,k)^2 / D_k with the square formed
+                          // off the pivot chain (one dependent FMA after 1/D_k instead of a multiply + FMA)
+#endif
 #ifndef QPB_WARM
 #define QPB_WARM 0        // 1: the warm-solve variant (qpb_solve_warm), compiled on demand
 #endif
@@ -360,7 +381,14 @@ static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, doub
 #define OFF_PR EVEN(OFF_T + NX * RS)
 #define OFF_H0 EVEN(OFF_PR + NX * RS)
 #define LOOP_END EVEN(OFF_H0 + NX * RS)
-#define LDS_ROW (LOOP_END > STG_END ? LOOP_END : STG_END)
+// QPB_R_GATHER: the row's vector area (z / w / v at 0..31, y at 32..47, x / dx at 48..63,
+// a zero at 64), after everything else (never overlays the staging)
+#define OFF_VEC (LOOP_END > STG_END ? LOOP_END : STG_END)
+// + QPB_R_PIVLDS: a dump slot at 65 and the pivots D_k at 66..81
+#define LDS_ROW (OFF_VEC + (QPB_R_GATHER || QPB_R_PIVLDS ? 82 : 0))
+#ifndef QPB_R_GATHER_A
+#define QPB_R_GATHER_A (QPB_AX_LEN + 2 <= QPB_AX_UNION)   // y rows' A products gathered when shorter
+#endif
 // QPB_R_SPLIT: per row, the iterate wave 0 forms (x y z0 z1 s0 s1: 6 x 16) and the residuals
 // wave 1 forms (rx ry rz0 rz1 -P x: 5 x 16, the four row sums)
 #define XCH_ROW (6 * 16 + 5 * 16 + 4)
@@ -490,6 +518,38 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     for (int r = 0; r < NZ; r++) nGc[r] = isx ? -Gd[ix * NZ + r] : 0.0;
 #pragma unroll
     for (int l = 0; l < NY1; l++) nAc[l] = (isx && NY > 0) ? -Ad[ix * NY + l] : 0.0;
+#if QPB_R_GATHER || QPB_R_PIVLDS
+    // gathered products: per-lane slot pointers into the vector area and the negated
+    // coefficients of this lane's terms (padding: the zero slot, coefficient 0)
+    double *const Vr = Ls + OFF_VEC;
+    const double *pXT[QPB_XT_LEN > 0 ? QPB_XT_LEN : 1], *pZ0[QPB_ZX0_LEN > 0 ? QPB_ZX0_LEN : 1],
+        *pZ1[QPB_ZX1_LEN > 0 ? QPB_ZX1_LEN : 1], *pAX[QPB_AX_LEN > 0 ? QPB_AX_LEN : 1];
+    double cXT[QPB_XT_LEN > 0 ? QPB_XT_LEN : 1], cZ0[QPB_ZX0_LEN > 0 ? QPB_ZX0_LEN : 1],
+        cZ1[QPB_ZX1_LEN > 0 ? QPB_ZX1_LEN : 1], cAX[QPB_AX_LEN > 0 ? QPB_AX_LEN : 1];
+    {
+        auto load = [&](auto lc, const auto &slot, const auto &src, const double **pp, double *cc) {
+#pragma unroll
+            for (int k = 0; k < decltype(lc)::value; k++) {
+                const int sr = src[c][k];
+                pp[k] = Vr + slot[c][k];
+                cc[k] = sr >= 0 ? -Ls[sr] : 0.0;
+            }
+        };
+        load(qpb_ic<QPB_XT_LEN>{}, qpb_slot_XT, qpb_src_XT, pXT, cXT);
+        load(qpb_ic<QPB_ZX0_LEN>{}, qpb_slot_ZX0, qpb_src_ZX0, pZ0, cZ0);
+        load(qpb_ic<QPB_ZX1_LEN>{}, qpb_slot_ZX1, qpb_src_ZX1, pZ1, cZ1);
+        load(qpb_ic<QPB_AX_LEN>{}, qpb_slot_AX, qpb_src_AX, pAX, cAX);
+        Vr[64] = 0.0;
+    }
+    // sum of a gathered list onto acc (two accumulators)
+    auto gsum = [&](auto lc, double acc, const double *const *pp, const double *cc) -> double {
+        constexpr int L = decltype(lc)::value;
+        double a2[2] = {acc, 0.0};
+#pragma unroll
+        for (int k = 0; k < L; k++) a2[k & 1] = __builtin_fma(cc[k], *pp[k], a2[k & 1]);
+        return L > 1 ? a2[0] + a2[1] : a2[0];
+    };
+#endif
     // H0 = P (upper triangle, symmetrised) + 1e7 A'A (the leaf y rows folded into the x block)
     double nP[NX], H0[NX];
     {
@@ -516,6 +576,13 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
 #pragma unroll
             for (int j = 0; j < NX; j++) { PR[c * RS + j] = nP[j]; H0s[c * RS + j] = H0[j]; }
         }
+#if QPB_R_PIVLDS
+        // the -L area: the factor writes only its strict lower part, the rest stays 0
+        // (the staging it overlays is dead: every static slice was read above)
+#pragma unroll
+        for (int i = 0; i < (NX * RS + 15) / 16; i++)
+            if (c + 16 * i < NX * RS) Tx[c + 16 * i] = 0.0;
+#endif
         qpb_wsync();
     }
 
@@ -529,9 +596,32 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     // -- the same operations as the fast pass otherwise, so the same bits.
     // H = H0 + G' diag(w) G
     auto gwg = [&](double w0, double w1) {
+#if GR_GWG
+        // lane j gathers w_r for the G rows r of its own column and forms -G(r,j) w_r
+        // (XG entries); the update of H(c, j) by row r then broadcasts lane j's entry
+        // for r (position qpb_xtpos[r][j], a compile-time constant) against the lane's
+        // own -G(r, c): += G(r,c) w_r G(r,j), one DPP FMA per structural (r, j)
+        Vr[c] = w0;
+        if constexpr (ZH) Vr[16 + c] = w1;
+        qpb_wsync();
+        double gw[QPB_XG_LEN > 0 ? QPB_XG_LEN : 1];
+#pragma unroll
+        for (int k = 0; k < QPB_XG_LEN; k++) gw[k] = cXT[k] * *pXT[k];
 #pragma unroll
         for (int e = 0; e < NX; e++) H[e] = QPB_R_REGH0 ? H0[e] : H0s[ix * RS + e];
-#if QPB_R_GWG4
+        qpb_for<0, NZ>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            qpb_for<0, NX>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                if constexpr (qpb_Gnz[r][j]) qpb_fxs<j>(H[j], gw[qpb_xtpos[r][j]], nGc[r]);
+            });
+        });
+#else
+#pragma unroll
+        for (int e = 0; e < NX; e++) H[e] = QPB_R_REGH0 ? H0[e] : H0s[ix * RS + e];
+#endif
+#if GR_GWG
+#elif QPB_R_GWG4
         // four rows at a time: the four products -G(r,c) w_r are formed (in their own
         // registers) before any of their DPP FMAs, so no FMA waits out the DPP operand
         // hazard behind the multiply that feeds it, and the rows do not serialise on
@@ -586,7 +676,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 rd = qpb_rcp_piv(dpiv);
             } else {
                 rd = qpb_rcp_nr(dpiv);
-                dmin = __builtin_fmin(dmin, __builtin_fabs(dpiv));
+                if constexpr (!QPB_R_PIVLDS) dmin = __builtin_fmin(dmin, __builtin_fabs(dpiv));
             }
 #if QPB_R_NLFIRST
             // -L(c,k) first: its multiply then sits two instructions ahead of the DPP
@@ -595,11 +685,20 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             double nl = H[k] * -rd;
             asm volatile("" : "+v"(nl));
 #endif
+#if QPB_R_PIVLDS
+            if (c == 0) Vr[66 + k] = dpiv;        // D_k (one lane per row: a loop-invariant exec mask)
+#endif
             if constexpr (k + 1 < NX) {
                 const double h = qpb_nb<k + 1>(H[k]), hkk = qpb_nb<k + 1>(H[k + 1]);
+#if QPB_R_H2
+                dpiv = __builtin_fma(-(h * h), rd, hkk);   // h^2 off the chain: rcp -> 2 Newton FMAs -> this FMA
+#else
                 dpiv = __builtin_fma(h, h * -rd, hkk);
+#endif
             }
+#if !QPB_R_PIVLDS
             rDd = c == k ? rd : rDd;
+#endif
 #if !QPB_R_NLFIRST
             const double nl = H[k] * -rd;        // -L(c,k)
 #endif
@@ -607,8 +706,19 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 constexpr int j = decltype(jc)::value;
                 qpb_fxs<j>(H[j], H[k], nl);        // H(c,j) -= L(c,k) H(j,k)
             });
+#if QPB_R_PIVLDS
+            H[k] = nl;                              // -L(c,k) for c > k (others: masked at the store)
+#else
             H[k] = c > k ? nl : 0.0;
+#endif
         });
+#if QPB_R_PIVLDS
+        // this lane's 1/D: the same function of the same D_c the chain used
+        qpb_wsync();
+        const double dc = Vr[66 + ix];
+        rDd = (REG || !QPB_R_LAZYREG) ? qpb_rcp_piv(dc) : qpb_rcp_nr(dc);
+        if constexpr (!REG && QPB_R_LAZYREG) dmin = isx ? __builtin_fabs(dc) : __builtin_huge_val();
+#endif
         return dmin;
     };
     auto factor_core = [&](double w0, double w1, auto regc) -> double {
@@ -620,10 +730,16 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
         const double dmin = early ? pivots(qpb_ic<0>{}) : factor_core(w0, w1, qpb_ic<0>{});
         if (QPB_R_LAZYREG && qpb_any(dmin <= 1e-14)) factor_core(w0, w1, qpb_ic<1>{});   // wave-uniform, rare
         // column c of -L, contiguous for lane c: Tx[c*NX + k] = -L(k, c)
+#if QPB_R_PIVLDS
+        // strict lower part only (e < c): the rest of the area is 0 from the prologue on
+#pragma unroll
+        for (int e = 0; e < NX; e++) *((isx && e < c) ? &Tx[e * RS + c] : Vr + 65) = H[e];
+#else
         if (isx) {
 #pragma unroll
             for (int e = 0; e < NX; e++) Tx[e * RS + c] = H[e];
         }
+#endif
         qpb_wsync();
     };
 
@@ -631,6 +747,14 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     auto solve = [&](double w0, double w1, double bx, double byv, double bz0, double bz1, double &dx, double &dy,
                      double &dz0, double &dz1) {
         const double v0 = -w0 * bz0, v1 = -w1 * bz1, yr = RDY * byv;   // leaf eliminations
+#if GR_SLV
+        // the leaf rows' values to the vector area; each x lane gathers its G' / A' terms
+        Vr[c] = v0;
+        if constexpr (ZH) Vr[16 + c] = v1;
+        if constexpr (NY > 0) Vr[32 + c] = yr;
+        qpb_wsync();
+        double t = gsum(qpb_ic<QPB_XT_LEN>{}, bx, pXT, cXT);
+#else
         qpb_fence(v0, v1, yr);
         double ta[4] = {bx, 0.0, 0.0, 0.0};
         qpb_for<0, NZ>([&](auto rc) {
@@ -642,7 +766,15 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             qpb_fx<l>(ta[(NZ + l) & 3], yr, nAc[l]);
         });
         double t = (ta[0] + ta[1]) + (ta[2] + ta[3]);
+#endif
+#if QPB_R_PIVLDS
+        double Lf[NX];                              // row c of -L (column c of the area): 0 from k = c on
+#pragma unroll
+        for (int k = 0; k < NX; k++) Lf[k] = Tx[k * RS + ix];
+        qpb_for<0, NX>([&](auto kc) { qpb_fxd<decltype(kc)::value>(t, Lf[decltype(kc)::value]); });
+#else
         qpb_for<0, NX>([&](auto kc) { qpb_fxd<decltype(kc)::value>(t, H[decltype(kc)::value]); });
+#endif
         t *= rDd;
         double Lt[NX];
 #pragma unroll
@@ -652,6 +784,19 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             qpb_fxd<k>(t, Lt[k]);
         });
         dx = t;
+#if GR_SLX
+        // dx to the vector area; z (and y) rows gather their G (A) row terms
+        Vr[48 + c] = t;
+        qpb_wsync();
+        double gy = 0.0;
+        if constexpr (NY > 0 && !QPB_R_GATHER_A) {
+            qpb_fence(t);
+            qpb_for<0, NX>([&](auto jc) { qpb_fx<decltype(jc)::value>(gy, t, nAr[decltype(jc)::value]); });
+        }
+        const double g0 = gsum(qpb_ic<QPB_ZX0_LEN>{}, 0.0, pZ0, cZ0);
+        const double g1 = ZH ? gsum(qpb_ic<QPB_ZX1_LEN>{}, 0.0, pZ1, cZ1) : 0.0;
+        if constexpr (NY > 0 && QPB_R_GATHER_A) gy = gsum(qpb_ic<QPB_AX_LEN>{}, 0.0, pAX, cAX);
+#else
         qpb_fence(t);
         double g0 = 0.0, g1 = 0.0, gy = 0.0;
         qpb_for<0, NX>([&](auto jc) {
@@ -660,6 +805,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             if constexpr (ZH && qpb_ghmask[j]) qpb_fx<j>(g1, t, nGh[j]);
             if constexpr (NY > 0) qpb_fx<j>(gy, t, nAr[j]);
         });
+#endif
         dz0 = -w0 * (bz0 + g0);                   // g = -G dx
         dz1 = -w1 * (bz1 + g1);
         dy = RDY * (byv + gy);
@@ -736,6 +882,25 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             tp = 0.0; ry = by; rz0 = hz0 - s0; rz1 = hz1 - s1;
 #pragma unroll
             for (int j = 0; j < NX; j++) nPr[j] = QPB_R_REGH0 ? nP[j] : PR[ix * RS + j];
+#if GR_RES
+            // x, z, y to the vector area; z (y) rows gather their G (A) row terms, x rows
+            // their G' / A' column terms; -P x (dense) stays a DPP product, issued while
+            // the gathers are in flight
+            Vr[48 + c] = x;
+            Vr[c] = z0;
+            if constexpr (ZH) Vr[16 + c] = z1;
+            if constexpr (NY > 0) Vr[32 + c] = y;
+            qpb_wsync();
+            qpb_for<0, NX>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                if constexpr (NY > 0 && !QPB_R_GATHER_A) qpb_fx<j>(ry, x, nAr[j]);
+                qpb_fx<j>(tp, x, nPr[j]);              // -P x
+            });
+            rz0 = gsum(qpb_ic<QPB_ZX0_LEN>{}, rz0, pZ0, cZ0);
+            if constexpr (ZH) rz1 = gsum(qpb_ic<QPB_ZX1_LEN>{}, rz1, pZ1, cZ1);
+            if constexpr (NY > 0 && QPB_R_GATHER_A) ry = gsum(qpb_ic<QPB_AX_LEN>{}, ry, pAX, cAX);
+            rx = gsum(qpb_ic<QPB_XT_LEN>{}, -cx, pXT, cXT) + tp;
+#else
             qpb_for<0, NX>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 qpb_fx<j>(rz0, x, nGl[j]);
@@ -753,6 +918,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 qpb_fx<l>(ra[(NZ + l) & 3], y, nAc[l]);
             });
             rx = ((ra[0] + ra[1]) + (ra[2] + ra[3])) + tp;
+#endif
             red[0] = isx ? rx * rx : 0.0;
             red[1] = isy ? ry * ry : 0.0;
             red[2] = (isz0 ? rz0 * rz0 : 0.0) + (isz1 ? rz1 * rz1 : 0.0);

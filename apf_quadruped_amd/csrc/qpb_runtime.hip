@@ -401,7 +401,7 @@ int compile_kernel(const std::string &kname, const std::function<std::string()> 
     const Compiler &cc = compiler();
     std::string id = cc.ident;
     for (auto &o : compile_options(exact)) id += " " + o;
-    id += getenv("QPB_NO_ASM_FIXUP") ? " no-dpp-fixup" : " dpp-wait-states-v1";   // qpb_hazard.cpp's rules
+    id += getenv("QPB_NO_ASM_FIXUP") ? " no-dpp-fixup" : " dpp-wait-states-v2";   // qpb_hazard.cpp's rules
     char tag[17];
     snprintf(tag, sizeof tag, "%016llx", (unsigned long long)fnv1a(id));
     const std::string dir = cache_dir();

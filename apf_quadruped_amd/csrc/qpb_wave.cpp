@@ -211,6 +211,95 @@ bool row_eligible(const Plan &pl) {
     return true;
 }
 
+// Gathered sparse products of the row kernel (qpb_row.hip QPB_R_GATHER).  A product
+// with G or A done by DPP broadcasts costs one instruction per column (or row) in the
+// union of the pattern -- G's 20 x 12 with 36 non-zeros takes 20 broadcasts for G'z
+// and 12 for G x, each useful in the 2-3 lanes whose coefficient is non-zero.  Done as
+// gathers, lane c reads exactly the vector entries its own row / column needs from the
+// row's LDS vector area (one ds_read_b64 each, lane-dependent slot) and issues one FMA
+// per term: the count is the longest list, not the union.  Per lane c (tables [16][len],
+// padded with the zero slot):
+//   XT: x row c's G'- then A'-column terms: G rows r with G(r,c) != 0 (first XG entries;
+//       z slot r), then A rows l with A(l,c) != 0 (y slot 32 + l);
+//   ZX0 / ZX1: z row c / 16 + c's G-row terms (x slot 48 + j);  AX: y row c's A-row terms.
+// Each term: its slot and the index of its coefficient in the staged dense matrices
+// (Ls: P at 0, A at n*n, G at n*n + max(p,1)*n, column-major), -1 for padding.
+// qpb_xtpos[r][j]: where G row r sits in lane j's XT list (the G'WG update's source).
+static void row_gather_tables(std::ostringstream &o, const Plan &pl, const std::vector<std::vector<int>> &gnz) {
+    const long n = pl.n, m = pl.m, p = pl.p;
+    const long off_a = n * n, off_g = off_a + std::max(p, 1L) * n;
+    std::vector<std::vector<int>> anz(std::max(p, 1L), std::vector<int>(n, 0));
+    for (long j = 0; j < n && p > 0; j++)
+        for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++) anz[pl.A.ir[k]][j] = 1;
+    const int kZero = 64;
+    typedef std::vector<std::pair<int, int>> Terms;
+    std::vector<Terms> xg(16), xa(16), zx0(16), zx1(16), ax(16);
+    for (long c = 0; c < 16; c++) {
+        if (c < n) {
+            for (long r = 0; r < m; r++)
+                if (gnz[r][c]) xg[c].push_back({(int)r, (int)(off_g + c * m + r)});
+            for (long l = 0; l < p; l++)
+                if (anz[l][c]) xa[c].push_back({(int)(32 + l), (int)(off_a + c * p + l)});
+        }
+        for (long j = 0; j < n; j++) {
+            if (c < m && gnz[c][j]) zx0[c].push_back({(int)(48 + j), (int)(off_g + j * m + c)});
+            if (16 + c < m && gnz[16 + c][j]) zx1[c].push_back({(int)(48 + j), (int)(off_g + j * m + 16 + c)});
+            if (c < p && anz[c][j]) ax[c].push_back({(int)(48 + j), (int)(off_a + j * p + c)});
+        }
+    }
+    auto len = [](const std::vector<Terms> &t) {
+        size_t k = 0;
+        for (auto &v : t) k = std::max(k, v.size());
+        return (long)k;
+    };
+    const long XG = len(xg), XA = len(xa);
+    std::vector<Terms> xt(16);
+    for (int c = 0; c < 16; c++) {
+        xt[c] = xg[c];
+        xt[c].resize((size_t)XG, {kZero, -1});
+        xt[c].insert(xt[c].end(), xa[c].begin(), xa[c].end());
+    }
+    auto emit = [&](const char *nm, std::vector<Terms> t, long L) {
+        o << "#define QPB_" << nm << "_LEN " << L << "\n";
+        const long Lp = std::max(L, 1L);
+        for (int which = 0; which < 2; which++) {
+            o << "static __device__ const int qpb_" << (which ? "src_" : "slot_") << nm << "[16][" << Lp << "] = {";
+            for (int c = 0; c < 16; c++) {
+                t[c].resize((size_t)Lp, {kZero, -1});
+                o << (c ? "," : "") << "{";
+                for (long k = 0; k < Lp; k++) o << (k ? "," : "") << (which ? t[c][k].second : t[c][k].first);
+                o << "}";
+            }
+            o << "};\n";
+        }
+    };
+    o << "#define QPB_XG_LEN " << XG << "\n";
+    emit("XT", xt, XG + XA);
+    emit("ZX0", zx0, len(zx0));
+    emit("ZX1", zx1, len(zx1));
+    emit("AX", ax, len(ax));
+    o << "static constexpr int qpb_xtpos[" << m << "][" << n << "] = {";
+    for (long r = 0; r < m; r++) {
+        o << (r ? "," : "") << "{";
+        for (long j = 0; j < n; j++) {
+            int pos = -1;
+            for (size_t k = 0; k < xg[j].size(); k++)
+                if (xg[j][k].first == r) pos = (int)k;
+            o << (j ? "," : "") << pos;
+        }
+        o << "}";
+    }
+    o << "};\n";
+    // unions of the DPP forms (what the gathers replace), for the generator's choice
+    long ucol = 0;
+    for (long j = 0; j < n; j++) {
+        int any = 0;
+        for (long l = 0; l < p; l++) any |= anz[l][j];
+        ucol += any;
+    }
+    o << "#define QPB_AX_UNION " << ucol << "\n";
+}
+
 // plan-specific prefix of the row kernel (sizes, scatter tables, G pattern)
 static std::string row_prefix(const Plan &pl) {
     const long n = pl.n, m = pl.m;
@@ -235,6 +324,7 @@ static std::string row_prefix(const Plan &pl) {
         o << (j ? "," : "") << any;
     }
     o << "};\n";
+    row_gather_tables(o, pl, gnz);
     return o.str();
 }
 
@@ -265,7 +355,9 @@ std::string generate_row_group_kernel(const std::vector<const Plan *> &pls, std:
     o << "#define QPB_GROUP 1\n#define QPB_ROW_COMMON_ONLY 1\n" << kRowTemplate << "\n#undef QPB_ROW_COMMON_ONLY\n";
     static const char *undef[] = {"QPB_NX", "QPB_NZ", "QPB_NY", "QPB_WG", "QPB_NNZP", "QPB_NNZA", "QPB_NNZG",
                                   "NX", "NZ", "NY", "NY1", "WPB", "ZH", "EVEN", "OFF_A", "OFF_G", "OFF_T",
-                                  "OFF_PR", "OFF_H0", "LDS_ROW", "STG_END", "LOOP_END"};
+                                  "OFF_PR", "OFF_H0", "LDS_ROW", "STG_END", "LOOP_END", "OFF_VEC",
+                                  "QPB_XG_LEN", "QPB_XT_LEN", "QPB_ZX0_LEN", "QPB_ZX1_LEN", "QPB_AX_LEN",
+                                  "QPB_AX_UNION", "QPB_R_GATHER_A"};
     for (size_t i = 0; i < pls.size(); i++) {
         o << "namespace qpb_g" << i << " {\n" << row_prefix(*pls[i]) << kRowTemplate
           << "\nstatic constexpr long qpb_lds_doubles = 4 * LDS_ROW;\n}  // namespace qpb_g" << i << "\n";

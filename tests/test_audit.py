@@ -88,3 +88,54 @@ def test_cached_dpp_kernels_were_audited():
         assert rec.endswith("clean") or "rebuilt with QPB_DPP_NOP=2" in rec, (f, rec)
         r, rep = _audit(open(f, "rb").read())
         assert r == 1 or "rebuilt" in rec, (f, rep)
+
+
+TRANS_SNIPPET = r"""
+#include <hip/hip_runtime.h>
+extern "C" __global__ void k(double *p) {
+    double a = p[threadIdx.x], b;
+    asm volatile("v_rcp_f64 %0, %1\n\t" PAD "v_add_f64 %0, %0, %1" : "=&v"(b) : "v"(a));
+    p[threadIdx.x] = b;
+}
+"""
+SGPR_SNIPPET = r"""
+#include <hip/hip_runtime.h>
+extern "C" __global__ void k(unsigned *p) {
+    unsigned v, lo = (unsigned)(size_t)p + threadIdx.x;   // (compiled and audited, never run)
+    asm volatile("v_readfirstlane_b32 s60, %1\n\tv_mov_b32 %0, 0\n\ts_mov_b32 s61, 0\n\t" PAD
+                 "global_load_dword %0, %0, s[60:61]\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(lo) : "s60", "s61");
+    p[threadIdx.x] = v;
+}
+"""
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="ROCm clang not present")
+@pytest.mark.parametrize("snippet,pad,expect", [(TRANS_SNIPPET, "", 0), (TRANS_SNIPPET, "s_nop 0\\n\\t", 1),
+                                                (SGPR_SNIPPET, "", 0), (SGPR_SNIPPET, "s_nop 2\\n\\t", 1)])
+def test_audit_flags_trans_forwarding_and_valu_sgpr_to_vmem(tmp_path, snippet, pad, expect):
+    """Two more gfx950 hazard classes the audit checks on every instruction: a VALU
+    reading a transcendental's result with no wait state between (trans forwarding,
+    1 wait state), and a VMEM instruction whose SGPR base a VALU wrote within 5 wait
+    states (v_readfirstlane -> global_load saddr)."""
+    src = tmp_path / "k.hip"
+    src.write_text(snippet.replace("PAD", f'"{pad}"'))
+    co = tmp_path / "k.co"
+    subprocess.run([CLANG, "-x", "hip", "--cuda-device-only", "--no-gpu-bundle-output", "--offload-arch=gfx950",
+                    "-O3", "-o", str(co), str(src)], check=True)
+    r, rep = _audit(co.read_bytes())
+    assert r == expect, rep
+
+
+def test_audit_clean_on_every_cached_kernel():
+    """Every code object in the in-tree cache passes all three hazard classes
+    (DPP operands / EXEC, trans forwarding, VALU SGPR -> VMEM) -- including the
+    compiler-generated code around the asm."""
+    objs = sorted(glob.glob(os.path.join(ROOT, "apf_quadruped_amd", "kcache", "*.hsaco")))
+    if not objs:
+        pytest.skip("no cached kernels (run __graft_entry__.build())")
+    bad = []
+    for f in objs[:400]:
+        r, rep = _audit(open(f, "rb").read())
+        if r == 0:
+            bad.append((os.path.basename(f), rep))
+    assert not bad, bad[:3]
