@@ -117,21 +117,33 @@ struct qpb_args {
 #define QPB_R_ALIAS 1     // the iteration's LDS areas overlay the staging area (half the LDS per QP)
 #endif
 #ifndef QPB_R_GATHER
-#define QPB_R_GATHER 15   // sparse products with G (and A') as per-lane gathers from the row's LDS vector
+#define QPB_R_GATHER 0    // sparse products with G (and A') as per-lane gathers from the row's LDS vector
                           // area (one ds_read + one FMA per term of the lane's own row / column) instead
                           // of one DPP broadcast per column of the pattern's union (qpb_wave.cpp
                           // row_gather_tables).  Bit mask: 1 the residual products, 2 G'WG's sources,
-                          // 4 the solves' leaf eliminations (G'v, A'yr), 8 the solves' G dx / A dx
+                          // 4 the solves' leaf eliminations (G'v, A'yr), 8 the solves' G dx / A dx.
+                          // Off: measured slower everywhere (profiles/r05_row_gather_ab.jsonl, DESIGN
+                          // §4c round 5) -- 18 % fewer VALU instructions per pass, but every gather is an
+                          // LDS round trip on the chain (1 024 QPs: 29.5 -> 32.1 us), and at 2^20 QPs the
+                          // CU's one LDS pipe serves four SIMDs: 3.58 -> 3.88 ms
 #endif
 #define GR_RES ((QPB_R_GATHER) & 1)
 #define GR_GWG ((QPB_R_GATHER) & 2)
 #define GR_SLV ((QPB_R_GATHER) & 4)
 #define GR_SLX ((QPB_R_GATHER) & 8)
 #ifndef QPB_R_PIVLDS
-#define QPB_R_PIVLDS 1    // the factor keeps no zeroed triangle and no 1/D select per pivot: each
-                          // pivot goes to an LDS slot (1/D re-formed per lane afterwards, the same bits),
-                          // -L goes to LDS under an address mask (strict lower part only; the rest of the
-                          // area stays zero), and both triangular solves read their multipliers there
+#define QPB_R_PIVLDS 0    // the factor keeps no zeroed triangle and no 1/D select per pivot: each pivot
+                          // goes to an LDS slot (1/D re-formed per lane afterwards, the same bits), -L goes
+                          // to LDS under an address mask (strict lower part only; the rest of the area
+                          // stays zero), and both triangular solves read their multipliers there.  -48
+                          // VALU instructions per factor, but two more LDS round trips per pass: 1 024 QPs
+                          // 29.5 -> 30.2 us, 2^20 unchanged (profiles/r05_row_gather_ab.jsonl); off
+#endif
+#ifndef QPB_R_RDLDS
+#define QPB_R_RDLDS 0     // each pivot D_k to an LDS slot (one store per pivot) and 1/D per lane re-formed
+                          // from its own D_c after the factor (the same bits) -- no 64-bit select per
+                          // pivot; the lazy regularisation check reads the same slots (QPB_R_PIVLDS does
+                          // this too, with the -L store masked and the solves reading -L from LDS)
 #endif
 #ifndef QPB_R_H2
 #define QPB_R_H2 1        // the lookahead pivot D_{k+1} = H(k+1,k+1) - H(k+1,k)^2 / D_k with the square formed
@@ -385,7 +397,7 @@ static __device__ __forceinline__ void qpb_argmin_arrive(const qpb_args &a, doub
 // a zero at 64), after everything else (never overlays the staging)
 #define OFF_VEC (LOOP_END > STG_END ? LOOP_END : STG_END)
 // + QPB_R_PIVLDS: a dump slot at 65 and the pivots D_k at 66..81
-#define LDS_ROW (OFF_VEC + (QPB_R_GATHER || QPB_R_PIVLDS ? 82 : 0))
+#define LDS_ROW (OFF_VEC + (QPB_R_GATHER || QPB_R_PIVLDS || QPB_R_RDLDS ? 82 : 0))
 #ifndef QPB_R_GATHER_A
 #define QPB_R_GATHER_A (QPB_AX_LEN + 2 <= QPB_AX_UNION)   // y rows' A products gathered when shorter
 #endif
@@ -518,7 +530,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     for (int r = 0; r < NZ; r++) nGc[r] = isx ? -Gd[ix * NZ + r] : 0.0;
 #pragma unroll
     for (int l = 0; l < NY1; l++) nAc[l] = (isx && NY > 0) ? -Ad[ix * NY + l] : 0.0;
-#if QPB_R_GATHER || QPB_R_PIVLDS
+#if QPB_R_GATHER || QPB_R_PIVLDS || QPB_R_RDLDS
     // gathered products: per-lane slot pointers into the vector area and the negated
     // coefficients of this lane's terms (padding: the zero slot, coefficient 0)
     double *const Vr = Ls + OFF_VEC;
@@ -676,7 +688,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 rd = qpb_rcp_piv(dpiv);
             } else {
                 rd = qpb_rcp_nr(dpiv);
-                if constexpr (!QPB_R_PIVLDS) dmin = __builtin_fmin(dmin, __builtin_fabs(dpiv));
+                if constexpr (!QPB_R_PIVLDS && !QPB_R_RDLDS) dmin = __builtin_fmin(dmin, __builtin_fabs(dpiv));
             }
 #if QPB_R_NLFIRST
             // -L(c,k) first: its multiply then sits two instructions ahead of the DPP
@@ -685,7 +697,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             double nl = H[k] * -rd;
             asm volatile("" : "+v"(nl));
 #endif
-#if QPB_R_PIVLDS
+#if QPB_R_PIVLDS || QPB_R_RDLDS
             if (c == 0) Vr[66 + k] = dpiv;        // D_k (one lane per row: a loop-invariant exec mask)
 #endif
             if constexpr (k + 1 < NX) {
@@ -696,7 +708,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
                 dpiv = __builtin_fma(h, h * -rd, hkk);
 #endif
             }
-#if !QPB_R_PIVLDS
+#if !QPB_R_PIVLDS && !QPB_R_RDLDS
             rDd = c == k ? rd : rDd;
 #endif
 #if !QPB_R_NLFIRST
@@ -712,7 +724,7 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
             H[k] = c > k ? nl : 0.0;
 #endif
         });
-#if QPB_R_PIVLDS
+#if QPB_R_PIVLDS || QPB_R_RDLDS
         // this lane's 1/D: the same function of the same D_c the chain used
         qpb_wsync();
         const double dc = Vr[66 + ix];
