@@ -26,12 +26,12 @@ QPB_P_FULL, QPB_P_UPPER, QPB_EXACT = 0x0, 0x1, 0x10
 # else minimum degree), "amd" (the reference's AMD: what qpSWIFT computes for
 # Permut = NULL, qpSWIFT.c:424-440), "mindeg", "leaves"
 ORDER_FLAGS = {"own": 0x0, "amd": 0x20, "mindeg": 0x40, "leaves": 0x80}
-QPB_KERNEL_LANE, QPB_KERNEL_WAVE, QPB_KERNEL_NOROW, QPB_KERNEL_TREE = 0x100, 0x200, 0x400, 0x800
+QPB_KERNEL_LANE, QPB_KERNEL_WAVE, QPB_KERNEL_NOROW, QPB_KERNEL_TREE, QPB_KERNEL_BAND = 0x100, 0x200, 0x400, 0x800, 0x1000
 # "wave" = the wave kernel in the form the plan picks (row form: four QPs per
 # wavefront, where it fits); "wave1" = one QP per wavefront regardless
 KERNEL_FLAGS = {"auto": 0, "lane": QPB_KERNEL_LANE, "wave": QPB_KERNEL_WAVE,
                 "wave1": QPB_KERNEL_WAVE | QPB_KERNEL_NOROW, "auto1": QPB_KERNEL_NOROW,
-                "tree": QPB_KERNEL_TREE}
+                "tree": QPB_KERNEL_TREE, "band": QPB_KERNEL_BAND}
 QP_OPTIMAL, QP_KKTFAIL, QP_MAXIT, QP_FATAL = 0, 1, 2, 3
 
 
@@ -155,7 +155,7 @@ class Plan:
         i = self.info
         if i.wave_ok and (i.wave_max_batch < 0 or B <= i.wave_max_batch):
             return "wave"
-        return {1: "lane", 2: "wave", 3: "tree"}[i.large_kernel]
+        return {1: "lane", 2: "wave", 3: "tree", 4: "band"}[i.large_kernel]
 
     def oracle_perm(self, B: int) -> np.ndarray:
         """The KKT permutation the kernels factor with (both kernels follow the

@@ -94,6 +94,36 @@ std::vector<long> min_degree_order(const Pattern &sym) {
     return order;
 }
 
+void band_shape(Plan &pl) {
+    pl.band_nb = pl.band_ns = pl.band_mz = pl.band_my = 0;
+    const long n = pl.n, m = pl.m, p = pl.p;
+    std::vector<long> gcnt(m, 0);
+    for (long k = 0; k < pl.G.nnz(); k++) gcnt[pl.G.ir[k]]++;
+    for (long r = 0; r < m; r++)
+        if (!gcnt[r]) return;
+    for (long nb = 1; nb <= 16; nb++) {
+        if (n % nb) continue;
+        const long ns = n / nb;
+        if (ns < 2 || m % ns || p % ns) continue;
+        const long mz = m / ns, my = p / ns;
+        if (mz > 64 || my > 64) continue;
+        bool ok = true;
+        for (long j = 0; j < n && ok; j++) {
+            const long sj = j / nb;
+            for (long k = pl.Pf.jc[j]; k < pl.Pf.jc[j + 1] && ok; k++) ok = pl.Pf.ir[k] / nb == sj;
+            for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1] && ok; k++) ok = pl.G.ir[k] / mz == sj;
+            if (p > 0)
+                for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1] && ok; k++) {
+                    const long sl = pl.A.ir[k] / my;
+                    ok = sl == sj || sl == sj + 1;
+                }
+        }
+        if (!ok) continue;
+        pl.band_nb = (int)nb; pl.band_ns = (int)ns; pl.band_mz = (int)mz; pl.band_my = (int)my;
+        return;
+    }
+}
+
 int build_plan(Plan &pl, long n, long m, long p, int pmode,
                const long *Pjc, const long *Pir,
                const long *Ajc, const long *Air,
@@ -135,6 +165,7 @@ int build_plan(Plan &pl, long n, long m, long p, int pmode,
         }
     }
     if (p > 0) transpose_src(pl.A, pl.At, pl.At_src);
+    band_shape(pl);
     transpose_src(pl.G, pl.Gt, pl.Gt_src);
 
     // KKT assembly with sources, Auxilary.c:71-181.
@@ -187,7 +218,11 @@ int build_plan(Plan &pl, long n, long m, long p, int pmode,
         // dense block (one row per lane): the row kernel for the contact-force
         // shapes, a 30-row dense block instead of AMD's 45-51 for the controller
         // shapes; minimum degree beyond (MPC horizon: the tree kernel)
-        if (order == ORDER_OWN) order = (n <= 64 && p <= 64 && m <= 256) ? ORDER_LEAVES : ORDER_MINDEG;
+        // own ordering: leaves first wherever the x block fits the wave kernel's
+        // dense block, and for multi-stage patterns (the band kernel eliminates the
+        // z / y leaves, then the block-tridiagonal x block stage by stage)
+        if (order == ORDER_OWN)
+            order = ((n <= 64 && p <= 64 && m <= 256) || pl.band_nb > 0) ? ORDER_LEAVES : ORDER_MINDEG;
         if (order == ORDER_LEAVES) {
             // z rows, y rows, then x in natural order.  Every z / y row is then a
             // leaf (its neighbours are x rows, all later) and the x block is dense --

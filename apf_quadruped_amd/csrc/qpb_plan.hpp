@@ -59,7 +59,8 @@ enum Ordering : int {
     ORDER_AMD = 2,      // the reference's AMD (amd_l_order with amd_l_defaults): Permut = NULL
     ORDER_LEAVES = 3,   // own: z rows, y rows, then x in natural order (small QPs)
     ORDER_OWN = 4,      // request only: ORDER_LEAVES for n, p <= 64, m <= 256 (the wave kernel's
-                        // range: its dense block is then the x block), else ORDER_MINDEG.  A plan
+                        // range: its dense block is then the x block) and for multi-stage patterns
+                        // (band_shape: the band kernel's elimination), else ORDER_MINDEG.  A plan
                         // in that range that a large batch sends to the lane or tree kernel also
                         // gets the dense x block (more fill than minimum degree; not measured)
 };
@@ -87,6 +88,10 @@ struct Plan {
     std::vector<long> perm, pinv, parent, Lp, Li;
     long lnz = 0;
     int ordering_kind = 0;                   // ORDER_* below: how perm was chosen
+    // multi-stage (block-tridiagonal) structure, 0 if none: x, z, y split into band_ns
+    // stages of band_nb / band_mz / band_my rows with P block diagonal, G row group k on
+    // stage k, A row group k on stages k-1 and k (band_shape; the band kernel, qpb_band.hip)
+    int band_nb = 0, band_ns = 0, band_mz = 0, band_my = 0;
     std::vector<FacStep> fac;                // numeric schedule
     long fac_updates = 0, fac_divs = 0;      // op counts (flop accounting)
     uint64_t hash = 0;
@@ -112,6 +117,12 @@ int build_plan(Plan &pl, long n, long m, long p, int pmode,
                const long *Ajc, const long *Air,
                const long *Gjc, const long *Gir,
                const long *perm, std::string *err, int order = ORDER_OWN);
+
+// Multi-stage structure of the plan's P / A / G patterns (fills pl.band_*): the
+// smallest stage width NB <= 16 with n = NB NS, m = MZ NS, p = MY NS (NS >= 2,
+// MZ <= 64, MY <= 64), every P entry inside a stage block, G row r on stage r / MZ
+// only, A row l on stages l / MY - 1 and l / MY only, and no empty G row.
+void band_shape(Plan &pl);
 
 // Minimum-degree ordering of a symmetric pattern (own implementation; ties go
 // to the lowest index).  Exposed for tests.

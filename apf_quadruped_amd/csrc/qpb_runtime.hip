@@ -521,6 +521,27 @@ int compile_tree(qpb_plan *plan) {
                           false, &plan->tree_code);
 }
 
+bool band_auto() {
+    static const bool on = [] { const char *e = getenv("QPB_BAND"); return !(e && atoi(e) == 0); }();
+    return on;
+}
+
+// the kernel a solve of B QPs runs: wave (row) form, band, tree, else the lane kernel
+Pick pick_kernel(const qpb_plan *plan, long B, bool warm) {
+    Pick k;
+    const int pref = plan->kernel_pref;
+    k.wave = plan->wave_ok && (pref == 2 || (pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
+    k.band = !k.wave && !warm && plan->band_ok && (pref == 4 || (pref == 0 && plan->large_tree && band_auto()));
+    k.tree = !k.wave && !k.band && (pref == 3 || ((pref == 0 || pref == 4) && plan->large_tree));
+    return k;
+}
+
+int compile_band(qpb_plan *plan) {
+    if (!plan->band_ok) return fail(QPB_EINVAL, "plan is not eligible for the band kernel");
+    return compile_kernel(plan->band_kname, [plan] { return generate_band_kernel(plan->pl, nullptr); }, false,
+                          &plan->band_code);
+}
+
 int compile_tree2(qpb_plan *plan) {
     if (plan->tree_occ_batch < 0) return fail(QPB_EINVAL, "plan has no large-batch tree kernel");
     return compile_kernel(plan->tree2_kname, [plan] { return generate_tree_kernel(plan->pl, plan->tree2_wg, nullptr); },
@@ -705,7 +726,8 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
     // from the reference's), for plans whose KKT has the z/y-leaf structure
     std::string why;
     plan->wave_ok = !plan->gen.exact && qpb::wave_eligible(plan->pl, &why);
-    plan->kernel_pref = (flags & QPB_KERNEL_TREE) ? 3 : (flags & QPB_KERNEL_WAVE) ? 2 : (flags & QPB_KERNEL_LANE) ? 1 : 0;
+    plan->kernel_pref = (flags & QPB_KERNEL_BAND) ? 4 : (flags & QPB_KERNEL_TREE) ? 3 : (flags & QPB_KERNEL_WAVE) ? 2
+                      : (flags & QPB_KERNEL_LANE) ? 1 : 0;
     if (plan->kernel_pref == 2 && !plan->wave_ok)
         return fail(QPB_EINVAL, "QPB_KERNEL_WAVE: " + (plan->gen.exact ? std::string("exact plans use the lane kernel") : why));
     // tree kernel (one QP per workgroup, level-scheduled sparse LDL'): any
@@ -733,6 +755,13 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
             }
         }
     }
+    // band kernel (multi-stage patterns in leaves-first order, cold solves): auto
+    // dispatch takes it where the tree kernel would run (QPB_BAND=0: the tree kernel)
+    std::string why_band;
+    plan->band_ok = !plan->gen.exact && qpb::band_eligible(plan->pl, &why_band);
+    if (plan->kernel_pref == 4 && !plan->band_ok)
+        return fail(QPB_EINVAL, "QPB_KERNEL_BAND: " + (plan->gen.exact ? std::string("exact plans use the lane kernel") : why_band));
+    if (plan->band_ok) qpb::generate_band_kernel(plan->pl, &plan->band_kname);
     plan->wave_max_batch = 4096;   // measured crossover vs the lane kernel
     if (plan->wave_ok) {
         // row form (four QPs per wavefront, all exchanges DPP) where the plan fits
@@ -786,10 +815,11 @@ int qpb_plan_get_info(const qpb_plan *plan, qpb_plan_info *info) {
     info->ordering = pl.ordering_kind; info->exact = plan->gen.exact ? 1 : 0;
     info->hash = pl.hash;
     info->wave_ok = plan->wave_ok ? 1 : 0;
-    info->wave_max_batch = (plan->kernel_pref == 1 || plan->kernel_pref == 3) ? 0 : plan->kernel_pref == 2 ? -1 : plan->wave_max_batch;
+    info->wave_max_batch = (plan->kernel_pref == 1 || plan->kernel_pref == 3 || plan->kernel_pref == 4) ? 0 : plan->kernel_pref == 2 ? -1 : plan->wave_max_batch;
     info->wave_qpw = plan->wave_qpw;
     info->tree_ok = plan->tree_ok ? 1 : 0;
-    info->large_kernel = plan->kernel_pref == 3 ? 3 : plan->kernel_pref == 2 ? 2 : plan->kernel_pref == 1 ? 1
+    info->large_kernel = qpb::pick_kernel(plan, 1L << 20, false).band ? 4
+                       : plan->kernel_pref == 3 ? 3 : plan->kernel_pref == 2 ? 2 : plan->kernel_pref == 1 ? 1
                        : plan->large_tree ? 3 : 1;
     return QPB_OK;
 }
@@ -843,10 +873,9 @@ long qpb_plan_wave_source(const qpb_plan *plan, char *buf, long cap) {
 
 long qpb_plan_kernel_name(const qpb_plan *plan, long B, char *buf, long cap) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
-    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
-                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
-    const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
-    const std::string &s = wave ? (plan->row_occ_batch >= 0 && B > plan->row_occ_batch ? plan->row2_kname
+    const qpb::Pick pk = qpb::pick_kernel(plan, B, false);
+    const bool wave = pk.wave, tree = pk.tree;
+    const std::string &s = pk.band ? plan->band_kname : wave ? (plan->row_occ_batch >= 0 && B > plan->row_occ_batch ? plan->row2_kname
                                    : plan->row_split ? plan->rowsplit_kname : plan->wave_kname)
                          : tree ? (plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch ? plan->tree2_kname : plan->tree_kname)
                                 : plan->kname;
@@ -861,9 +890,8 @@ long qpb_plan_kernel_name(const qpb_plan *plan, long B, char *buf, long cap) {
 int qpb_plan_compile_warm(qpb_plan *plan, long B) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     if (B < 1) B = 1;
-    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
-                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
-    const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
+    const qpb::Pick pk = qpb::pick_kernel(plan, B, true);
+    const bool wave = pk.wave, tree = pk.tree;
     const bool row2 = wave && plan->row_occ_batch >= 0 && B > plan->row_occ_batch;
     const bool tree2 = tree && plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch;
     const std::string &kn = row2 ? plan->row2_kname : wave ? plan->wave_kname : tree2 ? plan->tree2_kname
@@ -899,6 +927,7 @@ int qpb_plan_compile(qpb_plan *plan) {
     if (!rc && plan->tree_ok && (k == 3 || (k == 0 && plan->large_tree))) rc = qpb::compile_tree(plan);
     if (!rc && plan->tree_ok && (k == 3 || (k == 0 && plan->large_tree)) && plan->tree_occ_batch >= 0)
         rc = qpb::compile_tree2(plan);
+    if (!rc && plan->band_ok && (k == 4 || (k == 0 && plan->large_tree && qpb::band_auto()))) rc = qpb::compile_band(plan);
     return rc;
 }
 
@@ -920,18 +949,19 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
     // and wins while the batch does not fill the GPU with lane-kernel waves
     // beyond it: the lane kernel (one QP per lane) for small KKT systems, the tree
     // kernel (one QP per workgroup) for large ones
-    const bool wave = plan->wave_ok && (plan->kernel_pref == 2 ||
-                                        (plan->kernel_pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
-    const bool tree = !wave && (plan->kernel_pref == 3 || (plan->kernel_pref == 0 && plan->large_tree));
+    const qpb::Pick pk = qpb::pick_kernel(plan, B, warm);
+    const bool wave = pk.wave, tree = pk.tree, band = pk.band;
     hipFunction_t fn;
     const bool row2 = wave && plan->row_occ_batch >= 0 && B > plan->row_occ_batch;
     const bool tree2 = tree && plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch;
     const bool split = wave && !row2 && !warm && plan->row_split;      // cold batched solves only
     int rc;
     if (!warm) {
-        rc = split ? qpb::compile_rowsplit(plan) : row2 ? qpb::compile_row2(plan) : wave ? qpb::compile_wave(plan)
-           : tree2 ? qpb::compile_tree2(plan) : tree ? qpb::compile_tree(plan) : qpb::compile_plan(plan);
-        if (!rc) rc = split ? qpb::load_function(plan->rowsplit_kname, plan->rowsplit_code, &fn)
+        rc = band ? qpb::compile_band(plan) : split ? qpb::compile_rowsplit(plan) : row2 ? qpb::compile_row2(plan)
+           : wave ? qpb::compile_wave(plan) : tree2 ? qpb::compile_tree2(plan) : tree ? qpb::compile_tree(plan)
+           : qpb::compile_plan(plan);
+        if (!rc) rc = band ? qpb::load_function(plan->band_kname, plan->band_code, &fn)
+                    : split ? qpb::load_function(plan->rowsplit_kname, plan->rowsplit_code, &fn)
                     : row2 ? qpb::load_function(plan->row2_kname, plan->row2_code, &fn)
                     : wave ? qpb::load_function(plan->wave_kname, plan->wave_code, &fn)
                     : tree2 ? qpb::load_function(plan->tree2_kname, plan->tree2_code, &fn)
@@ -974,11 +1004,11 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
     // and the gap between two dependent launches; up to 4 096 waves
     bool fused = false;
     void *params[] = {&a};
-    const unsigned wg = (unsigned)(split ? 128 : wave ? plan->wave_wg : tree2 ? plan->tree2_wg : tree ? plan->tree_wg
-                                                                  : plan->gen.wg);
-    const long per_block = split ? 4 : wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup
+    const unsigned wg = (unsigned)(band ? 64 : split ? 128 : wave ? plan->wave_wg : tree2 ? plan->tree2_wg
+                                   : tree ? plan->tree_wg : plan->gen.wg);
+    const long per_block = band ? 1 : split ? 4 : wave ? (wg / 64) * plan->wave_qpw : tree ? 1 : wg;    // QPs per workgroup
     unsigned grid = (unsigned)((B + per_block - 1) / per_block);
-    if (wave || tree) grid = (grid + 7) & ~7u;      // XCD-aware block order (qpb_xcd_block)
+    if (wave || tree || band) grid = (grid + 7) & ~7u;      // XCD-aware block order (qpb_xcd_block)
     if (best && wave && plan->wave_qpw == 4 && !getenv("QPB_NO_FUSED_ARGMIN")) {
         const long nw = (long)grid * (wg / 64);
         if (nw <= 4096) {

@@ -19,7 +19,7 @@ struct qpb_plan {
     int wave_wg = 256;
     int wave_qpw = 1;                           // QPs per wavefront: 1 wave form, 4 row form
     long wave_max_batch = 0;                    // auto: wave kernel for B <= this
-    int kernel_pref = 0;                        // 0 auto, 1 lane only, 2 wave only
+    int kernel_pref = 0;                        // 0 auto, 1 lane only, 2 wave only, 3 tree, 4 band
     std::string wave_kname;
     std::shared_ptr<std::vector<char>> wave_code;
     // row form for large batches: the same kernel allocated for two waves per SIMD
@@ -32,6 +32,10 @@ struct qpb_plan {
     bool row_split = false;
     std::string rowsplit_kname;
     std::shared_ptr<std::vector<char>> rowsplit_code;
+    // band kernel (one QP per wavefront, multi-stage patterns): cold solves only
+    bool band_ok = false;
+    std::string band_kname;
+    std::shared_ptr<std::vector<char>> band_code;
     bool tree_ok = false;                       // tree kernel (one QP per workgroup, any pattern)
     bool large_tree = false;                    // auto: tree (not lane) kernel beyond the wave kernel's range
     int tree_wg = 256;
@@ -73,6 +77,10 @@ int compile_wave(qpb_plan *plan);
 int compile_row2(qpb_plan *plan);
 int compile_rowsplit(qpb_plan *plan);
 int compile_tree2(qpb_plan *plan);
+int compile_band(qpb_plan *plan);
+struct Pick { bool wave = false, band = false, tree = false; };   // neither: the lane kernel
+Pick pick_kernel(const qpb_plan *plan, long B, bool warm);
+bool band_auto();
 int compile_tree(qpb_plan *plan);
 int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
                  std::shared_ptr<std::vector<char>> **slot);

@@ -23,6 +23,9 @@ const char *kWaveTemplate =
 const char *kRowTemplate =
 #include "qpb_row_src.inc"
     ;
+const char *kBandTemplate =
+#include "qpb_band_src.inc"
+    ;
 
 template <class F>
 void table(std::ostringstream &o, const char *decl, long cnt, F f) {
@@ -508,6 +511,130 @@ std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out) 
     o << "};\n";
     const std::string body = o.str() + kWaveTemplate;
     const std::string name = named(body, "qpb_wave", pl, wg);
+    if (name_out) *name_out = name;
+    return "#define QPB_KERNEL_NAME " + name + "\n" + body;
+}
+
+}  // namespace qpb
+
+namespace qpb {
+
+// LDS layout of the band kernel (qpb_band.hip), doubles per QP
+struct BandLayout {
+    long RS, O_P, O_L, O_Z, O_G, O_AR, O_AL, O_STATIC_END;
+    long V_X, V_RX, V_DX, V_Y, V_RY, V_DY, V_Z, V_S, V_RZ, V_DZ, V_DS, V_W, V_Q, LDS_QP;
+};
+
+static BandLayout band_layout(const Plan &pl) {
+    const long nb = pl.band_nb, ns = pl.band_ns, mz = pl.band_mz, my = pl.band_my;
+    const long nx = nb * ns, nz = mz * ns, ny = my * ns, ny1 = ny > 0 ? ny : 1;
+    BandLayout L;
+    L.RS = nb + 1;
+    L.O_P = 0;
+    L.O_L = L.O_P + ns * nb * nb;
+    L.O_Z = L.O_L + ns * nb * L.RS;
+    L.O_G = L.O_Z + ns * nb * nb;
+    L.O_AR = L.O_G + ns * mz * nb;
+    L.O_AL = L.O_AR + ns * my * nb;
+    L.O_STATIC_END = L.O_AL + ns * my * nb;
+    L.V_X = L.O_STATIC_END;
+    L.V_RX = L.V_X + nx;
+    L.V_DX = L.V_RX + nx;
+    L.V_Y = L.V_DX + nx;
+    L.V_RY = L.V_Y + ny1;
+    L.V_DY = L.V_RY + ny1;
+    L.V_Z = L.V_DY + ny1;
+    L.V_S = L.V_Z + nz;
+    L.V_RZ = L.V_S + nz;
+    L.V_DZ = L.V_RZ + nz;
+    L.V_DS = L.V_DZ + nz;
+    L.V_W = L.V_DS + nz;
+    L.V_Q = L.V_W + nz;
+    L.LDS_QP = L.V_Q + 64;
+    return L;
+}
+
+long band_lds_bytes(const Plan &pl) { return pl.band_nb > 0 ? band_layout(pl).LDS_QP * 8 : 0; }
+
+bool band_eligible(const Plan &pl, std::string *why) {
+    auto no = [&](const char *m) { if (why) *why = m; return false; };
+    if (pl.band_nb <= 0) return no("not a multi-stage pattern (band_shape)");
+    // the kernel eliminates z rows, y rows, then x in natural order: the plan's
+    // permutation must be exactly that (ORDER_LEAVES), or results would follow a
+    // different factorisation than the plan's oracle
+    const long n = pl.n, m = pl.m, p = pl.p;
+    for (long k = 0; k < m; k++)
+        if (pl.perm[k] != n + p + k) return no("permutation is not leaves-first");
+    for (long k = 0; k < p; k++)
+        if (pl.perm[m + k] != n + k) return no("permutation is not leaves-first");
+    for (long k = 0; k < n; k++)
+        if (pl.perm[m + p + k] != k) return no("permutation is not leaves-first");
+    if (band_lds_bytes(pl) > 160L * 1024) return no("per-QP state exceeds the LDS of a CU");
+    if (why) why->clear();
+    return true;
+}
+
+std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
+    const long nb = pl.band_nb, ns = pl.band_ns, mz = pl.band_mz, my = pl.band_my;
+    const BandLayout L = band_layout(pl);
+    std::ostringstream o;
+    o << "#define QPB_ROW_COMMON_ONLY 1\n" << kRowTemplate << "\n#undef QPB_ROW_COMMON_ONLY\n";
+    o << "// generated by qpb_wave for plan " << std::hex << pl.hash << std::dec << ": n=" << pl.n << " m=" << pl.m
+      << " p=" << pl.p << " [band: " << ns << " stages of " << nb << "/" << mz << "/" << my << ", fast]\n";
+    if (const char *e = getenv("QPB_WAVE_OPTS")) {
+        std::istringstream in(e);
+        std::string kv;
+        while (in >> kv) {
+            const size_t eq = kv.find('=');
+            if (eq != std::string::npos) o << "#define " << kv.substr(0, eq) << " " << kv.substr(eq + 1) << "\n";
+        }
+    }
+    o << "#define QPB_BNB " << nb << "\n#define QPB_BNS " << ns << "\n#define QPB_BMZ " << mz << "\n#define QPB_BMY " << my
+      << "\n";
+    const long nP = pl.Pin.nnz(), nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz();
+    o << "#define QPB_NNZP " << nP << "\n#define QPB_NNZA " << nA << "\n#define QPB_NNZG " << nG << "\n";
+    const char *names[] = {"RS", "O_P", "O_L", "O_Z", "O_G", "O_AR", "O_AL", "O_STATIC_END", "V_X", "V_RX", "V_DX",
+                           "V_Y", "V_RY", "V_DY", "V_Z", "V_S", "V_RZ", "V_DZ", "V_DS", "V_W", "V_Q", "LDS_QP"};
+    const long vals[] = {L.RS, L.O_P, L.O_L, L.O_Z, L.O_G, L.O_AR, L.O_AL, L.O_STATIC_END, L.V_X, L.V_RX, L.V_DX,
+                         L.V_Y, L.V_RY, L.V_DY, L.V_Z, L.V_S, L.V_RZ, L.V_DZ, L.V_DS, L.V_W, L.V_Q, L.LDS_QP};
+    for (size_t i = 0; i < sizeof vals / sizeof vals[0]; i++) o << "#define " << names[i] << " " << vals[i] << "\n";
+    // CSC value -> LDS slot of the stage blocks
+    std::vector<long> pcol(nP), acol(nA), gcol(nG);
+    for (long j = 0; j < pl.n; j++) {
+        for (long k = pl.Pin.jc[j]; k < pl.Pin.jc[j + 1]; k++) pcol[k] = j;
+        if (nA)
+            for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++) acol[k] = j;
+        for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1]; k++) gcol[k] = j;
+    }
+    auto pslot = [&](long i, long j) { return L.O_P + (j / nb) * nb * nb + (i % nb) * nb + (j % nb); };
+    table(o, "static __device__ const int qpb_bsP", nP, [&](long k) { return pslot(pl.Pin.ir[k], pcol[k]); });
+    table(o, "static __device__ const int qpb_bsP2", nP, [&](long k) {
+        const long i = pl.Pin.ir[k], j = pcol[k];
+        return (pl.pmode == P_UPPER && i != j) ? pslot(j, i) : -1L;
+    });
+    std::vector<unsigned> gm(mz, 0), arm(my > 0 ? my : 1, 0), alm(my > 0 ? my : 1, 0);
+    table(o, "static __device__ const int qpb_bsG", nG, [&](long k) {
+        const long r = pl.G.ir[k], j = gcol[k];
+        gm[r % mz] |= 1u << (j % nb);
+        return L.O_G + (r / mz) * mz * nb + (r % mz) * nb + (j % nb);
+    });
+    table(o, "static __device__ const int qpb_bsA", nA, [&](long k) {
+        const long l = pl.A.ir[k], j = acol[k], st = l / my;
+        const bool right = j / nb == st;
+        (right ? arm : alm)[l % my] |= 1u << (j % nb);
+        return (right ? L.O_AR : L.O_AL) + st * my * nb + (l % my) * nb + (j % nb);
+    });
+    auto masks = [&](const char *nm, const std::vector<unsigned> &v) {
+        unsigned u = 0;
+        o << "static constexpr unsigned " << nm << "m[" << v.size() << "] = {";
+        for (size_t i = 0; i < v.size(); i++) { o << (i ? "," : "") << v[i] << "u"; u |= v[i]; }
+        o << "};\nstatic constexpr unsigned " << nm << "u = " << u << "u;\n";
+    };
+    masks("qpb_bG", gm);
+    masks("qpb_bAR", arm);
+    masks("qpb_bAL", alm);
+    const std::string body = o.str() + kBandTemplate;
+    const std::string name = named(body, "qpb_band", pl, 64);
     if (name_out) *name_out = name;
     return "#define QPB_KERNEL_NAME " + name + "\n" + body;
 }

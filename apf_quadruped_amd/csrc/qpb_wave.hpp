@@ -33,4 +33,9 @@ std::string generate_row_kernel(const Plan &pl, std::string *name_out, int wpe =
 // blocks [bend[i-1], bend[i]) run member i.
 constexpr int QPB_GROUP_MAX = 16;
 std::string generate_row_group_kernel(const std::vector<const Plan *> &pls, std::string *name_out);
+// Band form (qpb_band.hip, one QP per wavefront): multi-stage plans (Plan::band_*)
+// in leaves-first order whose per-QP state fits the LDS of a CU.
+bool band_eligible(const Plan &pl, std::string *why);
+long band_lds_bytes(const Plan &pl);
+std::string generate_band_kernel(const Plan &pl, std::string *name_out);
 }  // namespace qpb

@@ -68,6 +68,9 @@ typedef struct qpb_plan qpb_plan;
                                   where the row form (four QPs per wavefront) fits */
 #define QPB_KERNEL_TREE 0x800  /* always the tree kernel (one QP per workgroup,
                                   level-scheduled sparse LDL'; any pattern)        */
+#define QPB_KERNEL_BAND 0x1000 /* the band kernel for cold solves (one QP per wavefront,
+                                  block-tridiagonal LDL' over the stages of a multi-stage
+                                  pattern, e.g. an MPC horizon; warm solves: tree) */
 
 /* error codes */
 #define QPB_OK        0
@@ -97,7 +100,8 @@ typedef struct qpb_plan_info {
     long wave_max_batch;         /* qpb_solve uses it for B <= this (-1: always) */
     int  wave_qpw;               /* QPs per wavefront of that kernel: 1 wave form, 4 row form */
     int  tree_ok;                /* plan can use the tree kernel (one QP per workgroup) */
-    int  large_kernel;           /* kernel used beyond the wave kernel's range: 1 lane, 2 wave, 3 tree */
+    int  large_kernel;           /* kernel used beyond the wave kernel's range: 1 lane, 2 wave, 3 tree,
+                                    4 band (cold solves; warm solves of such plans: tree) */
 } qpb_plan_info;
 
 void qpb_default_settings(qpb_settings *st);

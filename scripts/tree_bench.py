@@ -1,6 +1,6 @@
 """Kernel timings per plan / kernel / batch (HIP events around qpb_solve).
 
-    python scripts/tree_bench.py [name:kernel:B ...]
+    python scripts/tree_bench.py [name:kernel:B[:order] ...]
 
 Default cases: the MPC-horizon QP on the tree kernel (configs[3]) and the
 controller / C1 shapes on the tree vs wave kernels.  One JSON line per case."""
@@ -30,10 +30,11 @@ def main():
                              "c1:wave:65536", "c1:lane:65536", "c1:wave:262144", "c1:lane:262144",
                              "c1:wave:1048576", "c1:lane:1048576"]
     for case in cases:
-        name, kernel, B = case.split(":")
+        name, kernel, B, *order = case.split(":")
         B = int(B)
         d0 = qp(name, np.arange(1))
-        plan = Plan.from_dense(d0["n"], d0["m"], d0["p"], d0["P"][0], d0["A"][0], d0["G"][0], kernel=kernel)
+        plan = Plan.from_dense(d0["n"], d0["m"], d0["p"], d0["P"][0], d0["A"][0], d0["G"][0], kernel=kernel,
+                              order=order[0] if order else "own")
         nb = min(B, 4096)
         d = qp(name, np.arange(nb))
         reps = (B + nb - 1) // nb

@@ -89,8 +89,9 @@ def test_tree_kernel_mpc_batch(B, oracle):
     deterministic, strided sample vs the oracle in the plan's order."""
     import torch
     from apf_quadruped_amd import plans, workloads as W
+    from apf_quadruped_amd.batch import Plan
     d = W.mpc_qp(plans.SEED + 4, np.arange(B))
-    plan = plans.standard_plan("mpc_h10")
+    plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel="tree")
     assert plan.kernel_for(B) == "tree"
     vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"],
                                                                 d["b"]).items()}
