@@ -18,14 +18,16 @@
 // (ldl.c:253-326, pivot regularisation ldl.c:273-274), in block form, and the same
 // triangular solves (kktsolve, Auxilary.c:471-564) as block forward / backward sweeps.
 //
-// Lanes: x quantities of the current stage live in lane c = lane & 15 of EVERY 16-lane
-// DPP row (four identical copies), so a z row r (lane r < MZ <= 64) or a y row
-// (lane l < MY <= 64) reads x_j of its stage with a DPP row_newbcast:j in any row;
-// the 12 x 12 stage blocks are the row kernel's DPP products and pivot chain.  z / y
-// values reach the x lanes through LDS (same-address broadcast reads).  All of the
-// QP's state -- P, G, A stage blocks, the factor's L_k (with 1/D_k) and -Z_k rows, the
-// iterate, residuals and directions -- stays in the workgroup's LDS for the whole
-// solve (79 KB for MPC: two QPs per CU); inputs are read once, outputs written once.
+// Lanes.  Work that is independent across stages (residuals, the blocks H_kk and X_k,
+// the solves' right-hand sides t_k and their dz / dy) runs stage-parallel: DPP row R of
+// the wavefront takes stage 4 i + R, lane c holding x_c, y_c and the z rows c + 16 u of
+// it -- the row kernel's layout, one stage per row, products as DPP row_newbcast FMAs,
+// the neighbouring stages' x / y values loaded per lane.  The recurrences (Z_k, the
+// Schur update and pivots of each stage, the forward / backward sweeps) run stage by
+// stage.  All of the QP's state -- P, G, A stage blocks, the factor's L_k (with 1/D_k)
+// and -Z_k rows, the iterate, residuals and directions -- stays in the workgroup's LDS
+// for the whole solve (79 KB for MPC: two QPs per CU); inputs are read once, outputs
+// written once.
 //
 // The loop is the row kernel's (qpSWIFT.c:473-644): kkt_initialize as iteration -1,
 // residuals + exit test, factor, predictor, corrector, step lengths (Auxilary.c:359-393),
@@ -41,14 +43,16 @@
 #define BNZ (MZ * NS)
 #define BNY (MY * NS)
 #define BNY1 (BNY > 0 ? BNY : 1)
+#define ZS ((MZ + 15) / 16)       // z sub-rows of a DPP row (z rows c, c + 16, ..)
+#define NR ((NS + 3) / 4)         // rounds of the stage-parallel passes (four stages each)
 // per-stage blocks and vectors (doubles; offsets emitted by the generator, qpb_wave.cpp
 // band_layout): O_P P_k rows (stride NB), O_L rows of -L_k at stride RS = NB + 1 (zeros
 // from the diagonal on, 1 / D_c at column NB), O_Z rows of -Z_k (stride NB), O_G G_k rows,
 // O_AR / O_AL the A row groups' stage-k / stage-(k-1) parts (stride NB); the vectors
-// x, rx, dx | y, ry, dy | z, s, rz, dz, ds, w in natural order; V_Q one stage's w o bz.
+// x, rx, dx | y, ry, dy | z, s, rz, dz, ds, w in natural order.
 #define BLKP (NB * NB)
 #define BLKL (NB * RS)
-static_assert(NB >= 1 && NB <= 16 && MZ >= 1 && MZ <= 64 && MY <= 64 && NS >= 2, "band kernel sizes");
+static_assert(NB >= 1 && NB <= 16 && MZ >= 1 && MZ <= 64 && MY <= 16 && NS >= 2, "band kernel sizes");
 
 // 64-lane sums / maxima: the row butterfly, then the four row results (fixed order)
 static __device__ __forceinline__ double qpb_bsum(double v) {
@@ -76,8 +80,15 @@ static __device__ __forceinline__ double qpb_bmax(double v) {
 // solve modes: the right-hand side's z part (bx = RX, by = RY in every mode)
 enum { BM_SETUP = 0, BM_PRED = 1, BM_CORR = 2 };
 
+// union of the structural columns of the G rows of z sub-row u (rows 16u .. 16u + 15)
+static constexpr unsigned qpb_bgsub(int u) {
+    unsigned m = 0;
+    for (int r = 16 * u; r < 16 * u + 16 && r < MZ; r++) m |= qpb_bGm[r];
+    return m;
+}
+
 static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, double *__restrict__ Ls) {
-    const int lane = threadIdx.x & 63, c = lane & 15;
+    const int lane = threadIdx.x & 63, R = lane >> 4, c = lane & 15;
     if (q >= a.B) return;                      // grid padding (XCD order): wave-uniform
 #if QPB_B_TIMING
     double tph[6] = {0, 0, 0, 0, 0, 0};
@@ -85,13 +96,28 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #endif
     const long tile = q >> 6;
     const int ql = (int)(q & 63);
-    const int xc = c < NB ? c : NB - 1;        // x lane (clamped: lanes NB..15 compute copies)
-    const bool x0 = lane < NB;                 // the x lanes that store / count (row 0)
-    const bool isz = lane < MZ, isy = lane < MY;
-    const int zr = isz ? lane : MZ - 1, yl = isy ? lane : (MY > 0 ? MY - 1 : 0);
+    // Lanes.  Stage-parallel passes: DPP row R works on stage 4 i + R, lane c holds x_c,
+    // y_c (c < MY) and z rows c + 16 u (u < ZS) of it -- the row kernel's layout per stage.
+    // Sequential passes (the block factor's Schur complements and pivots, the triangular
+    // sweeps): every row computes the same stage (row 0 stores), except the factor, whose
+    // rows each hold their own stage's block from the stage-parallel part.
+    const int xc = c < NB ? c : NB - 1;
+    const bool isx = c < NB, isy = c < MY;
+    const int yc = isy ? c : (MY > 0 ? MY - 1 : 0);
+    int zrc[ZS];
+    bool isz[ZS];
+#pragma unroll
+    for (int u = 0; u < ZS; u++) {
+        isz[u] = c + 16 * u < MZ;
+        zrc[u] = isz[u] ? c + 16 * u : MZ - 1;
+    }
+    const bool st0 = R == 0 && isx;            // the x lanes that store in sequential passes
     constexpr double RDY = 1.0 / -1e-7;        // leaf y pivots: D = 0 regularised to -1e-7
+    const double *gc = a.c + tile * (BNX * QPB_TSTR) + ql;
+    const double *gh = a.h + tile * (BNZ * QPB_TSTR) + ql;
+    const double *gb = a.b + tile * (BNY1 * QPB_TSTR) + ql;
 
-    // ---- stage P, G, A into the per-stage dense blocks; c, b, h into RX, RY, RZ
+    // ---- stage P, G, A into the per-stage dense blocks; -c, b, h into RX, RY, RZ
     for (int i = lane; i < O_STATIC_END; i += 64) Ls[i] = 0.0;
     qpb_wsync();
     {
@@ -107,12 +133,12 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         const double *tA = a.A + tile * (QPB_NNZA * QPB_TSTR) + ql;
         for (int k = lane; k < QPB_NNZA; k += 64) Ls[qpb_bsA[k]] = QPB_LDS(&tA[k * QPB_TSTR]);
 #endif
-        for (int i = lane; i < BNX; i += 64) Ls[V_RX + i] = -QPB_LDS(&a.c[tile * (BNX * QPB_TSTR) + i * QPB_TSTR + ql]);
+        for (int i = lane; i < BNX; i += 64) Ls[V_RX + i] = -QPB_LDS(&gc[i * QPB_TSTR]);
 #if MY > 0
-        for (int i = lane; i < BNY; i += 64) Ls[V_RY + i] = QPB_LDS(&a.b[tile * (BNY * QPB_TSTR) + i * QPB_TSTR + ql]);
+        for (int i = lane; i < BNY; i += 64) Ls[V_RY + i] = QPB_LDS(&gb[i * QPB_TSTR]);
 #endif
         for (int i = lane; i < BNZ; i += 64) {
-            Ls[V_RZ + i] = QPB_LDS(&a.h[tile * (BNZ * QPB_TSTR) + i * QPB_TSTR + ql]);
+            Ls[V_RZ + i] = QPB_LDS(&gh[i * QPB_TSTR]);
             Ls[V_Z + i] = 1.0;
             Ls[V_S + i] = 1.0;
         }
@@ -122,83 +148,204 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
     qpb_wsync();
     QPB_BT(5);
 
-    // per-element helpers (z lanes): 1 / z, the KKT diagonal's w = -1 / regularise(-s / z)
-    auto wz = [](double s, double z) { return -qpb_rcp_reg(-s * qpb_rcp(z)); };
+    // the KKT diagonal's w = -1 / regularise(-s / z) per z row (kkt_initialize: -I, w = 1)
     auto w_pass = [&](bool setup) {
         for (int i = lane; i < BNZ; i += 64)
-            Ls[V_W + i] = setup ? 1.0 : wz(Ls[V_S + i], Ls[V_Z + i]);   // kkt_initialize: -I (w = 1)
+            Ls[V_W + i] = setup ? 1.0 : -qpb_rcp_reg(-Ls[V_S + i] * qpb_rcp(Ls[V_Z + i]));
         qpb_wsync();
     };
 
-    // ---- factor: block LDL' of the x block, stage by stage
-    double nLp[NB], rdp = 0.0;                 // previous stage: row xc of -L, 1 / D_xc
+    // this row's stage slices (stage kc): column xc of G_k, AR_k, AL_k, AL_{k+1} (the last
+    // zero when k + 1 = NS), rows zrc[u] of G_k, row yc of AR_k and AL_k
+    auto col_G = [&](int kc, double (&g)[MZ]) {
+        const double *Gk = Ls + O_G + kc * (MZ * NB) + xc;
 #pragma unroll
-    for (int f = 0; f < NB; f++) nLp[f] = 0.0;
-    auto factor = [&]() {
+        for (int r = 0; r < MZ; r++) g[r] = Gk[r * NB];
+    };
+    auto col_A = [&](int off, int kc, double (&v)[MY1]) {
+        const double *Ak = Ls + off + kc * (MY * NB) + xc;
+#pragma unroll
+        for (int l = 0; l < MY1; l++) v[l] = MY > 0 ? Ak[l * NB] : 0.0;
+    };
+
+    // ---- residuals (Auxilary.c:745-786), stage-parallel; returns the objective and the
+    // four sums rx'rx, ry'ry, rz'rz, s'z
+    auto residuals = [&](double (&red)[4]) -> double {
+        double srx = 0.0, sry = 0.0, srz = 0.0, ssz = 0.0, sfv = 0.0;
 #pragma unroll 1
-        for (int k = 0; k < NS; k++) {
-            const double *Pr = Ls + O_P + k * BLKP + xc * NB;
-            const double *Gk = Ls + O_G + k * (MZ * NB);
-            const double *Wk = Ls + V_W + k * MZ;
-            double H[NB];
+        for (int i = 0; i < NR; i++) {
+            const int k = 4 * i + R;
+            const bool act = k < NS;
+            const int kc = act ? k : NS - 1;
+            const bool nxt = kc + 1 < NS;
+            const double cx = QPB_LDS(&gc[(kc * NB + xc) * QPB_TSTR]);
+            double hz[ZS], zk[ZS], sk[ZS];
 #pragma unroll
-            for (int j = 0; j < NB; j++) H[j] = Pr[j];
-            // + G_k' W_k G_k: per row r, lane j's G(r, j) broadcast against G(r, c) w_r
+            for (int u = 0; u < ZS; u++) {
+                hz[u] = QPB_LDS(&gh[(kc * MZ + zrc[u]) * QPB_TSTR]);
+                zk[u] = Ls[V_Z + kc * MZ + zrc[u]];
+                sk[u] = Ls[V_S + kc * MZ + zrc[u]];
+            }
+            const double xk = Ls[V_X + kc * NB + xc];
+            const double xp = kc > 0 ? Ls[V_X + (kc - 1) * NB + xc] : 0.0;
+            double pr[NB], gr[ZS][NB], gcl[MZ];
+            const double *Pr = Ls + O_P + kc * (NB * NB) + xc * NB;
+#pragma unroll
+            for (int j = 0; j < NB; j++) pr[j] = Pr[j];
+#pragma unroll
+            for (int u = 0; u < ZS; u++) {
+                const double *Gr = Ls + O_G + kc * (MZ * NB) + zrc[u] * NB;
+#pragma unroll
+                for (int j = 0; j < NB; j++) gr[u][j] = Gr[j];
+            }
+            col_G(kc, gcl);
+            double ta[4] = {cx, 0.0, 0.0, 0.0}, px = 0.0, gx[ZS];
+#pragma unroll
+            for (int u = 0; u < ZS; u++) gx[u] = 0.0;
+#if MY > 0
+            const double by = QPB_LDS(&gb[(kc * MY + yc) * QPB_TSTR]);
+            const double yk = Ls[V_Y + kc * MY + yc];
+            const double yn = nxt ? Ls[V_Y + (kc + 1) * MY + yc] : 0.0;
+            double arc[MY1], alnc[MY1], arr[NB], alr[NB];
+            col_A(O_AR, kc, arc);
+            col_A(O_AL, nxt ? kc + 1 : kc, alnc);
+            const double *ARr = Ls + O_AR + kc * (MY * NB) + yc * NB, *ALr = Ls + O_AL + kc * (MY * NB) + yc * NB;
+#pragma unroll
+            for (int j = 0; j < NB; j++) { arr[j] = ARr[j]; alr[j] = ALr[j]; }
+            double ay = 0.0;
+#endif
+            qpb_fence(xk, xp);
+            qpb_for<0, NB>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                qpb_fx<j>(px, xk, pr[j]);                                   // P x
+                qpb_for<0, ZS>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    if constexpr ((qpb_bgsub(u) >> j) & 1) qpb_fx<j>(gx[u], xk, gr[u][j]);    // G x
+                });
+#if MY > 0
+                if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(ay, xk, arr[j]);       // AR_k x_k
+                if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(ay, xp, alr[j]);       // AL_k x_{k-1}
+#endif
+            });
+            // G'z, AR_k' y_k, AL_{k+1}' y_{k+1}: z / y lanes of the row by DPP broadcast
+            qpb_fence(zk[0]);
             qpb_for<0, MZ>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                const double g = Gk[r * NB + xc];
-                const double t = g * Wk[r];
-                qpb_fence(g, t);
-                qpb_for<0, NB>([&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    if constexpr ((qpb_bGm[r] >> j) & 1) qpb_fx<j>(H[j], g, t);
-                });
+                qpb_fx<(r & 15)>(ta[r & 3], zk[r >> 4], gcl[r]);
             });
 #if MY > 0
-            // + 1e7 AR_k' AR_k + 1e7 AL_{k+1}' AL_{k+1}
-            const double *ARk = Ls + O_AR + k * (MY * NB);
+            qpb_fence(yk, yn);
             qpb_for<0, MY>([&](auto lc) {
                 constexpr int l = decltype(lc)::value;
-                const double av = ARk[l * NB + xc];
-                const double t = -RDY * av;
-                qpb_fence(av, t);
-                qpb_for<0, NB>([&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    if constexpr ((qpb_bARm[l] >> j) & 1) qpb_fx<j>(H[j], av, t);
-                });
+                qpb_fx<l>(ta[(MZ + l) & 3], yk, arc[l]);
+                qpb_fx<l>(ta[(MZ + MY + l) & 3], yn, nxt ? alnc[l] : 0.0);
             });
-            if (k + 1 < NS) {
-                const double *ALn = Ls + O_AL + (k + 1) * (MY * NB);
-                qpb_for<0, MY>([&](auto lc) {
-                    constexpr int l = decltype(lc)::value;
-                    const double av = ALn[l * NB + xc];
-                    const double t = -RDY * av;
-                    qpb_fence(av, t);
-                    qpb_for<0, NB>([&](auto jc) {
-                        constexpr int j = decltype(jc)::value;
-                        if constexpr ((qpb_bALm[l] >> j) & 1) qpb_fx<j>(H[j], av, t);
-                    });
-                });
+#endif
+            const double rx = -(((ta[0] + ta[1]) + (ta[2] + ta[3])) + px);
+            if (act && isx) {
+                Ls[V_RX + k * NB + c] = rx;
+                srx = __builtin_fma(rx, rx, srx);
+                sfv = __builtin_fma(xk, __builtin_fma(0.5, px, cx), sfv);   // objective (Auxilary.c:1133-1141)
             }
-            if (k > 0) {
-                // X_k(c, j) = 1e7 sum_l AR_k(l, c) AL_k(l, j); Z_k = X_k L_{k-1}^-T
-                const double *ALk = Ls + O_AL + k * (MY * NB);
-                double Zr[NB];
 #pragma unroll
-                for (int j = 0; j < NB; j++) Zr[j] = 0.0;
-                qpb_for<0, MY>([&](auto lc) {
-                    constexpr int l = decltype(lc)::value;
-                    const double al = ALk[l * NB + xc];
-                    const double t = -RDY * ARk[l * NB + xc];
-                    qpb_fence(al, t);
-                    qpb_for<0, NB>([&](auto jc) {
-                        constexpr int j = decltype(jc)::value;
-                        if constexpr ((qpb_bALm[l] >> j) & 1) qpb_fx<j>(Zr[j], al, t);
+            for (int u = 0; u < ZS; u++) {
+                if (act && isz[u]) {
+                    const double rz = (hz[u] - sk[u]) - gx[u];
+                    Ls[V_RZ + k * MZ + c + 16 * u] = rz;
+                    srz = __builtin_fma(rz, rz, srz);
+                    ssz = __builtin_fma(sk[u], zk[u], ssz);
+                }
+            }
+#if MY > 0
+            if (act && isy) {
+                const double ry = by - ay;
+                Ls[V_RY + k * MY + c] = ry;
+                sry = __builtin_fma(ry, ry, sry);
+            }
+#endif
+        }
+        qpb_wsync();
+        red[0] = qpb_bsum(srx);
+        red[1] = qpb_bsum(sry);
+        red[2] = qpb_bsum(srz);
+        red[3] = qpb_bsum(ssz);
+        return qpb_bsum(sfv);
+    };
+
+    // ---- factor: block LDL' of the x block.  Every fourth stage a stage-parallel part
+    // forms H_kk = P_k + G_k'W_k G_k + 1e7 (AR_k'AR_k + AL_{k+1}'AL_{k+1}) and X_k for the
+    // four stages of the round (row R: stage k + R, in registers); then the stages'
+    // sequential parts: Z_k = X_k L_{k-1}^-T, H_kk -= Z_k D_{k-1}^-1 Z_k', the pivots.
+    auto factor = [&]() {
+        double H[NB], Xr[NB];
+#pragma unroll 1
+        for (int k = 0; k < NS; k++) {
+            if ((k & 3) == 0) {
+                const int ks = k + R;
+                const int kc = ks < NS ? ks : NS - 1;
+                const bool nxt = kc + 1 < NS;
+                const double *Pr = Ls + O_P + kc * (NB * NB) + xc * NB;
+#pragma unroll
+                for (int j = 0; j < NB; j++) H[j] = Pr[j];
+                double gcl[MZ], wz[ZS];
+                col_G(kc, gcl);
+#pragma unroll
+                for (int u = 0; u < ZS; u++) wz[u] = Ls[V_W + kc * MZ + zrc[u]];
+                // + G_k' W_k G_k: four rows' products G(r, c) w_r first, then their DPP FMAs
+                qpb_for<0, (MZ + 3) / 4>([&](auto qc4) {
+                    constexpr int r0 = 4 * decltype(qc4)::value;
+                    double cr[4];
+                    qpb_for<0, 4>([&](auto uc) {
+                        constexpr int r = r0 + decltype(uc)::value;
+                        if constexpr (r < MZ) cr[decltype(uc)::value] = gcl[r] * qpb_nb<(r & 15)>(wz[r >> 4]);
+                        else cr[decltype(uc)::value] = 0.0;
+                    });
+                    asm volatile("" : "+v"(cr[0]), "+v"(cr[1]), "+v"(cr[2]), "+v"(cr[3]));
+                    qpb_for<0, 4>([&](auto uc) {
+                        constexpr int r = r0 + decltype(uc)::value;
+                        if constexpr (r < MZ) {
+                            qpb_for<0, NB>([&](auto jc) {
+                                constexpr int j = decltype(jc)::value;
+                                if constexpr ((qpb_bGm[r] >> j) & 1) qpb_fxs<j>(H[j], gcl[r], cr[decltype(uc)::value]);
+                            });
+                        }
                     });
                 });
+#if MY > 0
+                double arc[MY1], alc[MY1], alnc[MY1];
+                col_A(O_AR, kc, arc);
+                col_A(O_AL, kc, alc);
+                col_A(O_AL, nxt ? kc + 1 : kc, alnc);
+#pragma unroll
+                for (int j = 0; j < NB; j++) Xr[j] = 0.0;
+                qpb_for<0, MY>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
+                    const double tr = -RDY * arc[l], an = nxt ? alnc[l] : 0.0, tn = -RDY * an;
+                    qpb_fence(tr, an, tn);
+                    qpb_for<0, NB>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        if constexpr ((qpb_bARm[l] >> j) & 1) qpb_fx<j>(H[j], arc[l], tr);    // 1e7 AR_k'AR_k
+                        if constexpr ((qpb_bALm[l] >> j) & 1) {
+                            qpb_fx<j>(H[j], an, tn);                                       // 1e7 AL_{k+1}'AL_{k+1}
+                            qpb_fx<j>(Xr[j], alc[l], tr);                                  // X_k = 1e7 AR_k'AL_k
+                        }
+                    });
+                });
+#endif
+            }
+            const int kr = k & 3;                   // the row holding stage k's block
+            double Hs[NB];
+#pragma unroll
+            for (int j = 0; j < NB; j++) Hs[j] = H[j];
+#if MY > 0
+            if (k > 0) {
+                const double *Lp = Ls + O_L + (k - 1) * (NB * RS) + xc * RS;
+                double nLp[NB], Zr[NB];
+#pragma unroll
+                for (int f = 0; f < NB; f++) { nLp[f] = Lp[f]; Zr[f] = Xr[f]; }
+                const double rdp = Lp[NB];
                 // Z(c, e) = X(c, e) - sum_{f<e} L_{k-1}(e, f) Z(c, f): lane e's -L row broadcast,
-                // right-looking (column f of Z final -> every later column), so consecutive
-                // FMAs are independent; each Z(c, e) still sums over f in ascending order
+                // right-looking (each Z(c, e) sums over f in ascending order)
                 qpb_for<0, NB - 1>([&](auto fc) {
                     constexpr int f = decltype(fc)::value;
                     qpb_for<f + 1, NB>([&](auto ec) {
@@ -206,18 +353,18 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                         qpb_fx<e>(Zr[e], nLp[f], Zr[f]);
                     });
                 });
-                // H -= Z D_{k-1}^-1 Z'; -Z rows to LDS (the solves' coupling terms)
-                double *Zs = Ls + O_Z + k * BLKP + xc * NB;
+                // H_kk -= Z D_{k-1}^-1 Z'; -Z rows to LDS (the sweeps' coupling terms)
                 qpb_for<0, NB>([&](auto ec) {
                     constexpr int e = decltype(ec)::value;
                     const double t = -(Zr[e] * qpb_nb<e>(rdp));
                     qpb_fence(t);
                     qpb_for<0, NB>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
-                        qpb_fx<j>(H[j], Zr[e], t);
+                        qpb_fx<j>(Hs[j], Zr[e], t);
                     });
                 });
-                if (x0) {
+                if (R == kr && isx) {
+                    double *Zs = Ls + O_Z + k * (NB * NB) + c * NB;
 #pragma unroll
                     for (int e = 0; e < NB; e++) Zs[e] = -Zr[e];
                 }
@@ -225,34 +372,31 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #endif
             // LDL' of the stage block in natural order (the row kernel's pivot chain)
             double rDd = 0.0;
-            double dpiv = qpb_nb<0>(H[0]);
-            qpb_for<0, NB>([&](auto kc) {
-                constexpr int kk = decltype(kc)::value;
+            double dpiv = qpb_nb<0>(Hs[0]);
+            qpb_for<0, NB>([&](auto kc2) {
+                constexpr int kk = decltype(kc2)::value;
                 const double rd = qpb_rcp_reg(dpiv);
-                double nl = H[kk] * -rd;
+                double nl = Hs[kk] * -rd;
                 asm volatile("" : "+v"(nl));
                 if constexpr (kk + 1 < NB) {
-                    const double h = qpb_nb<kk + 1>(H[kk]), hkk = qpb_nb<kk + 1>(H[kk + 1]);
+                    const double h = qpb_nb<kk + 1>(Hs[kk]), hkk = qpb_nb<kk + 1>(Hs[kk + 1]);
                     dpiv = __builtin_fma(-(h * h), rd, hkk);
                 }
                 rDd = xc == kk ? rd : rDd;
                 qpb_for<kk + 1, NB>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
-                    qpb_fxs<j>(H[j], H[kk], nl);
+                    qpb_fxs<j>(Hs[j], Hs[kk], nl);
                 });
-                H[kk] = xc > kk ? nl : 0.0;
+                Hs[kk] = xc > kk ? nl : 0.0;
             });
-            double *Lr = Ls + O_L + k * BLKL + xc * RS;
-            if (x0) {
+            if (R == kr && isx) {
+                double *Lr = Ls + O_L + k * (NB * RS) + c * RS;
 #pragma unroll
-                for (int f = 0; f < NB; f++) Lr[f] = H[f];
+                for (int f = 0; f < NB; f++) Lr[f] = Hs[f];
                 Lr[NB] = rDd;
             }
-#pragma unroll
-            for (int f = 0; f < NB; f++) nLp[f] = H[f];
-            rdp = rDd;
+            qpb_wsync();
         }
-        qpb_wsync();
     };
 
     // ---- solve K [dx; dy; dz] = [RX; RY; bz] (bz per mode) into DX, DY, DZ (+ DS)
@@ -273,242 +417,158 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         return __builtin_fma(-cc, rzi, rz + s);
     };
     auto solve = [&](int mode, double smu, bool pcd) {
-        // forward: u_k = L_k^-1 (t_k - Z_k v_{k-1}), v_k = D_k^-1 u_k -> DX
+        // stage-parallel: t_k = bx_k + G_k'(w o bz) + 1e7 (AR_k' by_k + AL_{k+1}' by_{k+1}) -> DX
+#pragma unroll 1
+        for (int i = 0; i < NR; i++) {
+            const int k = 4 * i + R;
+            const bool act = k < NS;
+            const int kc = act ? k : NS - 1;
+            const bool nxt = kc + 1 < NS;
+            double v[ZS], gcl[MZ];
+#pragma unroll
+            for (int u = 0; u < ZS; u++) {
+                double cc;
+                const int iz = kc * MZ + zrc[u];
+                v[u] = Ls[V_W + iz] * bz_of(mode, iz, smu, pcd, &cc);
+            }
+            col_G(kc, gcl);
+            double ta[4] = {Ls[V_RX + kc * NB + xc], 0.0, 0.0, 0.0};
+            qpb_fence(v[0]);
+            qpb_for<0, MZ>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                qpb_fx<(r & 15)>(ta[r & 3], v[r >> 4], gcl[r]);
+            });
+#if MY > 0
+            double arc[MY1], alnc[MY1];
+            col_A(O_AR, kc, arc);
+            col_A(O_AL, nxt ? kc + 1 : kc, alnc);
+            const double yr = -RDY * Ls[V_RY + kc * MY + yc];
+            const double yrn = nxt ? -RDY * Ls[V_RY + (kc + 1) * MY + yc] : 0.0;
+            qpb_fence(yr, yrn);
+            qpb_for<0, MY>([&](auto lc) {
+                constexpr int l = decltype(lc)::value;
+                qpb_fx<l>(ta[(MZ + l) & 3], yr, arc[l]);
+                qpb_fx<l>(ta[(MZ + MY + l) & 3], yrn, alnc[l]);
+            });
+#endif
+            if (act && isx) Ls[V_DX + k * NB + c] = (ta[0] + ta[1]) + (ta[2] + ta[3]);
+        }
+        qpb_wsync();
+        // forward sweep: u_k = L_k^-1 (t_k - Z_k v_{k-1}), v_k = D_k^-1 u_k -> DX
         double vprev = 0.0;
 #pragma unroll 1
         for (int k = 0; k < NS; k++) {
-            // leaf values of the stage's z rows: w_r bz_r (LDS, read by every x lane)
-            if (isz) {
-                double cc;
-                const int i = k * MZ + lane;
-                Ls[V_Q + lane] = Ls[V_W + i] * bz_of(mode, i, smu, pcd, &cc);
-            }
-            qpb_wsync();
-            const double *Gk = Ls + O_G + k * (MZ * NB);
-            double ta[4] = {Ls[V_RX + k * NB + xc], 0.0, 0.0, 0.0};
+            double t = Ls[V_DX + k * NB + xc];
+            const double *Lr = Ls + O_L + k * (NB * RS) + xc * RS;
+            double nl[NB];
 #pragma unroll
-            for (int r = 0; r < MZ; r++) ta[r & 3] = __builtin_fma(Gk[r * NB + xc], Ls[V_Q + r], ta[r & 3]);
+            for (int f = 0; f < NB; f++) nl[f] = Lr[f];
+            const double rd = Lr[NB];
 #if MY > 0
-            const double *ARk = Ls + O_AR + k * (MY * NB);
-#pragma unroll
-            for (int l = 0; l < MY; l++)
-                ta[(MZ + l) & 3] = __builtin_fma(ARk[l * NB + xc] * -RDY, Ls[V_RY + k * MY + l], ta[(MZ + l) & 3]);
-            if (k + 1 < NS) {
-                const double *ALn = Ls + O_AL + (k + 1) * (MY * NB);
-#pragma unroll
-                for (int l = 0; l < MY; l++)
-                    ta[(MZ + MY + l) & 3] =
-                        __builtin_fma(ALn[l * NB + xc] * -RDY, Ls[V_RY + (k + 1) * MY + l], ta[(MZ + MY + l) & 3]);
-            }
-#endif
-            double t = (ta[0] + ta[1]) + (ta[2] + ta[3]);
-            const double *Zr = Ls + O_Z + k * BLKP + xc * NB;
-            const double *Lr = Ls + O_L + k * BLKL + xc * RS;
             if (k > 0) {
+                const double *Zr = Ls + O_Z + k * (NB * NB) + xc * NB;
                 double nz[NB];
 #pragma unroll
                 for (int e = 0; e < NB; e++) nz[e] = Zr[e];
                 qpb_fence(vprev);
                 qpb_for<0, NB>([&](auto ec) { qpb_fx<decltype(ec)::value>(t, vprev, nz[decltype(ec)::value]); });
             }
-            double nl[NB];
-#pragma unroll
-            for (int f = 0; f < NB; f++) nl[f] = Lr[f];
-            const double rd = Lr[NB];
+#endif
             qpb_fence(t);
             qpb_for<0, NB>([&](auto fc) { qpb_fxd<decltype(fc)::value>(t, nl[decltype(fc)::value]); });
             vprev = t * rd;
-            if (x0) Ls[V_DX + k * NB + c] = vprev;
-            qpb_wsync();
+            if (st0) Ls[V_DX + k * NB + c] = vprev;
         }
-        // backward: dx_k = L_k^-T (v_k - D_k^-1 Z_{k+1}' dx_{k+1}); dz, dy of the stages
+        qpb_wsync();
+        // backward sweep: dx_k = L_k^-T (v_k - D_k^-1 Z_{k+1}' dx_{k+1}) -> DX
         double dxn = 0.0;
 #pragma unroll 1
         for (int k = NS - 1; k >= 0; k--) {
-            const double *Lk = Ls + O_L + k * BLKL;
+            const double *Lk = Ls + O_L + k * (NB * RS);
             double r = Ls[V_DX + k * NB + xc];
-            if (k + 1 < NS) {
-                const double *Zn = Ls + O_Z + (k + 1) * BLKP;    // -Z_{k+1}, read by columns
-                double zt[NB];
-#pragma unroll
-                for (int j = 0; j < NB; j++) zt[j] = Zn[j * NB + xc];
-                double acc = 0.0;
-                qpb_fence(dxn);
-                qpb_for<0, NB>([&](auto jc) { qpb_fx<decltype(jc)::value>(acc, dxn, zt[decltype(jc)::value]); });
-                r = __builtin_fma(acc, Lk[xc * RS + NB], r);
-            }
             double lt[NB];
 #pragma unroll
             for (int e = 0; e < NB; e++) lt[e] = Lk[e * RS + xc];      // -L(e, c): column c
+            const double rd = Lk[xc * RS + NB];
+#if MY > 0
+            if (k + 1 < NS) {
+                const double *Zn = Ls + O_Z + (k + 1) * (NB * NB) + xc;    // -Z_{k+1}, by columns
+                double zt[NB];
+#pragma unroll
+                for (int j = 0; j < NB; j++) zt[j] = Zn[j * NB];
+                double acc = 0.0;
+                qpb_fence(dxn);
+                qpb_for<0, NB>([&](auto jc) { qpb_fx<decltype(jc)::value>(acc, dxn, zt[decltype(jc)::value]); });
+                r = __builtin_fma(acc, rd, r);
+            }
+#endif
             qpb_fence(r);
             qpb_for<0, NB>([&](auto ec) {
                 constexpr int e = NB - 1 - decltype(ec)::value;
                 qpb_fxd<e>(r, lt[e]);
             });
-            const double dx = r;
-            if (x0) Ls[V_DX + k * NB + c] = dx;
-            // z rows of stage k: dz = w (G dx - bz)
-            {
-                const double *Gr = Ls + O_G + k * (MZ * NB) + zr * NB;
-                double g[NB];
+            if (st0) Ls[V_DX + k * NB + c] = r;
+            dxn = r;
+        }
+        qpb_wsync();
+        // stage-parallel: dz = w (G dx - bz) (+ ds in the corrector), dy = -1e7 (by - A dx)
+#pragma unroll 1
+        for (int i = 0; i < NR; i++) {
+            const int k = 4 * i + R;
+            const bool act = k < NS;
+            const int kc = act ? k : NS - 1;
+            const double dxk = Ls[V_DX + kc * NB + xc];
+            double gr[ZS][NB], gz[ZS];
 #pragma unroll
-                for (int j = 0; j < NB; j++) g[j] = Gr[j];
-                double gs = 0.0;
-                qpb_fence(dx);
-                qpb_for<0, NB>([&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    if constexpr ((qpb_bGu >> j) & 1) qpb_fx<j>(gs, dx, g[j]);
+            for (int u = 0; u < ZS; u++) {
+                const double *Gr = Ls + O_G + kc * (MZ * NB) + zrc[u] * NB;
+#pragma unroll
+                for (int j = 0; j < NB; j++) gr[u][j] = Gr[j];
+                gz[u] = 0.0;
+            }
+#if MY > 0
+            const double dxp = kc > 0 ? Ls[V_DX + (kc - 1) * NB + xc] : 0.0;
+            double arr[NB], alr[NB], gy = 0.0;
+            const double *ARr = Ls + O_AR + kc * (MY * NB) + yc * NB, *ALr = Ls + O_AL + kc * (MY * NB) + yc * NB;
+#pragma unroll
+            for (int j = 0; j < NB; j++) { arr[j] = ARr[j]; alr[j] = ALr[j]; }
+            qpb_fence(dxk, dxp);
+#else
+            qpb_fence(dxk);
+#endif
+            qpb_for<0, NB>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                qpb_for<0, ZS>([&](auto uc) {
+                    constexpr int u = decltype(uc)::value;
+                    if constexpr ((qpb_bgsub(u) >> j) & 1) qpb_fx<j>(gz[u], dxk, gr[u][j]);
                 });
-                if (isz) {
-                    const int i = k * MZ + lane;
+#if MY > 0
+                if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(gy, dxk, arr[j]);
+                if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(gy, dxp, alr[j]);
+#endif
+            });
+#pragma unroll
+            for (int u = 0; u < ZS; u++) {
+                if (act && isz[u]) {
+                    const int iz = k * MZ + c + 16 * u;
                     double cc = 0.0;
-                    const double bz = bz_of(mode, i, smu, pcd, &cc);
-                    const double w = Ls[V_W + i];
-                    const double dz = w * (gs - bz);
-                    Ls[V_DZ + i] = dz;
+                    const double bz = bz_of(mode, iz, smu, pcd, &cc);
+                    const double dz = Ls[V_W + iz] * (gz[u] - bz);
+                    Ls[V_DZ + iz] = dz;
                     if (mode == BM_CORR) {
-                        const double s = Ls[V_S + i], rzi = qpb_rcp(Ls[V_Z + i]);
-                        Ls[V_DS + i] = __builtin_fma(__builtin_fma(-s, dz, cc), rzi, -s);
+                        const double s = Ls[V_S + iz], rzi = qpb_rcp(Ls[V_Z + iz]);
+                        Ls[V_DS + iz] = __builtin_fma(__builtin_fma(-s, dz, cc), rzi, -s);
                     }
                 }
             }
 #if MY > 0
-            // y rows of stage k + 1 (their x neighbours dx_{k+1}, dx_k are known now)
-            if (k + 1 < NS) {
-                const double *ARn = Ls + O_AR + (k + 1) * (MY * NB) + yl * NB;
-                const double *ALn = Ls + O_AL + (k + 1) * (MY * NB) + yl * NB;
-                double ar[NB], al[NB];
-#pragma unroll
-                for (int j = 0; j < NB; j++) { ar[j] = ARn[j]; al[j] = ALn[j]; }
-                double gy = 0.0;
-                qpb_fence(dxn, dx);
-                qpb_for<0, NB>([&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(gy, dxn, ar[j]);
-                    if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(gy, dx, al[j]);
-                });
-                if (isy) {
-                    const int i = (k + 1) * MY + lane;
-                    Ls[V_DY + i] = RDY * (Ls[V_RY + i] - gy);
-                }
-            }
-            if (k == 0) {
-                const double *AR0 = Ls + O_AR + yl * NB;
-                double ar[NB];
-#pragma unroll
-                for (int j = 0; j < NB; j++) ar[j] = AR0[j];
-                double gy = 0.0;
-                qpb_fence(dx);
-                qpb_for<0, NB>([&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(gy, dx, ar[j]);
-                });
-                if (isy) Ls[V_DY + lane] = RDY * (Ls[V_RY + lane] - gy);
+            if (act && isy) {
+                const int iy = k * MY + c;
+                Ls[V_DY + iy] = RDY * (Ls[V_RY + iy] - gy);
             }
 #endif
-            dxn = dx;
         }
         qpb_wsync();
-    };
-
-    // ---- residuals (Auxilary.c:745-786) of the iterate in LDS; returns the objective
-    // and the four sums rx'rx, ry'ry, rz'rz, s'z
-    auto residuals = [&](double (&red)[4]) -> double {
-        double srx = 0.0, sry = 0.0, srz = 0.0, ssz = 0.0, sfv = 0.0;
-        double xprev = 0.0;
-        // c of the next stage, prefetched (the only input the loop reads from memory)
-        double cnext = QPB_LDS(&a.c[tile * (BNX * QPB_TSTR) + xc * QPB_TSTR + ql]);
-        double hnext = QPB_LDS(&a.h[tile * (BNZ * QPB_TSTR) + zr * QPB_TSTR + ql]);
-#if MY > 0
-        double bnext = QPB_LDS(&a.b[tile * (BNY * QPB_TSTR) + yl * QPB_TSTR + ql]);
-#endif
-#pragma unroll 1
-        for (int k = 0; k < NS; k++) {
-            const double cx = cnext, hz = hnext;
-#if MY > 0
-            const double by = bnext;
-#endif
-            if (k + 1 < NS) {
-                cnext = QPB_LDS(&a.c[tile * (BNX * QPB_TSTR) + ((k + 1) * NB + xc) * QPB_TSTR + ql]);
-                hnext = QPB_LDS(&a.h[tile * (BNZ * QPB_TSTR) + ((k + 1) * MZ + zr) * QPB_TSTR + ql]);
-#if MY > 0
-                bnext = QPB_LDS(&a.b[tile * (BNY * QPB_TSTR) + ((k + 1) * MY + yl) * QPB_TSTR + ql]);
-#endif
-            }
-            const double xk = Ls[V_X + k * NB + xc];
-            const double *Pr = Ls + O_P + k * BLKP + xc * NB;
-            const double *Gk = Ls + O_G + k * (MZ * NB);
-            double pr[NB], gr[NB];
-#pragma unroll
-            for (int j = 0; j < NB; j++) { pr[j] = Pr[j]; gr[j] = Gk[zr * NB + j]; }
-            // x lanes: P x (DPP), G'z and A'y (LDS broadcast reads of z, y)
-            double px = 0.0, ta[4] = {cx, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int r = 0; r < MZ; r++) ta[r & 3] = __builtin_fma(Gk[r * NB + xc], Ls[V_Z + k * MZ + r], ta[r & 3]);
-#if MY > 0
-            const double *ARk = Ls + O_AR + k * (MY * NB);
-#pragma unroll
-            for (int l = 0; l < MY; l++)
-                ta[(MZ + l) & 3] = __builtin_fma(ARk[l * NB + xc], Ls[V_Y + k * MY + l], ta[(MZ + l) & 3]);
-            if (k + 1 < NS) {
-                const double *ALn = Ls + O_AL + (k + 1) * (MY * NB);
-#pragma unroll
-                for (int l = 0; l < MY; l++)
-                    ta[(MZ + MY + l) & 3] =
-                        __builtin_fma(ALn[l * NB + xc], Ls[V_Y + (k + 1) * MY + l], ta[(MZ + MY + l) & 3]);
-            }
-#endif
-            // z lanes: G x;  y lanes: AR_k x_k + AL_k x_{k-1}
-            double gx = 0.0;
-            qpb_fence(xk);
-            qpb_for<0, NB>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                qpb_fx<j>(px, xk, pr[j]);
-                if constexpr ((qpb_bGu >> j) & 1) qpb_fx<j>(gx, xk, gr[j]);
-            });
-            const double rx = -(((ta[0] + ta[1]) + (ta[2] + ta[3])) + px);
-            if (x0) {
-                Ls[V_RX + k * NB + c] = rx;
-                srx = __builtin_fma(rx, rx, srx);
-                sfv = __builtin_fma(xk, __builtin_fma(0.5, px, cx), sfv);   // objective (Auxilary.c:1133-1141)
-            }
-            if (isz) {
-                const int i = k * MZ + lane;
-                const double s = Ls[V_S + i];
-                const double rz = (hz - s) - gx;
-                Ls[V_RZ + i] = rz;
-                srz = __builtin_fma(rz, rz, srz);
-                ssz = __builtin_fma(s, Ls[V_Z + i], ssz);
-            }
-#if MY > 0
-            {
-                const double *ARr = Ls + O_AR + k * (MY * NB) + yl * NB;
-                const double *ALr = Ls + O_AL + k * (MY * NB) + yl * NB;
-                double ar[NB], al[NB];
-#pragma unroll
-                for (int j = 0; j < NB; j++) { ar[j] = ARr[j]; al[j] = ALr[j]; }
-                double ax = 0.0;
-                qpb_fence(xk, xprev);
-                qpb_for<0, NB>([&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(ax, xk, ar[j]);
-                    if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(ax, xprev, al[j]);
-                });
-                if (isy) {
-                    const double ry = by - ax;
-                    Ls[V_RY + k * MY + lane] = ry;
-                    sry = __builtin_fma(ry, ry, sry);
-                }
-            }
-#endif
-            xprev = xk;
-        }
-        qpb_wsync();
-        red[0] = qpb_bsum(srx);
-        red[1] = qpb_bsum(sry);
-        red[2] = qpb_bsum(srz);
-        red[3] = qpb_bsum(ssz);
-        return qpb_bsum(sfv);
     };
 
     // step lengths (Auxilary.c:359-393): alpha = 1 / max(-d / v) over d < 0, 1 if none

@@ -106,7 +106,7 @@ void band_shape(Plan &pl) {
         const long ns = n / nb;
         if (ns < 2 || m % ns || p % ns) continue;
         const long mz = m / ns, my = p / ns;
-        if (mz > 64 || my > 64) continue;
+        if (mz > 64 || my > 16) continue;
         bool ok = true;
         for (long j = 0; j < n && ok; j++) {
             const long sj = j / nb;

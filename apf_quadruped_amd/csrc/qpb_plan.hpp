@@ -120,7 +120,7 @@ int build_plan(Plan &pl, long n, long m, long p, int pmode,
 
 // Multi-stage structure of the plan's P / A / G patterns (fills pl.band_*): the
 // smallest stage width NB <= 16 with n = NB NS, m = MZ NS, p = MY NS (NS >= 2,
-// MZ <= 64, MY <= 64), every P entry inside a stage block, G row r on stage r / MZ
+// MZ <= 64, MY <= 16), every P entry inside a stage block, G row r on stage r / MZ
 // only, A row l on stages l / MY - 1 and l / MY only, and no empty G row.
 void band_shape(Plan &pl);
 

@@ -550,7 +550,7 @@ static BandLayout band_layout(const Plan &pl) {
     L.V_DS = L.V_DZ + nz;
     L.V_W = L.V_DS + nz;
     L.V_Q = L.V_W + nz;
-    L.LDS_QP = L.V_Q + 64;
+    L.LDS_QP = L.V_Q;
     return L;
 }
 
