@@ -527,9 +527,8 @@ def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
 def _sq_record(kname, B):
     """The newest SQ-counter summary for this kernel at this batch (profiles/r0N_sq_*.json,
     scripts/gpu_sq*.sh + scripts/sq_summary.py): row-kernel files key "B=<B>", the tree
-    file "B=<B>", the wave file "<kernel> B=<B>"."""
-    kind = "row" if kname.startswith("qpb_row") else ("tree" if kname.startswith("qpb_tree") else
-                                                      ("wave" if kname.startswith("qpb_wave") else None))
+    and band files "B=<B>", the wave file "<kernel> B=<B>"."""
+    kind = next((k for k in ("row", "tree", "wave", "band") if kname.startswith("qpb_" + k)), None)
     if kind is None:
         return None, None
     for rnd in ("r05", "r04", "r03"):
@@ -719,7 +718,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(seed, args.cpu_sample, args.cpu_passes, args.tol)
 
-    # configs[3] (MPC horizon, N = 380, tree kernel) and the controller's own
+    # configs[3] (MPC horizon, N = 380, band kernel) and the controller's own
     # stance QP (30/68/18), each with its CPU reference
     shapes = None
     if rank == 0 and world == 1 and args.shapes:

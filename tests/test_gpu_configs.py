@@ -191,17 +191,23 @@ def test_config2_four_gait_patterns_group_launch(oracle):
 
 
 @pytest.mark.gpu
-def test_config3_mpc_horizon_tree_kernel(oracle):
+@pytest.mark.parametrize("kernel", ["auto", "tree"])
+def test_config3_mpc_horizon(kernel, oracle):
     """configs[3]: 1 024 MPC-horizon QPs (N = 10 stages, 120/200/60, KKT N = 380) on
-    the tree kernel's 192-thread form (the bench's launch) -- all optimal, KKT
-    residuals < 1e-5, deterministic, a strided sample vs the oracle in the plan's
-    order (1e-9 relative, identical iteration counts)."""
+    the band kernel (auto dispatch: the bench's launch) and on the tree kernel's
+    192-thread form -- all optimal, KKT residuals < 1e-5, deterministic, a strided
+    sample vs the oracle in the plan's order (1e-9 relative, identical iteration
+    counts)."""
     import torch
     from apf_quadruped_amd import plans, workloads as W
+    from apf_quadruped_amd.batch import Plan
     B = 1024
-    plan = plans.standard_plan("mpc_h10")
-    assert plan.kernel_for(B) == "tree" and "_w192_" in plan.kernel_name(B), plan.kernel_name(B)
     d = W.mpc_qp(plans.SEED + 4, np.arange(B))
+    plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel=kernel)
+    if kernel == "auto":
+        assert plan.kernel_for(B) == "band" and plan.kernel_name(B).startswith("qpb_band_"), plan.kernel_name(B)
+    else:
+        assert plan.kernel_for(B) == "tree" and "_w192_" in plan.kernel_name(B), plan.kernel_name(B)
     vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"],
                                                                 d["b"]).items()}
     r1 = plan.unpack(plan.solve(**vals, B=B), B)

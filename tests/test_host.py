@@ -57,10 +57,22 @@ def test_own_ordering_is_a_permutation_and_sparse():
     assert plan.info.lnz <= 138          # no worse than the reference AMD order
 
 
-def test_own_ordering_of_larger_plans_is_min_degree():
+def test_own_ordering_of_larger_plans():
+    """Multi-stage patterns (the MPC horizon) are ordered leaves first -- the band
+    kernel's elimination; other plans beyond the wave kernel's range by minimum degree."""
     from apf_quadruped_amd import plans
     plan = plans.standard_plan("mpc_h10")
-    assert plan.info.ordering == 1 and sorted(plan.perm.tolist()) == list(range(380))
+    assert plan.info.ordering == 3
+    assert plan.perm.tolist() == list(range(180, 380)) + list(range(120, 180)) + list(range(120))
+    rng = np.random.default_rng(5)
+    n, m = 80, 100
+    P = rng.standard_normal((n, n)) * (rng.random((n, n)) < 0.1)
+    P = P @ P.T + np.eye(n)
+    G = rng.standard_normal((m, n)) * (rng.random((m, n)) < 0.1)
+    G[np.arange(m), rng.integers(0, n, m)] = 1.0
+    plan = Plan.from_dense(n, m, 0, P, None, G)
+    assert plan.info.ordering == 1 and sorted(plan.perm.tolist()) == list(range(n + m))
+    assert plan.kernel_for(1024) == "tree"
 
 
 def test_plan_rejects_bad_input():
