@@ -71,10 +71,19 @@ static __device__ __forceinline__ double qpb_bmax(double v) {
 #define QPB_B_TIMING 0    // 1: cycles per phase (w + residuals, factor, predictor, corrector, steps +
                           // updates, staging) into stats instead of the statistics
 #endif
-#if QPB_B_TIMING
+// 2: cycles per part instead: factor stage-parallel / sequential, solve right-hand sides /
+//    forward sweep / backward sweep / directions
+#if QPB_B_TIMING == 1
 #define QPB_BT(k) { const long t2_ = (long)__builtin_readcyclecounter(); tph[k] += (double)(t2_ - tcy); tcy = t2_; }
 #else
 #define QPB_BT(k)
+#endif
+#if QPB_B_TIMING == 2
+#define QPB_BT0() { tcy = (long)__builtin_readcyclecounter(); }
+#define QPB_BT2(k) { const long t2_ = (long)__builtin_readcyclecounter(); tph[k] += (double)(t2_ - tcy); tcy = t2_; }
+#else
+#define QPB_BT0()
+#define QPB_BT2(k)
 #endif
 
 // solve modes: the right-hand side's z part (bx = RX, by = RY in every mode)
@@ -118,20 +127,36 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
     const double *gb = a.b + tile * (BNY1 * QPB_TSTR) + ql;
 
     // ---- stage P, G, A into the per-stage dense blocks; -c, b, h into RX, RY, RZ
-    for (int i = lane; i < O_STATIC_END; i += 64) Ls[i] = 0.0;
+    for (int i = 2 * lane; i < O_STATIC_END; i += 128)      // O_STATIC_END even, 16-byte aligned base
+        *reinterpret_cast<double2 *>(Ls + i) = double2{0.0, 0.0};
     qpb_wsync();
     {
-        const double *tP = a.P + tile * (QPB_NNZP * QPB_TSTR) + ql;
-        for (int k = lane; k < QPB_NNZP; k += 64) {
-            const double v = QPB_LDS(&tP[k * QPB_TSTR]);
-            Ls[qpb_bsP[k]] = v;
-            if (qpb_bsP2[k] >= 0) Ls[qpb_bsP2[k]] = v;
-        }
-        const double *tG = a.G + tile * (QPB_NNZG * QPB_TSTR) + ql;
-        for (int k = lane; k < QPB_NNZG; k += 64) Ls[qpb_bsG[k]] = QPB_LDS(&tG[k * QPB_TSTR]);
+        // eight values per lane in flight per round (their loads issued before the stores)
+        auto scatter = [&](const double *src, auto nnzc, const int *slot, const int *slot2) {
+            constexpr int NNZ = decltype(nnzc)::value;
+#pragma unroll 1
+            for (int k0 = 0; k0 < NNZ; k0 += 512) {
+                double v[8];
+                int s1[8], s2[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const int k = k0 + 64 * u + lane;
+                    const bool ok = k < NNZ;
+                    v[u] = ok ? QPB_LDS(&src[k * QPB_TSTR]) : 0.0;
+                    s1[u] = ok ? slot[k] : -1;
+                    s2[u] = (ok && slot2) ? slot2[k] : -1;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    if (s1[u] >= 0) Ls[s1[u]] = v[u];
+                    if (s2[u] >= 0) Ls[s2[u]] = v[u];
+                }
+            }
+        };
+        scatter(a.P + tile * (QPB_NNZP * QPB_TSTR) + ql, qpb_ic<QPB_NNZP>{}, qpb_bsP, qpb_bsP2);
+        scatter(a.G + tile * (QPB_NNZG * QPB_TSTR) + ql, qpb_ic<QPB_NNZG>{}, qpb_bsG, nullptr);
 #if MY > 0
-        const double *tA = a.A + tile * (QPB_NNZA * QPB_TSTR) + ql;
-        for (int k = lane; k < QPB_NNZA; k += 64) Ls[qpb_bsA[k]] = QPB_LDS(&tA[k * QPB_TSTR]);
+        scatter(a.A + tile * (QPB_NNZA * QPB_TSTR) + ql, qpb_ic<QPB_NNZA>{}, qpb_bsA, nullptr);
 #endif
         for (int i = lane; i < BNX; i += 64) Ls[V_RX + i] = -QPB_LDS(&gc[i * QPB_TSTR]);
 #if MY > 0
@@ -276,10 +301,16 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
     // forms H_kk = P_k + G_k'W_k G_k + 1e7 (AR_k'AR_k + AL_{k+1}'AL_{k+1}) and X_k for the
     // four stages of the round (row R: stage k + R, in registers); then the stages'
     // sequential parts: Z_k = X_k L_{k-1}^-T, H_kk -= Z_k D_{k-1}^-1 Z_k', the pivots.
-    auto factor = [&]() {
+    // reg: pivots regularised inline (ldl.c:273-274).  The fast pass (reg = false) takes
+    // every 1/D as v_rcp_f64 + Newton; the caller redoes the factor with reg = true when
+    // a stored 1/D shows a pivot |D| <= 1e-14 (rare) -- otherwise the same operations,
+    // so the same bits.
+    auto factor = [&](auto regc) {
+        constexpr bool REG = decltype(regc)::value != 0;
         double H[NB], Xr[NB];
 #pragma unroll 1
         for (int k = 0; k < NS; k++) {
+            QPB_BT0();
             if ((k & 3) == 0) {
                 const int ks = k + R;
                 const int kc = ks < NS ? ks : NS - 1;
@@ -333,6 +364,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 });
 #endif
             }
+            QPB_BT2(0);
             const int kr = k & 3;                   // the row holding stage k's block
             double Hs[NB];
 #pragma unroll
@@ -375,7 +407,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             double dpiv = qpb_nb<0>(Hs[0]);
             qpb_for<0, NB>([&](auto kc2) {
                 constexpr int kk = decltype(kc2)::value;
-                const double rd = qpb_rcp_reg(dpiv);
+                const double rd = REG ? qpb_rcp_reg(dpiv) : qpb_rcp_nr(dpiv);
                 double nl = Hs[kk] * -rd;
                 asm volatile("" : "+v"(nl));
                 if constexpr (kk + 1 < NB) {
@@ -396,6 +428,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 Lr[NB] = rDd;
             }
             qpb_wsync();
+            QPB_BT2(1);
         }
     };
 
@@ -417,6 +450,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         return __builtin_fma(-cc, rzi, rz + s);
     };
     auto solve = [&](int mode, double smu, bool pcd) {
+        QPB_BT0();
         // stage-parallel: t_k = bx_k + G_k'(w o bz) + 1e7 (AR_k' by_k + AL_{k+1}' by_{k+1}) -> DX
 #pragma unroll 1
         for (int i = 0; i < NR; i++) {
@@ -454,6 +488,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             if (act && isx) Ls[V_DX + k * NB + c] = (ta[0] + ta[1]) + (ta[2] + ta[3]);
         }
         qpb_wsync();
+        QPB_BT2(2);
         // forward sweep: u_k = L_k^-1 (t_k - Z_k v_{k-1}), v_k = D_k^-1 u_k -> DX
         double vprev = 0.0;
 #pragma unroll 1
@@ -480,6 +515,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             if (st0) Ls[V_DX + k * NB + c] = vprev;
         }
         qpb_wsync();
+        QPB_BT2(3);
         // backward sweep: dx_k = L_k^-T (v_k - D_k^-1 Z_{k+1}' dx_{k+1}) -> DX
         double dxn = 0.0;
 #pragma unroll 1
@@ -511,6 +547,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             dxn = r;
         }
         qpb_wsync();
+        QPB_BT2(4);
         // stage-parallel: dz = w (G dx - bz) (+ ds in the corrector), dy = -1e7 (by - A dx)
 #pragma unroll 1
         for (int i = 0; i < NR; i++) {
@@ -569,6 +606,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #endif
         }
         qpb_wsync();
+        QPB_BT2(5);
     };
 
     // step lengths (Auxilary.c:359-393): alpha = 1 / max(-d / v) over d < 0, 1 if none
@@ -613,7 +651,15 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         }
         const double rsz = qpb_rcp(red[3]);
         QPB_BT(0);
-        factor();
+        factor(qpb_ic<0>{});
+        {
+            bool tiny = false;      // any |D| <= 1e-14: |1/D| >= 1e14 (or not finite)
+            for (int i = lane; i < BNX; i += 64) {
+                const double rdv = Ls[O_L + (i / NB) * (NB * RS) + (i % NB) * RS + NB];
+                tiny |= !(__builtin_fabs(rdv) < 1e14);
+            }
+            if (qpb_any(tiny)) factor(qpb_ic<1>{});
+        }
         QPB_BT(1);
         if (it < 0) {
             // setup solve, rhs [-c; b; h]: x0, y0; s0, z0 from -dz (Auxilary.c:1010-1040)

@@ -536,7 +536,7 @@ static BandLayout band_layout(const Plan &pl) {
     L.O_G = L.O_Z + ns * nb * nb;
     L.O_AR = L.O_G + ns * mz * nb;
     L.O_AL = L.O_AR + ns * my * nb;
-    L.O_STATIC_END = L.O_AL + ns * my * nb;
+    L.O_STATIC_END = (L.O_AL + ns * my * nb + 1) & ~1L;   // even: 16-byte zero-fill stores
     L.V_X = L.O_STATIC_END;
     L.V_RX = L.V_X + nx;
     L.V_DX = L.V_RX + nx;

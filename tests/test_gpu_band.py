@@ -136,3 +136,34 @@ def test_band_kernel_stage_shapes_vs_oracle(shape, p_upper, oracle):
         assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (shape, q, r["iters"][q], o["iters"])
         for k in ("x", "z", "s") + (("y",) if p else ()):
             _close(r[k][q], o[k], f"{shape}[{q}].{k}", 1e-7)
+
+
+@pytest.mark.gpu
+def test_band_kernel_regularised_pivot_vs_oracle(oracle):
+    """A variable with no cost and no constraint row gives a zero pivot: the fast
+    factor pass sees |D| <= 1e-14 and the factor is redone with the reference's
+    regularisation (ldl.c:273-274), as the oracle does."""
+    from apf_quadruped_amd import workloads as W
+    from apf_quadruped_amd.batch import Plan
+    B = 4
+    d = stage_qp(6, 4, 8, 2, B=B, seed=11)
+    dead = 8                                           # stage 1, variable 2
+    for key in ("P", "G", "A"):
+        d[key][:, :, dead] = 0.0
+    d["P"][:, dead, :] = 0.0
+    d["c"][:, dead] = 0.0
+    for r in range(d["m"]):                            # keep every G row non-empty
+        if not d["G"][0, r].any():
+            st = r // 8
+            d["G"][:, r, 6 * st] = 1.0
+    d["h"] = np.einsum("bij,bj->bi", d["G"], np.zeros((B, d["n"]))) + 1.0
+    d["b"] = np.zeros((B, d["p"]))
+    n, m, p = d["n"], d["m"], d["p"]
+    plan = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0], kernel="band")
+    r = _run(plan, d, B)
+    Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    for q in range(B):
+        o = oracle.solve_dense(n, m, p, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm)
+        assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (q, r["iters"][q], o["iters"])
+        for k in ("x", "z", "s"):
+            _close(r[k][q], o[k], f"reg[{q}].{k}", 1e-7)
