@@ -13,7 +13,7 @@ def main():
     ap.add_argument("--batch", type=int, default=262144)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--exact", action="store_true")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave", "tree"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "wave", "tree", "band"])
     ap.add_argument("--shape", default="c1", help="plans.standard_qp name (c1, mpc_h10, ...)")
     a = ap.parse_args()
     import torch

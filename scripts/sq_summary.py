@@ -5,6 +5,7 @@ scripts/gpu_sq_tree.sh (the tree kernel on MPC QPs, one QP per workgroup).
 
     python scripts/sq_summary.py gpurun_out/sq profiles/r02_sq_row.json
     python scripts/sq_summary.py gpurun_out/sqt profiles/r02_sq_tree.json tree
+    python scripts/sq_summary.py gpurun_out/sqb profiles/r05_sq_band.json band
 
 Units (MI355X_MICROARCH.md, rocprofv3 PMC): SQ_WAVE_CYCLES / SQ_WAIT_* /
 SQ_ACTIVE_INST_* count quad-cycles summed over waves; SQ_INSTS_* count wave
@@ -39,9 +40,11 @@ def load(d, prefix="qpb_row", by_name=False):
 
 def main():
     src, out = sys.argv[1], sys.argv[2]
-    tree = len(sys.argv) > 3 and sys.argv[3] == "tree"
+    band = len(sys.argv) > 3 and sys.argv[3] == "band"     # one MPC QP per wavefront (block-tridiagonal)
+    tree = (len(sys.argv) > 3 and sys.argv[3] == "tree") or band
     wave = len(sys.argv) > 3 and sys.argv[3] == "wave"      # one QP per wavefront (controller shapes)
-    vals, dur, wgs = load(src, "qpb_tree" if tree else ("qpb_wave" if wave else "qpb_row"), by_name=wave)
+    vals, dur, wgs = load(src, "qpb_band" if band else ("qpb_tree" if tree else ("qpb_wave" if wave else "qpb_row")),
+                          by_name=wave)
     res = {}
     for grid in sorted({g for g, _ in vals}):
         c = {n: sum(v) / len(v) for (g, n), v in vals.items() if g == grid}
@@ -60,7 +63,11 @@ def main():
         fma_lane = c["SQ_INSTS_VALU_FMA_F64"] * 64 / B
         flops_issued = (2 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"]) * 64
         wps = wc / (SIMDS * cyc)
-        if tree:
+        if band:
+            kind = (f"one QP per wavefront, two per CU: {wps:.2f} waves per SIMD on average over the launch, SIMD VALU "
+                    f"busy {c['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * cyc):.0%}, a wave waits {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.0%} "
+                    f"of its cycles (LDS)")
+        elif tree:
             kind = (f"one QP's step chain: {wps:.2f} waves per SIMD on average over the launch, SIMD VALU busy "
                     f"{c['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * cyc):.0%}, a wave waits {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.0%} "
                     f"of its cycles (LDS / descriptor loads / barriers)")
@@ -87,7 +94,9 @@ def main():
             "fp64_issue_frac_of_peak": flops_issued / (FP64_PEAK_FLOP_PER_CYC_SIMD * SIMDS * cyc),
             "counters": c,
         }
-    res["reading"] = ("controller-shape QPs (30 variables), one QP per wavefront: the dense LDL' and the "
+    res["reading"] = ("MPC (N = 380) on the band kernel: one QP per wavefront, LDS-resident state (80 KB: two QPs "
+                      "per CU, two SIMDs of four busy); the stage recurrences (Schur complement, pivots, sweeps) are "
+                      "the chain; no descriptor tables (SALU = loop control only)") if band else ("controller-shape QPs (30 variables), one QP per wavefront: the dense LDL' and the "
                       "triangular solves are one wave's dependency chain; see DESIGN §4b") if wave else ("MPC (N = 380): one QP alone runs 6 passes of ~118 gather / panel steps each (~1 us per "
                       "step: descriptor wait, LDS terms, butterfly, epilogue, barrier); at 1 024 QPs (4 per CU) the "
                       "average wave lives ~0.98 ms of the 1.65 ms launch -- the launch is as long as the slowest QP "
@@ -98,7 +107,7 @@ def main():
                       "SIMD's VALU busy most cycles: issue-bound, not HBM- (6-7 % of 8 TB/s) or FP64-bound; FP64 "
                       "lane-FMAs per QP are ~3.8x the algorithmic count (16 lanes per QP, sparse G rows and the "
                       "dense-row LDL' update every lane)")
-    if tree:
+    if tree and not band:
         for k, v in res.items():
             if isinstance(v, dict):
                 v.pop("fp64_issue_frac_of_peak", None)
