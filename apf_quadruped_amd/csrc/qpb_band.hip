@@ -46,12 +46,15 @@
 #define ZS ((MZ + 15) / 16)       // z sub-rows of a DPP row (z rows c, c + 16, ..)
 #define NR ((NS + 3) / 4)         // rounds of the stage-parallel passes (four stages each)
 // per-stage blocks and vectors (doubles; offsets emitted by the generator, qpb_wave.cpp
-// band_layout): O_P P_k rows (stride NB), O_L rows of -L_k at stride RS = NB + 1 (zeros
-// from the diagonal on, 1 / D_c at column NB), O_Z rows of -Z_k (stride NB), O_G G_k rows,
-// O_AR / O_AL the A row groups' stage-k / stage-(k-1) parts (stride NB); the vectors
-// x, rx, dx | y, ry, dy | z, s, rz, dz, ds, w in natural order.
+// band_layout), packed by pattern so that three QPs share a CU: O_P P_k's upper triangle
+// (PP per stage, (i, j) at j (j + 1) / 2 + i), O_L -L_k's strict lower triangle (LP per
+// stage, row c from c (c - 1) / 2), O_RD 1 / D_k, O_Z rows of -Z_k (NB x NB), O_G G_k on
+// the union of the stages' G patterns (GS per stage, the last slot zero; per-lane
+// position tables qpb_bgc / qpb_bgr), O_AR / O_AL the A row groups' stage-k /
+// stage-(k-1) parts (dense rows), O_DUMP one slot per lane for masked stores; the
+// vectors x, rx, dx | y, ry, dy | z, s, rz, dz, ds in natural order (w = -1 / reg(-s/z)
+// is formed where it is used).
 #define BLKP (NB * NB)
-#define BLKL (NB * RS)
 static_assert(NB >= 1 && NB <= 16 && MZ >= 1 && MZ <= 64 && MY <= 16 && NS >= 2, "band kernel sizes");
 
 // 64-lane sums / maxima: the row butterfly, then the four row results (fixed order)
@@ -121,6 +124,18 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         zrc[u] = isz[u] ? c + 16 * u : MZ - 1;
     }
     const bool st0 = R == 0 && isx;            // the x lanes that store in sequential passes
+    // per-lane positions in the packed blocks: P_k row xc, G_k column xc (x lanes) and
+    // rows zrc[u] (z lanes), -L_k row xc from lb
+    int pidx[NB], gic[MZ], gir[ZS][NB];
+#pragma unroll
+    for (int j = 0; j < NB; j++) pidx[j] = xc <= j ? j * (j + 1) / 2 + xc : xc * (xc + 1) / 2 + j;
+#pragma unroll
+    for (int r = 0; r < MZ; r++) gic[r] = qpb_bgc[xc][r];
+#pragma unroll
+    for (int u = 0; u < ZS; u++)
+#pragma unroll
+        for (int j = 0; j < NB; j++) gir[u][j] = qpb_bgr[zrc[u]][j];
+    const int lb = xc * (xc - 1) / 2;
     constexpr double RDY = 1.0 / -1e-7;        // leaf y pivots: D = 0 regularised to -1e-7
     const double *gc = a.c + tile * (BNX * QPB_TSTR) + ql;
     const double *gh = a.h + tile * (BNZ * QPB_TSTR) + ql;
@@ -153,7 +168,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 }
             }
         };
-        scatter(a.P + tile * (QPB_NNZP * QPB_TSTR) + ql, qpb_ic<QPB_NNZP>{}, qpb_bsP, qpb_bsP2);
+        scatter(a.P + tile * (QPB_NNZP * QPB_TSTR) + ql, qpb_ic<QPB_NNZP>{}, qpb_bsP, nullptr);
         scatter(a.G + tile * (QPB_NNZG * QPB_TSTR) + ql, qpb_ic<QPB_NNZG>{}, qpb_bsG, nullptr);
 #if MY > 0
         scatter(a.A + tile * (QPB_NNZA * QPB_TSTR) + ql, qpb_ic<QPB_NNZA>{}, qpb_bsA, nullptr);
@@ -173,19 +188,41 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
     qpb_wsync();
     QPB_BT(5);
 
-    // the KKT diagonal's w = -1 / regularise(-s / z) per z row (kkt_initialize: -I, w = 1)
-    auto w_pass = [&](bool setup) {
-        for (int i = lane; i < BNZ; i += 64)
-            Ls[V_W + i] = setup ? 1.0 : -qpb_rcp_reg(-Ls[V_S + i] * qpb_rcp(Ls[V_Z + i]));
-        qpb_wsync();
+    // the KKT diagonal's w = -1 / regularise(-s / z) of z row iz (kkt_initialize: -I, w = 1)
+    bool wset = true;
+    auto wz = [&](int iz) -> double {
+        return wset ? 1.0 : -qpb_rcp_reg(-Ls[V_S + iz] * qpb_rcp(Ls[V_Z + iz]));
     };
 
     // this row's stage slices (stage kc): column xc of G_k, AR_k, AL_k, AL_{k+1} (the last
     // zero when k + 1 = NS), rows zrc[u] of G_k, row yc of AR_k and AL_k
     auto col_G = [&](int kc, double (&g)[MZ]) {
-        const double *Gk = Ls + O_G + kc * (MZ * NB) + xc;
+        const double *Gk = Ls + O_G + kc * GS;
 #pragma unroll
-        for (int r = 0; r < MZ; r++) g[r] = Gk[r * NB];
+        for (int r = 0; r < MZ; r++) g[r] = Gk[gic[r]];
+    };
+    auto row_G = [&](int kc, double (&g)[ZS][NB]) {
+        const double *Gk = Ls + O_G + kc * GS;
+#pragma unroll
+        for (int u = 0; u < ZS; u++)
+#pragma unroll
+            for (int j = 0; j < NB; j++) g[u][j] = Gk[gir[u][j]];
+    };
+    auto row_P = [&](int kc, double (&pr)[NB]) {
+        const double *Pk = Ls + O_P + kc * PP;
+#pragma unroll
+        for (int j = 0; j < NB; j++) pr[j] = Pk[pidx[j]];
+    };
+    // row xc / column xc of -L_k (zero from the diagonal on)
+    auto row_L = [&](int k, double (&nl)[NB]) {
+        const double *Lk = Ls + O_L + k * LP + lb;
+#pragma unroll
+        for (int f = 0; f < NB; f++) nl[f] = f < xc ? Lk[f] : 0.0;
+    };
+    auto col_L = [&](int k, double (&lt)[NB]) {
+        const double *Lk = Ls + O_L + k * LP + xc;
+#pragma unroll
+        for (int e = 0; e < NB; e++) lt[e] = e > xc ? Lk[e * (e - 1) / 2] : 0.0;
     };
     auto col_A = [&](int off, int kc, double (&v)[MY1]) {
         const double *Ak = Ls + off + kc * (MY * NB) + xc;
@@ -214,15 +251,8 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             const double xk = Ls[V_X + kc * NB + xc];
             const double xp = kc > 0 ? Ls[V_X + (kc - 1) * NB + xc] : 0.0;
             double pr[NB], gr[ZS][NB], gcl[MZ];
-            const double *Pr = Ls + O_P + kc * (NB * NB) + xc * NB;
-#pragma unroll
-            for (int j = 0; j < NB; j++) pr[j] = Pr[j];
-#pragma unroll
-            for (int u = 0; u < ZS; u++) {
-                const double *Gr = Ls + O_G + kc * (MZ * NB) + zrc[u] * NB;
-#pragma unroll
-                for (int j = 0; j < NB; j++) gr[u][j] = Gr[j];
-            }
+            row_P(kc, pr);
+            row_G(kc, gr);
             col_G(kc, gcl);
             double ta[4] = {cx, 0.0, 0.0, 0.0}, px = 0.0, gx[ZS];
 #pragma unroll
@@ -315,20 +345,18 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 const int ks = k + R;
                 const int kc = ks < NS ? ks : NS - 1;
                 const bool nxt = kc + 1 < NS;
-                const double *Pr = Ls + O_P + kc * (NB * NB) + xc * NB;
-#pragma unroll
-                for (int j = 0; j < NB; j++) H[j] = Pr[j];
-                double gcl[MZ], wz[ZS];
+                row_P(kc, H);
+                double gcl[MZ], wr[ZS];
                 col_G(kc, gcl);
 #pragma unroll
-                for (int u = 0; u < ZS; u++) wz[u] = Ls[V_W + kc * MZ + zrc[u]];
+                for (int u = 0; u < ZS; u++) wr[u] = wz(kc * MZ + zrc[u]);
                 // + G_k' W_k G_k: four rows' products G(r, c) w_r first, then their DPP FMAs
                 qpb_for<0, (MZ + 3) / 4>([&](auto qc4) {
                     constexpr int r0 = 4 * decltype(qc4)::value;
                     double cr[4];
                     qpb_for<0, 4>([&](auto uc) {
                         constexpr int r = r0 + decltype(uc)::value;
-                        if constexpr (r < MZ) cr[decltype(uc)::value] = gcl[r] * qpb_nb<(r & 15)>(wz[r >> 4]);
+                        if constexpr (r < MZ) cr[decltype(uc)::value] = gcl[r] * qpb_nb<(r & 15)>(wr[r >> 4]);
                         else cr[decltype(uc)::value] = 0.0;
                     });
                     asm volatile("" : "+v"(cr[0]), "+v"(cr[1]), "+v"(cr[2]), "+v"(cr[3]));
@@ -371,11 +399,11 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             for (int j = 0; j < NB; j++) Hs[j] = H[j];
 #if MY > 0
             if (k > 0) {
-                const double *Lp = Ls + O_L + (k - 1) * (NB * RS) + xc * RS;
                 double nLp[NB], Zr[NB];
+                row_L(k - 1, nLp);
 #pragma unroll
-                for (int f = 0; f < NB; f++) { nLp[f] = Lp[f]; Zr[f] = Xr[f]; }
-                const double rdp = Lp[NB];
+                for (int f = 0; f < NB; f++) Zr[f] = Xr[f];
+                const double rdp = Ls[O_RD + (k - 1) * NB + xc];
                 // Z(c, e) = X(c, e) - sum_{f<e} L_{k-1}(e, f) Z(c, f): lane e's -L row broadcast,
                 // right-looking (each Z(c, e) sums over f in ascending order)
                 qpb_for<0, NB - 1>([&](auto fc) {
@@ -422,10 +450,10 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 Hs[kk] = xc > kk ? nl : 0.0;
             });
             if (R == kr && isx) {
-                double *Lr = Ls + O_L + k * (NB * RS) + c * RS;
+                const int lrow = O_L + k * LP + c * (c - 1) / 2;
 #pragma unroll
-                for (int f = 0; f < NB; f++) Lr[f] = Hs[f];
-                Lr[NB] = rDd;
+                for (int f = 0; f < NB; f++) Ls[f < c ? lrow + f : O_DUMP + lane] = Hs[f];
+                Ls[O_RD + k * NB + c] = rDd;
             }
             qpb_wsync();
             QPB_BT2(1);
@@ -463,7 +491,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             for (int u = 0; u < ZS; u++) {
                 double cc;
                 const int iz = kc * MZ + zrc[u];
-                v[u] = Ls[V_W + iz] * bz_of(mode, iz, smu, pcd, &cc);
+                v[u] = wz(iz) * bz_of(mode, iz, smu, pcd, &cc);
             }
             col_G(kc, gcl);
             double ta[4] = {Ls[V_RX + kc * NB + xc], 0.0, 0.0, 0.0};
@@ -494,11 +522,9 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #pragma unroll 1
         for (int k = 0; k < NS; k++) {
             double t = Ls[V_DX + k * NB + xc];
-            const double *Lr = Ls + O_L + k * (NB * RS) + xc * RS;
             double nl[NB];
-#pragma unroll
-            for (int f = 0; f < NB; f++) nl[f] = Lr[f];
-            const double rd = Lr[NB];
+            row_L(k, nl);
+            const double rd = Ls[O_RD + k * NB + xc];
 #if MY > 0
             if (k > 0) {
                 const double *Zr = Ls + O_Z + k * (NB * NB) + xc * NB;
@@ -520,12 +546,10 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         double dxn = 0.0;
 #pragma unroll 1
         for (int k = NS - 1; k >= 0; k--) {
-            const double *Lk = Ls + O_L + k * (NB * RS);
             double r = Ls[V_DX + k * NB + xc];
             double lt[NB];
-#pragma unroll
-            for (int e = 0; e < NB; e++) lt[e] = Lk[e * RS + xc];      // -L(e, c): column c
-            const double rd = Lk[xc * RS + NB];
+            col_L(k, lt);                                                  // -L(e, c): column c
+            const double rd = Ls[O_RD + k * NB + xc];
 #if MY > 0
             if (k + 1 < NS) {
                 const double *Zn = Ls + O_Z + (k + 1) * (NB * NB) + xc;    // -Z_{k+1}, by columns
@@ -556,13 +580,9 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             const int kc = act ? k : NS - 1;
             const double dxk = Ls[V_DX + kc * NB + xc];
             double gr[ZS][NB], gz[ZS];
+            row_G(kc, gr);
 #pragma unroll
-            for (int u = 0; u < ZS; u++) {
-                const double *Gr = Ls + O_G + kc * (MZ * NB) + zrc[u] * NB;
-#pragma unroll
-                for (int j = 0; j < NB; j++) gr[u][j] = Gr[j];
-                gz[u] = 0.0;
-            }
+            for (int u = 0; u < ZS; u++) gz[u] = 0.0;
 #if MY > 0
             const double dxp = kc > 0 ? Ls[V_DX + (kc - 1) * NB + xc] : 0.0;
             double arr[NB], alr[NB], gy = 0.0;
@@ -590,7 +610,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                     const int iz = k * MZ + c + 16 * u;
                     double cc = 0.0;
                     const double bz = bz_of(mode, iz, smu, pcd, &cc);
-                    const double dz = Ls[V_W + iz] * (gz[u] - bz);
+                    const double dz = wz(iz) * (gz[u] - bz);
                     Ls[V_DZ + iz] = dz;
                     if (mode == BM_CORR) {
                         const double s = Ls[V_S + iz], rzi = qpb_rcp(Ls[V_Z + iz]);
@@ -633,7 +653,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
     double fv = 0.0, st_rx2 = 0.0, st_ry2 = 0.0, st_rz2 = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;
     for (;;) {
         if (it >= 0 && it >= a.maxit) { itq = it; flag = 2; break; }
-        w_pass(it < 0);
+        wset = it < 0;
         double red[4] = {0.0, 0.0, 0.0, 1.0};
         double mu = 0.0;
         bool pc = true;
@@ -654,10 +674,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         factor(qpb_ic<0>{});
         {
             bool tiny = false;      // any |D| <= 1e-14: |1/D| >= 1e14 (or not finite)
-            for (int i = lane; i < BNX; i += 64) {
-                const double rdv = Ls[O_L + (i / NB) * (NB * RS) + (i % NB) * RS + NB];
-                tiny |= !(__builtin_fabs(rdv) < 1e14);
-            }
+            for (int i = lane; i < BNX; i += 64) tiny |= !(__builtin_fabs(Ls[O_RD + i]) < 1e14);
             if (qpb_any(tiny)) factor(qpb_ic<1>{});
         }
         QPB_BT(1);

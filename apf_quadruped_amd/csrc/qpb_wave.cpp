@@ -519,24 +519,40 @@ std::string generate_wave_kernel(const Plan &pl, int wg, std::string *name_out) 
 
 namespace qpb {
 
-// LDS layout of the band kernel (qpb_band.hip), doubles per QP
+// LDS layout of the band kernel (qpb_band.hip), doubles per QP: packed stage blocks
+// (P_k upper triangle, strictly lower -L_k, G_k on the union of the stages' G patterns)
 struct BandLayout {
-    long RS, O_P, O_L, O_Z, O_G, O_AR, O_AL, O_STATIC_END;
-    long V_X, V_RX, V_DX, V_Y, V_RY, V_DY, V_Z, V_S, V_RZ, V_DZ, V_DS, V_W, V_Q, LDS_QP;
+    long PP, LP, GS, O_P, O_L, O_RD, O_Z, O_G, O_AR, O_AL, O_DUMP, O_STATIC_END;
+    long V_X, V_RX, V_DX, V_Y, V_RY, V_DY, V_Z, V_S, V_RZ, V_DZ, V_DS, LDS_QP;
 };
+
+// (row, column) pairs of the stage-relative G pattern, union over the stages, row-major
+static std::vector<std::pair<long, long>> band_gunion(const Plan &pl) {
+    const long nb = pl.band_nb, mz = pl.band_mz;
+    std::vector<std::pair<long, long>> u;
+    for (long j = 0; j < pl.n; j++)
+        for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1]; k++) u.push_back({pl.G.ir[k] % mz, j % nb});
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    return u;
+}
 
 static BandLayout band_layout(const Plan &pl) {
     const long nb = pl.band_nb, ns = pl.band_ns, mz = pl.band_mz, my = pl.band_my;
     const long nx = nb * ns, nz = mz * ns, ny = my * ns, ny1 = ny > 0 ? ny : 1;
     BandLayout L;
-    L.RS = nb + 1;
+    L.PP = nb * (nb + 1) / 2;
+    L.LP = nb * (nb - 1) / 2;
+    L.GS = (long)band_gunion(pl).size() + 1;          // + a zero slot
     L.O_P = 0;
-    L.O_L = L.O_P + ns * nb * nb;
-    L.O_Z = L.O_L + ns * nb * L.RS;
+    L.O_L = L.O_P + ns * L.PP;
+    L.O_RD = L.O_L + ns * L.LP;
+    L.O_Z = L.O_RD + ns * nb;
     L.O_G = L.O_Z + ns * nb * nb;
-    L.O_AR = L.O_G + ns * mz * nb;
+    L.O_AR = L.O_G + ns * L.GS;
     L.O_AL = L.O_AR + ns * my * nb;
-    L.O_STATIC_END = (L.O_AL + ns * my * nb + 1) & ~1L;   // even: 16-byte zero-fill stores
+    L.O_DUMP = L.O_AL + ns * my * nb;                 // one slot per lane (masked stores)
+    L.O_STATIC_END = (L.O_DUMP + 64 + 1) & ~1L;       // even: 16-byte zero-fill stores
     L.V_X = L.O_STATIC_END;
     L.V_RX = L.V_X + nx;
     L.V_DX = L.V_RX + nx;
@@ -548,9 +564,7 @@ static BandLayout band_layout(const Plan &pl) {
     L.V_RZ = L.V_S + nz;
     L.V_DZ = L.V_RZ + nz;
     L.V_DS = L.V_DZ + nz;
-    L.V_W = L.V_DS + nz;
-    L.V_Q = L.V_W + nz;
-    L.LDS_QP = L.V_Q;
+    L.LDS_QP = L.V_DS + nz;
     return L;
 }
 
@@ -593,10 +607,12 @@ std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
       << "\n";
     const long nP = pl.Pin.nnz(), nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz();
     o << "#define QPB_NNZP " << nP << "\n#define QPB_NNZA " << nA << "\n#define QPB_NNZG " << nG << "\n";
-    const char *names[] = {"RS", "O_P", "O_L", "O_Z", "O_G", "O_AR", "O_AL", "O_STATIC_END", "V_X", "V_RX", "V_DX",
-                           "V_Y", "V_RY", "V_DY", "V_Z", "V_S", "V_RZ", "V_DZ", "V_DS", "V_W", "V_Q", "LDS_QP"};
-    const long vals[] = {L.RS, L.O_P, L.O_L, L.O_Z, L.O_G, L.O_AR, L.O_AL, L.O_STATIC_END, L.V_X, L.V_RX, L.V_DX,
-                         L.V_Y, L.V_RY, L.V_DY, L.V_Z, L.V_S, L.V_RZ, L.V_DZ, L.V_DS, L.V_W, L.V_Q, L.LDS_QP};
+    const char *names[] = {"PP", "LP", "GS", "O_P", "O_L", "O_RD", "O_Z", "O_G", "O_AR", "O_AL", "O_DUMP",
+                           "O_STATIC_END", "V_X", "V_RX", "V_DX", "V_Y", "V_RY", "V_DY", "V_Z", "V_S", "V_RZ", "V_DZ",
+                           "V_DS", "LDS_QP"};
+    const long vals[] = {L.PP, L.LP, L.GS, L.O_P, L.O_L, L.O_RD, L.O_Z, L.O_G, L.O_AR, L.O_AL, L.O_DUMP,
+                         L.O_STATIC_END, L.V_X, L.V_RX, L.V_DX, L.V_Y, L.V_RY, L.V_DY, L.V_Z, L.V_S, L.V_RZ, L.V_DZ,
+                         L.V_DS, L.LDS_QP};
     for (size_t i = 0; i < sizeof vals / sizeof vals[0]; i++) o << "#define " << names[i] << " " << vals[i] << "\n";
     // CSC value -> LDS slot of the stage blocks
     std::vector<long> pcol(nP), acol(nA), gcol(nG);
@@ -606,17 +622,38 @@ std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
             for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++) acol[k] = j;
         for (long k = pl.G.jc[j]; k < pl.G.jc[j + 1]; k++) gcol[k] = j;
     }
-    auto pslot = [&](long i, long j) { return L.O_P + (j / nb) * nb * nb + (i % nb) * nb + (j % nb); };
+    // P_k packed upper: (i, j), i <= j, at j (j + 1) / 2 + i (both triangles of a full P
+    // land on the same slot)
+    auto pslot = [&](long i, long j) {
+        const long a = std::min(i % nb, j % nb), b = std::max(i % nb, j % nb);
+        return L.O_P + (j / nb) * L.PP + b * (b + 1) / 2 + a;
+    };
     table(o, "static __device__ const int qpb_bsP", nP, [&](long k) { return pslot(pl.Pin.ir[k], pcol[k]); });
-    table(o, "static __device__ const int qpb_bsP2", nP, [&](long k) {
-        const long i = pl.Pin.ir[k], j = pcol[k];
-        return (pl.pmode == P_UPPER && i != j) ? pslot(j, i) : -1L;
-    });
+    // G_k on the union pattern; per-lane position tables (the zero slot GS - 1 where the
+    // union has no entry): column c's rows (x lanes), row r's columns (z lanes)
+    const std::vector<std::pair<long, long>> gu = band_gunion(pl);
+    auto gpos = [&](long r, long j) {
+        auto it = std::lower_bound(gu.begin(), gu.end(), std::make_pair(r, j));
+        return (it != gu.end() && *it == std::make_pair(r, j)) ? (long)(it - gu.begin()) : L.GS - 1;
+    };
+    o << "static __device__ const unsigned short qpb_bgc[16][" << mz << "] = {";
+    for (long cc = 0; cc < 16; cc++) {
+        o << (cc ? "," : "") << "{";
+        for (long r = 0; r < mz; r++) o << (r ? "," : "") << (cc < nb ? gpos(r, cc) : L.GS - 1);
+        o << "}";
+    }
+    o << "};\nstatic __device__ const unsigned short qpb_bgr[64][" << nb << "] = {";
+    for (long r = 0; r < 64; r++) {
+        o << (r ? "," : "") << "{";
+        for (long j = 0; j < nb; j++) o << (j ? "," : "") << (r < mz ? gpos(r, j) : L.GS - 1);
+        o << "}";
+    }
+    o << "};\n";
     std::vector<unsigned> gm(mz, 0), arm(my > 0 ? my : 1, 0), alm(my > 0 ? my : 1, 0);
     table(o, "static __device__ const int qpb_bsG", nG, [&](long k) {
         const long r = pl.G.ir[k], j = gcol[k];
         gm[r % mz] |= 1u << (j % nb);
-        return L.O_G + (r / mz) * mz * nb + (r % mz) * nb + (j % nb);
+        return L.O_G + (r / mz) * L.GS + gpos(r % mz, j % nb);
     });
     table(o, "static __device__ const int qpb_bsA", nA, [&](long k) {
         const long l = pl.A.ir[k], j = acol[k], st = l / my;
