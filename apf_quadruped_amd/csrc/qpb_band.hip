@@ -24,10 +24,10 @@
 // it -- the row kernel's layout, one stage per row, products as DPP row_newbcast FMAs,
 // the neighbouring stages' x / y values loaded per lane.  The recurrences (Z_k, the
 // Schur update and pivots of each stage, the forward / backward sweeps) run stage by
-// stage.  All of the QP's state -- P, G, A stage blocks, the factor's L_k (with 1/D_k)
-// and -Z_k rows, the iterate, residuals and directions -- stays in the workgroup's LDS
-// for the whole solve (79 KB for MPC: two QPs per CU); inputs are read once, outputs
-// written once.
+// stage.  All of the QP's state -- P, G, A stage blocks, the factor's L_k and 1/D_k
+// (and -Z_k rows, unless QPB_B_NOZ), the iterate, residuals and directions -- stays in
+// the workgroup's LDS for the whole solve, packed by pattern (MPC: 39 KB with
+// QPB_B_NOZ, four QPs per CU); inputs are read once, outputs written once.
 //
 // The loop is the row kernel's (qpSWIFT.c:473-644): kkt_initialize as iteration -1,
 // residuals + exit test, factor, predictor, corrector, step lengths (Auxilary.c:359-393),
@@ -55,6 +55,11 @@
 // vectors x, rx, dx | y, ry, dy | z, s, rz, dz, ds in natural order (w = -1 / reg(-s/z)
 // is formed where it is used).
 #define BLKP (NB * NB)
+#ifndef QPB_B_NOZ
+#define QPB_B_NOZ 0       // 1 (the generator's choice where it makes four QPs fit a CU): -Z_k not
+                          // stored; the sweeps form their coupling terms from X_k = 1e7 AR_k'AL_k and
+                          // L_{k-1} (one more triangular chain per stage and sweep)
+#endif
 static_assert(NB >= 1 && NB <= 16 && MZ >= 1 && MZ <= 64 && MY <= 16 && NS >= 2, "band kernel sizes");
 
 // 64-lane sums / maxima: the row butterfly, then the four row results (fixed order)
@@ -423,11 +428,13 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                         qpb_fx<j>(Hs[j], Zr[e], t);
                     });
                 });
+#if !QPB_B_NOZ
                 if (R == kr && isx) {
                     double *Zs = Ls + O_Z + k * (NB * NB) + c * NB;
 #pragma unroll
                     for (int e = 0; e < NB; e++) Zs[e] = -Zr[e];
                 }
+#endif
             }
 #endif
             // LDL' of the stage block in natural order (the row kernel's pivot chain)
@@ -525,7 +532,38 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             double nl[NB];
             row_L(k, nl);
             const double rd = Ls[O_RD + k * NB + xc];
-#if MY > 0
+#if MY > 0 && QPB_B_NOZ
+            if (k > 0) {
+                // Z_k v_{k-1} = 1e7 AR_k' (AL_k w), w = L_{k-1}^-T v_{k-1}
+                double ltp[NB], alr[NB], arc[MY1];
+                col_L(k - 1, ltp);
+                const double *ALr = Ls + O_AL + k * (MY * NB) + yc * NB;
+#pragma unroll
+                for (int j = 0; j < NB; j++) alr[j] = ALr[j];
+                col_A(O_AR, k, arc);
+                double w = vprev;
+                qpb_fence(w);
+                qpb_for<0, NB>([&](auto ec) {
+                    constexpr int e = NB - 1 - decltype(ec)::value;
+                    qpb_fxd<e>(w, ltp[e]);
+                });
+                double qy[2] = {0.0, 0.0};
+                qpb_fence(w);
+                qpb_for<0, NB>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(qy[j & 1], w, alr[j]);
+                });
+                const double nq = RDY * (qy[0] + qy[1]);
+                double t2 = 0.0;
+                qpb_fence(nq);
+                qpb_for<0, MY>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
+                    if constexpr (l & 1) qpb_fx<l>(t2, nq, arc[l]);
+                    else qpb_fx<l>(t, nq, arc[l]);
+                });
+                t += t2;
+            }
+#elif MY > 0
             if (k > 0) {
                 const double *Zr = Ls + O_Z + k * (NB * NB) + xc * NB;
                 double nz[NB];
@@ -550,7 +588,34 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             double lt[NB];
             col_L(k, lt);                                                  // -L(e, c): column c
             const double rd = Ls[O_RD + k * NB + xc];
-#if MY > 0
+#if MY > 0 && QPB_B_NOZ
+            if (k + 1 < NS) {
+                // Z_{k+1}' dx_{k+1} = L_k^-1 (1e7 AL_{k+1}' (AR_{k+1} dx_{k+1}))
+                double arr[NB], alc[MY1], nlk[NB];
+                const double *ARr = Ls + O_AR + (k + 1) * (MY * NB) + yc * NB;
+#pragma unroll
+                for (int j = 0; j < NB; j++) arr[j] = ARr[j];
+                col_A(O_AL, k + 1, alc);
+                row_L(k, nlk);
+                double py[2] = {0.0, 0.0};
+                qpb_fence(dxn);
+                qpb_for<0, NB>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(py[j & 1], dxn, arr[j]);
+                });
+                const double pp = -RDY * (py[0] + py[1]);
+                double sa[2] = {0.0, 0.0};
+                qpb_fence(pp);
+                qpb_for<0, MY>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
+                    qpb_fx<l>(sa[l & 1], pp, alc[l]);
+                });
+                double sx = sa[0] + sa[1];
+                qpb_fence(sx);
+                qpb_for<0, NB>([&](auto fc) { qpb_fxd<decltype(fc)::value>(sx, nlk[decltype(fc)::value]); });
+                r = __builtin_fma(-sx, rd, r);
+            }
+#elif MY > 0
             if (k + 1 < NS) {
                 const double *Zn = Ls + O_Z + (k + 1) * (NB * NB) + xc;    // -Z_{k+1}, by columns
                 double zt[NB];

@@ -537,7 +537,7 @@ static std::vector<std::pair<long, long>> band_gunion(const Plan &pl) {
     return u;
 }
 
-static BandLayout band_layout(const Plan &pl) {
+static BandLayout band_layout(const Plan &pl, bool noz) {
     const long nb = pl.band_nb, ns = pl.band_ns, mz = pl.band_mz, my = pl.band_my;
     const long nx = nb * ns, nz = mz * ns, ny = my * ns, ny1 = ny > 0 ? ny : 1;
     BandLayout L;
@@ -548,7 +548,7 @@ static BandLayout band_layout(const Plan &pl) {
     L.O_L = L.O_P + ns * L.PP;
     L.O_RD = L.O_L + ns * L.LP;
     L.O_Z = L.O_RD + ns * nb;
-    L.O_G = L.O_Z + ns * nb * nb;
+    L.O_G = L.O_Z + (noz ? 0 : ns * nb * nb);
     L.O_AR = L.O_G + ns * L.GS;
     L.O_AL = L.O_AR + ns * my * nb;
     L.O_DUMP = L.O_AL + ns * my * nb;                 // one slot per lane (masked stores)
@@ -568,7 +568,15 @@ static BandLayout band_layout(const Plan &pl) {
     return L;
 }
 
-long band_lds_bytes(const Plan &pl) { return pl.band_nb > 0 ? band_layout(pl).LDS_QP * 8 : 0; }
+// -Z_k not stored (QPB_B_NOZ) when that, and only that, fits four QPs in a CU's 160 KB
+// (QPB_BAND_NOZ=0/1 overrides)
+static bool band_noz(const Plan &pl) {
+    if (const char *e = getenv("QPB_BAND_NOZ")) return atoi(e) != 0;
+    const long quarter = 160L * 1024 / 4;
+    return band_layout(pl, false).LDS_QP * 8 > quarter && band_layout(pl, true).LDS_QP * 8 <= quarter;
+}
+
+long band_lds_bytes(const Plan &pl) { return pl.band_nb > 0 ? band_layout(pl, band_noz(pl)).LDS_QP * 8 : 0; }
 
 bool band_eligible(const Plan &pl, std::string *why) {
     auto no = [&](const char *m) { if (why) *why = m; return false; };
@@ -590,7 +598,8 @@ bool band_eligible(const Plan &pl, std::string *why) {
 
 std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
     const long nb = pl.band_nb, ns = pl.band_ns, mz = pl.band_mz, my = pl.band_my;
-    const BandLayout L = band_layout(pl);
+    const bool noz = band_noz(pl);
+    const BandLayout L = band_layout(pl, noz);
     std::ostringstream o;
     o << "#define QPB_ROW_COMMON_ONLY 1\n" << kRowTemplate << "\n#undef QPB_ROW_COMMON_ONLY\n";
     o << "// generated by qpb_wave for plan " << std::hex << pl.hash << std::dec << ": n=" << pl.n << " m=" << pl.m
@@ -603,6 +612,7 @@ std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
             if (eq != std::string::npos) o << "#define " << kv.substr(0, eq) << " " << kv.substr(eq + 1) << "\n";
         }
     }
+    if (noz) o << "#define QPB_B_NOZ 1\n";
     o << "#define QPB_BNB " << nb << "\n#define QPB_BNS " << ns << "\n#define QPB_BMZ " << mz << "\n#define QPB_BMY " << my
       << "\n";
     const long nP = pl.Pin.nnz(), nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz();
