@@ -24,10 +24,12 @@
 // it -- the row kernel's layout, one stage per row, products as DPP row_newbcast FMAs,
 // the neighbouring stages' x / y values loaded per lane.  The recurrences (Z_k, the
 // Schur update and pivots of each stage, the forward / backward sweeps) run stage by
-// stage.  All of the QP's state -- P, G, A stage blocks, the factor's L_k and 1/D_k
-// (and -Z_k rows, unless QPB_B_NOZ), the iterate, residuals and directions -- stays in
-// the workgroup's LDS for the whole solve, packed by pattern (MPC: 39 KB with
-// QPB_B_NOZ, four QPs per CU); inputs are read once, outputs written once.
+// stage.  The coupling X_k = 1e7 AR_k'AL_k has rank <= MY, so the factor keeps
+// Y_k = S_{k-1}^-1 AL_k' (NB x MY) instead of the NB x NB block L_{k,k-1}: the sweeps'
+// recursions become short products and their triangular chains run stage-parallel.
+// All of the QP's state -- P, G, A stage blocks, the factor's L_k, 1/D_k and Y_k, the
+// iterate, residuals and directions -- stays in the workgroup's LDS for the whole
+// solve, packed by pattern; inputs are read once, outputs written once.
 //
 // The loop is the row kernel's (qpSWIFT.c:473-644): kkt_initialize as iteration -1,
 // residuals + exit test, factor, predictor, corrector, step lengths (Auxilary.c:359-393),
@@ -48,18 +50,20 @@
 // per-stage blocks and vectors (doubles; offsets emitted by the generator, qpb_wave.cpp
 // band_layout), packed by pattern so that three QPs share a CU: O_P P_k's upper triangle
 // (PP per stage, (i, j) at j (j + 1) / 2 + i), O_L -L_k's strict lower triangle (LP per
-// stage, row c from c (c - 1) / 2), O_RD 1 / D_k, O_Z rows of -Z_k (NB x NB), O_G G_k on
+// stage, row c from c (c - 1) / 2), O_RD 1 / D_k, O_Y Y_k by columns (MY x NB), O_G G_k on
 // the union of the stages' G patterns (GS per stage, the last slot zero; per-lane
 // position tables qpb_bgc / qpb_bgr), O_AR / O_AL the A row groups' stage-k /
-// stage-(k-1) parts (dense rows), O_DUMP one slot per lane for masked stores; the
-// vectors x, rx, dx | y, ry, dy | z, s, rz, dz, ds in natural order (w = -1 / reg(-s/z)
-// is formed where it is used).
+// stage-(k-1) parts (dense rows); the vectors x, dx | y, ry | z, s, rz, dz in natural
+// order.  rx is not kept (the solves' right-hand side re-forms it inside its own
+// products); the corrector's dy and ds overwrite ry and rz once these are consumed;
+// O_DUMP (one slot per lane for masked stores) lies in dz, dead while the factor runs;
+// w = -1 / reg(-s/z) is formed where it is used.
 #define BLKP (NB * NB)
-#ifndef QPB_B_NOZ
-#define QPB_B_NOZ 0       // 1 (the generator's choice where it makes four QPs fit a CU): -Z_k not
-                          // stored; the sweeps form their coupling terms from X_k = 1e7 AR_k'AL_k and
-                          // L_{k-1} (one more triangular chain per stage and sweep)
-#endif
+// A row group k: its stage-k part AR_k, its stage-(k-1) part AL_k (k >= 1; stage 0 has none:
+// ALB(0) points at finite data that is only ever multiplied by zero); Y_k (k >= 1)
+#define ARB(k) (O_AR + (k) * (MY * NB))
+#define ALB(k) (O_AL + ((k) - 1) * (MY * NB))
+#define YB(k) (O_Y + ((k) - 1) * (MY * NB))
 static_assert(NB >= 1 && NB <= 16 && MZ >= 1 && MZ <= 64 && MY <= 16 && NS >= 2, "band kernel sizes");
 
 // 64-lane sums / maxima: the row butterfly, then the four row results (fixed order)
@@ -178,7 +182,6 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #if MY > 0
         scatter(a.A + tile * (QPB_NNZA * QPB_TSTR) + ql, qpb_ic<QPB_NNZA>{}, qpb_bsA, nullptr);
 #endif
-        for (int i = lane; i < BNX; i += 64) Ls[V_RX + i] = -QPB_LDS(&gc[i * QPB_TSTR]);
 #if MY > 0
         for (int i = lane; i < BNY; i += 64) Ls[V_RY + i] = QPB_LDS(&gb[i * QPB_TSTR]);
 #endif
@@ -229,8 +232,8 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #pragma unroll
         for (int e = 0; e < NB; e++) lt[e] = e > xc ? Lk[e * (e - 1) / 2] : 0.0;
     };
-    auto col_A = [&](int off, int kc, double (&v)[MY1]) {
-        const double *Ak = Ls + off + kc * (MY * NB) + xc;
+    auto col_A = [&](int base, double (&v)[MY1]) {
+        const double *Ak = Ls + base + xc;
 #pragma unroll
         for (int l = 0; l < MY1; l++) v[l] = MY > 0 ? Ak[l * NB] : 0.0;
     };
@@ -267,9 +270,9 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             const double yk = Ls[V_Y + kc * MY + yc];
             const double yn = nxt ? Ls[V_Y + (kc + 1) * MY + yc] : 0.0;
             double arc[MY1], alnc[MY1], arr[NB], alr[NB];
-            col_A(O_AR, kc, arc);
-            col_A(O_AL, nxt ? kc + 1 : kc, alnc);
-            const double *ARr = Ls + O_AR + kc * (MY * NB) + yc * NB, *ALr = Ls + O_AL + kc * (MY * NB) + yc * NB;
+            col_A(ARB(kc), arc);
+            col_A(ALB(nxt ? kc + 1 : kc), alnc);
+            const double *ARr = Ls + ARB(kc) + yc * NB, *ALr = Ls + ALB(kc) + yc * NB;
 #pragma unroll
             for (int j = 0; j < NB; j++) { arr[j] = ARr[j]; alr[j] = ALr[j]; }
             double ay = 0.0;
@@ -303,7 +306,6 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #endif
             const double rx = -(((ta[0] + ta[1]) + (ta[2] + ta[3])) + px);
             if (act && isx) {
-                Ls[V_RX + k * NB + c] = rx;
                 srx = __builtin_fma(rx, rx, srx);
                 sfv = __builtin_fma(xk, __builtin_fma(0.5, px, cx), sfv);   // objective (Auxilary.c:1133-1141)
             }
@@ -342,7 +344,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
     // so the same bits.
     auto factor = [&](auto regc) {
         constexpr bool REG = decltype(regc)::value != 0;
-        double H[NB], Xr[NB];
+        double H[NB];
 #pragma unroll 1
         for (int k = 0; k < NS; k++) {
             QPB_BT0();
@@ -376,12 +378,9 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                     });
                 });
 #if MY > 0
-                double arc[MY1], alc[MY1], alnc[MY1];
-                col_A(O_AR, kc, arc);
-                col_A(O_AL, kc, alc);
-                col_A(O_AL, nxt ? kc + 1 : kc, alnc);
-#pragma unroll
-                for (int j = 0; j < NB; j++) Xr[j] = 0.0;
+                double arc[MY1], alnc[MY1];
+                col_A(ARB(kc), arc);
+                col_A(ALB(nxt ? kc + 1 : kc), alnc);
                 qpb_for<0, MY>([&](auto lc) {
                     constexpr int l = decltype(lc)::value;
                     const double tr = -RDY * arc[l], an = nxt ? alnc[l] : 0.0, tn = -RDY * an;
@@ -389,10 +388,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                     qpb_for<0, NB>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
                         if constexpr ((qpb_bARm[l] >> j) & 1) qpb_fx<j>(H[j], arc[l], tr);    // 1e7 AR_k'AR_k
-                        if constexpr ((qpb_bALm[l] >> j) & 1) {
-                            qpb_fx<j>(H[j], an, tn);                                       // 1e7 AL_{k+1}'AL_{k+1}
-                            qpb_fx<j>(Xr[j], alc[l], tr);                                  // X_k = 1e7 AR_k'AL_k
-                        }
+                        if constexpr ((qpb_bALm[l] >> j) & 1) qpb_fx<j>(H[j], an, tn);        // 1e7 AL_{k+1}'AL_{k+1}
                     });
                 });
 #endif
@@ -404,37 +400,59 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             for (int j = 0; j < NB; j++) Hs[j] = H[j];
 #if MY > 0
             if (k > 0) {
-                double nLp[NB], Zr[NB];
-                row_L(k - 1, nLp);
-#pragma unroll
-                for (int f = 0; f < NB; f++) Zr[f] = Xr[f];
+                // H_kk -= X_k S_{k-1}^-1 X_k' with X_k = 1e7 AR_k' AL_k (rank <= MY):
+                //   Y_k = S_{k-1}^-1 AL_k' = L^-T D^-1 L^-1 AL_k'   (x lanes: row c of Y_k)
+                //   M = AL_k Y_k, T = M AR_k                          (y lanes: rows l)
+                //   H(c, j) -= 1e14 sum_l AR_k(l, c) T(l, j)          (x lanes)
+                double nlr[NB], nlc[NB], Yr[MY1], arc[MY1], alr[NB], arr[NB];
+                row_L(k - 1, nlr);
+                col_L(k - 1, nlc);
                 const double rdp = Ls[O_RD + (k - 1) * NB + xc];
-                // Z(c, e) = X(c, e) - sum_{f<e} L_{k-1}(e, f) Z(c, f): lane e's -L row broadcast,
-                // right-looking (each Z(c, e) sums over f in ascending order)
-                qpb_for<0, NB - 1>([&](auto fc) {
+                col_A(ALB(k), Yr);
+                col_A(ARB(k), arc);
+                const double *ALr = Ls + ALB(k) + yc * NB, *ARr = Ls + ARB(k) + yc * NB;
+#pragma unroll
+                for (int j = 0; j < NB; j++) { alr[j] = ALr[j]; arr[j] = ARr[j]; }
+                qpb_for<0, NB>([&](auto fc) {
                     constexpr int f = decltype(fc)::value;
-                    qpb_for<f + 1, NB>([&](auto ec) {
-                        constexpr int e = decltype(ec)::value;
-                        qpb_fx<e>(Zr[e], nLp[f], Zr[f]);
-                    });
+                    qpb_for<0, MY>([&](auto lc) { qpb_fxd<f>(Yr[decltype(lc)::value], nlr[f]); });
                 });
-                // H_kk -= Z D_{k-1}^-1 Z'; -Z rows to LDS (the sweeps' coupling terms)
+#pragma unroll
+                for (int l = 0; l < MY; l++) Yr[l] *= rdp;
                 qpb_for<0, NB>([&](auto ec) {
-                    constexpr int e = decltype(ec)::value;
-                    const double t = -(Zr[e] * qpb_nb<e>(rdp));
-                    qpb_fence(t);
+                    constexpr int e = NB - 1 - decltype(ec)::value;
+                    qpb_for<0, MY>([&](auto lc) { qpb_fxd<e>(Yr[decltype(lc)::value], nlc[e]); });
+                });
+                if (R == kr && isx) {
+#pragma unroll
+                    for (int l = 0; l < MY; l++) Ls[YB(k) + l * NB + c] = Yr[l];
+                }
+                double M[MY1], T[NB];
+#pragma unroll
+                for (int l = 0; l < MY; l++) M[l] = 0.0;
+#pragma unroll
+                for (int j = 0; j < NB; j++) T[j] = 0.0;
+                qpb_for<0, NB>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    if constexpr ((qpb_bALu >> j) & 1)
+                        qpb_for<0, MY>([&](auto lc) { qpb_fx<j>(M[decltype(lc)::value], Yr[decltype(lc)::value], alr[j]); });
+                });
+                qpb_for<0, MY>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
                     qpb_for<0, NB>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
-                        qpb_fx<j>(Hs[j], Zr[e], t);
+                        if constexpr ((qpb_bARu >> j) & 1) qpb_fx<l>(T[j], arr[j], M[l]);
                     });
                 });
-#if !QPB_B_NOZ
-                if (R == kr && isx) {
-                    double *Zs = Ls + O_Z + k * (NB * NB) + c * NB;
-#pragma unroll
-                    for (int e = 0; e < NB; e++) Zs[e] = -Zr[e];
-                }
-#endif
+                qpb_for<0, MY>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
+                    const double m = -1e14 * arc[l];
+                    qpb_fence(m);
+                    qpb_for<0, NB>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        if constexpr ((qpb_bARu >> j) & 1) qpb_fx<l>(Hs[j], T[j], m);
+                    });
+                });
             }
 #endif
             // LDL' of the stage block in natural order (the row kernel's pivot chain)
@@ -493,15 +511,26 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             const bool act = k < NS;
             const int kc = act ? k : NS - 1;
             const bool nxt = kc + 1 < NS;
+            // t = bx + G'(w o bz) + 1e7 A' by with bx = rx = -c - P x - G'z - A'y (-c at
+            // kkt_initialize): rx is not kept, its G' / A' terms fold into the same products
+            const bool it0 = mode == BM_SETUP;
             double v[ZS], gcl[MZ];
 #pragma unroll
             for (int u = 0; u < ZS; u++) {
                 double cc;
                 const int iz = kc * MZ + zrc[u];
-                v[u] = wz(iz) * bz_of(mode, iz, smu, pcd, &cc);
+                v[u] = wz(iz) * bz_of(mode, iz, smu, pcd, &cc) - (it0 ? 0.0 : Ls[V_Z + iz]);
             }
             col_G(kc, gcl);
-            double ta[4] = {Ls[V_RX + kc * NB + xc], 0.0, 0.0, 0.0};
+            double ta[4] = {-QPB_LDS(&gc[(kc * NB + xc) * QPB_TSTR]), 0.0, 0.0, 0.0};
+            if (!it0) {
+                double pr[NB], px = 0.0;
+                row_P(kc, pr);
+                const double xk = Ls[V_X + kc * NB + xc];
+                qpb_fence(xk);
+                qpb_for<0, NB>([&](auto jc) { qpb_fx<decltype(jc)::value>(px, xk, pr[decltype(jc)::value]); });
+                ta[1] = -px;
+            }
             qpb_fence(v[0]);
             qpb_for<0, MZ>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
@@ -509,10 +538,11 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             });
 #if MY > 0
             double arc[MY1], alnc[MY1];
-            col_A(O_AR, kc, arc);
-            col_A(O_AL, nxt ? kc + 1 : kc, alnc);
-            const double yr = -RDY * Ls[V_RY + kc * MY + yc];
-            const double yrn = nxt ? -RDY * Ls[V_RY + (kc + 1) * MY + yc] : 0.0;
+            col_A(ARB(kc), arc);
+            col_A(ALB(nxt ? kc + 1 : kc), alnc);
+            const double yr = -RDY * Ls[V_RY + kc * MY + yc] - (it0 ? 0.0 : Ls[V_Y + kc * MY + yc]);
+            const double yrn = nxt ? -RDY * Ls[V_RY + (kc + 1) * MY + yc] - (it0 ? 0.0 : Ls[V_Y + (kc + 1) * MY + yc])
+                                   : 0.0;
             qpb_fence(yr, yrn);
             qpb_for<0, MY>([&](auto lc) {
                 constexpr int l = decltype(lc)::value;
@@ -524,36 +554,27 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         }
         qpb_wsync();
         QPB_BT2(2);
-        // forward sweep: u_k = L_k^-1 (t_k - Z_k v_{k-1}), v_k = D_k^-1 u_k -> DX
-        double vprev = 0.0;
+        // block forward / backward substitution (block Thomas) with X_k S_{k-1}^-1 = U_k Y_k',
+        // U_k = 1e7 AR_k':  r_0 = t_0, r_k = t_k - U_k (Y_k' r_{k-1});  g_k = S_k^-1 r_k
+        // (stage-parallel: two triangular chains per stage);  dx_{NS-1} = g_{NS-1},
+        // dx_k = g_k - Y_{k+1} (U_{k+1}' dx_{k+1}).  The recursions are short products.
+#if MY > 0
+        {
+            double rprev = Ls[V_DX + xc];
 #pragma unroll 1
-        for (int k = 0; k < NS; k++) {
-            double t = Ls[V_DX + k * NB + xc];
-            double nl[NB];
-            row_L(k, nl);
-            const double rd = Ls[O_RD + k * NB + xc];
-#if MY > 0 && QPB_B_NOZ
-            if (k > 0) {
-                // Z_k v_{k-1} = 1e7 AR_k' (AL_k w), w = L_{k-1}^-T v_{k-1}
-                double ltp[NB], alr[NB], arc[MY1];
-                col_L(k - 1, ltp);
-                const double *ALr = Ls + O_AL + k * (MY * NB) + yc * NB;
+            for (int k = 1; k < NS; k++) {
+                double yt[NB], arc[MY1];
+                const double *Yk = Ls + YB(k) + yc * NB;                    // Y_k(:, yc)
 #pragma unroll
-                for (int j = 0; j < NB; j++) alr[j] = ALr[j];
-                col_A(O_AR, k, arc);
-                double w = vprev;
-                qpb_fence(w);
-                qpb_for<0, NB>([&](auto ec) {
-                    constexpr int e = NB - 1 - decltype(ec)::value;
-                    qpb_fxd<e>(w, ltp[e]);
-                });
-                double qy[2] = {0.0, 0.0};
-                qpb_fence(w);
+                for (int j = 0; j < NB; j++) yt[j] = Yk[j];
+                col_A(ARB(k), arc);
+                double t = Ls[V_DX + k * NB + xc];
+                double q[2] = {0.0, 0.0};
                 qpb_for<0, NB>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
-                    if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(qy[j & 1], w, alr[j]);
+                    qpb_fx<j>(q[j & 1], rprev, yt[j]);
                 });
-                const double nq = RDY * (qy[0] + qy[1]);
+                const double nq = RDY * (q[0] + q[1]);
                 double t2 = 0.0;
                 qpb_fence(nq);
                 qpb_for<0, MY>([&](auto lc) {
@@ -562,80 +583,67 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                     else qpb_fx<l>(t, nq, arc[l]);
                 });
                 t += t2;
+                if (st0) Ls[V_DX + k * NB + c] = t;
+                rprev = t;
             }
-#elif MY > 0
-            if (k > 0) {
-                const double *Zr = Ls + O_Z + k * (NB * NB) + xc * NB;
-                double nz[NB];
-#pragma unroll
-                for (int e = 0; e < NB; e++) nz[e] = Zr[e];
-                qpb_fence(vprev);
-                qpb_for<0, NB>([&](auto ec) { qpb_fx<decltype(ec)::value>(t, vprev, nz[decltype(ec)::value]); });
-            }
-#endif
-            qpb_fence(t);
-            qpb_for<0, NB>([&](auto fc) { qpb_fxd<decltype(fc)::value>(t, nl[decltype(fc)::value]); });
-            vprev = t * rd;
-            if (st0) Ls[V_DX + k * NB + c] = vprev;
+            qpb_wsync();
         }
-        qpb_wsync();
-        QPB_BT2(3);
-        // backward sweep: dx_k = L_k^-T (v_k - D_k^-1 Z_{k+1}' dx_{k+1}) -> DX
-        double dxn = 0.0;
-#pragma unroll 1
-        for (int k = NS - 1; k >= 0; k--) {
-            double r = Ls[V_DX + k * NB + xc];
-            double lt[NB];
-            col_L(k, lt);                                                  // -L(e, c): column c
-            const double rd = Ls[O_RD + k * NB + xc];
-#if MY > 0 && QPB_B_NOZ
-            if (k + 1 < NS) {
-                // Z_{k+1}' dx_{k+1} = L_k^-1 (1e7 AL_{k+1}' (AR_{k+1} dx_{k+1}))
-                double arr[NB], alc[MY1], nlk[NB];
-                const double *ARr = Ls + O_AR + (k + 1) * (MY * NB) + yc * NB;
-#pragma unroll
-                for (int j = 0; j < NB; j++) arr[j] = ARr[j];
-                col_A(O_AL, k + 1, alc);
-                row_L(k, nlk);
-                double py[2] = {0.0, 0.0};
-                qpb_fence(dxn);
-                qpb_for<0, NB>([&](auto jc) {
-                    constexpr int j = decltype(jc)::value;
-                    if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(py[j & 1], dxn, arr[j]);
-                });
-                const double pp = -RDY * (py[0] + py[1]);
-                double sa[2] = {0.0, 0.0};
-                qpb_fence(pp);
-                qpb_for<0, MY>([&](auto lc) {
-                    constexpr int l = decltype(lc)::value;
-                    qpb_fx<l>(sa[l & 1], pp, alc[l]);
-                });
-                double sx = sa[0] + sa[1];
-                qpb_fence(sx);
-                qpb_for<0, NB>([&](auto fc) { qpb_fxd<decltype(fc)::value>(sx, nlk[decltype(fc)::value]); });
-                r = __builtin_fma(-sx, rd, r);
-            }
-#elif MY > 0
-            if (k + 1 < NS) {
-                const double *Zn = Ls + O_Z + (k + 1) * (NB * NB) + xc;    // -Z_{k+1}, by columns
-                double zt[NB];
-#pragma unroll
-                for (int j = 0; j < NB; j++) zt[j] = Zn[j * NB];
-                double acc = 0.0;
-                qpb_fence(dxn);
-                qpb_for<0, NB>([&](auto jc) { qpb_fx<decltype(jc)::value>(acc, dxn, zt[decltype(jc)::value]); });
-                r = __builtin_fma(acc, rd, r);
-            }
 #endif
+        QPB_BT2(3);
+#pragma unroll 1
+        for (int i = 0; i < NR; i++) {
+            const int k = 4 * i + R;
+            const bool act = k < NS;
+            const int kc = act ? k : NS - 1;
+            double r = Ls[V_DX + kc * NB + xc];
+            double nl[NB], lt[NB];
+            row_L(kc, nl);
+            col_L(kc, lt);
+            const double rd = Ls[O_RD + kc * NB + xc];
+            qpb_fence(r);
+            qpb_for<0, NB>([&](auto fc) { qpb_fxd<decltype(fc)::value>(r, nl[decltype(fc)::value]); });
+            r *= rd;
             qpb_fence(r);
             qpb_for<0, NB>([&](auto ec) {
                 constexpr int e = NB - 1 - decltype(ec)::value;
                 qpb_fxd<e>(r, lt[e]);
             });
-            if (st0) Ls[V_DX + k * NB + c] = r;
-            dxn = r;
+            if (act && isx) Ls[V_DX + k * NB + c] = r;
         }
         qpb_wsync();
+#if MY > 0
+        {
+            double dxn = Ls[V_DX + (NS - 1) * NB + xc];
+#pragma unroll 1
+            for (int k = NS - 2; k >= 0; k--) {
+                double arr[NB], ycl[MY1];
+                const double *ARr = Ls + ARB(k + 1) + yc * NB;
+#pragma unroll
+                for (int j = 0; j < NB; j++) arr[j] = ARr[j];
+                const double *Yn = Ls + YB(k + 1) + xc;                         // Y_{k+1}(xc, :)
+#pragma unroll
+                for (int l = 0; l < MY; l++) ycl[l] = Yn[l * NB];
+                double g = Ls[V_DX + k * NB + xc];
+                double p[2] = {0.0, 0.0};
+                qpb_for<0, NB>([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(p[j & 1], dxn, arr[j]);
+                });
+                const double np = RDY * (p[0] + p[1]);
+                double g2 = 0.0;
+                qpb_fence(np);
+                qpb_for<0, MY>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
+                    if constexpr (l & 1) qpb_fx<l>(g2, np, ycl[l]);
+                    else qpb_fx<l>(g, np, ycl[l]);
+                });
+                g += g2;
+                if (st0) Ls[V_DX + k * NB + c] = g;
+                dxn = g;
+            }
+            qpb_wsync();
+        }
+#endif
         QPB_BT2(4);
         // stage-parallel: dz = w (G dx - bz) (+ ds in the corrector), dy = -1e7 (by - A dx)
 #pragma unroll 1
@@ -651,7 +659,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #if MY > 0
             const double dxp = kc > 0 ? Ls[V_DX + (kc - 1) * NB + xc] : 0.0;
             double arr[NB], alr[NB], gy = 0.0;
-            const double *ARr = Ls + O_AR + kc * (MY * NB) + yc * NB, *ALr = Ls + O_AL + kc * (MY * NB) + yc * NB;
+            const double *ARr = Ls + ARB(kc) + yc * NB, *ALr = Ls + ALB(kc) + yc * NB;
 #pragma unroll
             for (int j = 0; j < NB; j++) { arr[j] = ARr[j]; alr[j] = ALr[j]; }
             qpb_fence(dxk, dxp);
@@ -677,16 +685,16 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                     const double bz = bz_of(mode, iz, smu, pcd, &cc);
                     const double dz = wz(iz) * (gz[u] - bz);
                     Ls[V_DZ + iz] = dz;
-                    if (mode == BM_CORR) {
+                    if (mode == BM_CORR) {      // ds replaces rz (read above, dead from here on)
                         const double s = Ls[V_S + iz], rzi = qpb_rcp(Ls[V_Z + iz]);
-                        Ls[V_DS + iz] = __builtin_fma(__builtin_fma(-s, dz, cc), rzi, -s);
+                        Ls[V_RZ + iz] = __builtin_fma(__builtin_fma(-s, dz, cc), rzi, -s);
                     }
                 }
             }
 #if MY > 0
-            if (act && isy) {
+            if (act && isy && mode != BM_PRED) {    // dy replaces ry (the predictor's dy is unused)
                 const int iy = k * MY + c;
-                Ls[V_DY + iy] = RDY * (Ls[V_RY + iy] - gy);
+                Ls[V_RY + iy] = RDY * (Ls[V_RY + iy] - gy);
             }
 #endif
         }
@@ -700,7 +708,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         for (int i = lane; i < BNZ; i += 64) {
             const double s = Ls[V_S + i], z = Ls[V_Z + i], dz = Ls[V_DZ + i];
             const double rzi = qpb_rcp(z);
-            const double dsl = corr ? Ls[V_DS + i] : -s * __builtin_fma(dz, rzi, 1.0);
+            const double dsl = corr ? Ls[V_RZ + i] : -s * __builtin_fma(dz, rzi, 1.0);
             bp = __builtin_fmax(bp, -dsl * __builtin_amdgcn_rcp(s));
             bd = __builtin_fmax(bd, -dz * rzi);
         }
@@ -759,7 +767,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 Ls[V_Z + i] = hi < 0 ? -zi : -zi + (1 + hi);
             }
             for (int i = lane; i < BNX; i += 64) Ls[V_X + i] = Ls[V_DX + i];
-            for (int i = lane; i < BNY; i += 64) Ls[V_Y + i] = Ls[V_DY + i];
+            for (int i = lane; i < BNY; i += 64) Ls[V_Y + i] = Ls[V_RY + i];
             qpb_wsync();
             QPB_BT(2);
             it = 0;
@@ -791,9 +799,9 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
         ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
         for (int i = lane; i < BNX; i += 64) Ls[V_X + i] = __builtin_fma(Ls[V_DX + i], ap, Ls[V_X + i]);
-        for (int i = lane; i < BNY; i += 64) Ls[V_Y + i] = __builtin_fma(Ls[V_DY + i], ad, Ls[V_Y + i]);
+        for (int i = lane; i < BNY; i += 64) Ls[V_Y + i] = __builtin_fma(Ls[V_RY + i], ad, Ls[V_Y + i]);
         for (int i = lane; i < BNZ; i += 64) {
-            Ls[V_S + i] = __builtin_fma(Ls[V_DS + i], ap, Ls[V_S + i]);
+            Ls[V_S + i] = __builtin_fma(Ls[V_RZ + i], ap, Ls[V_S + i]);
             Ls[V_Z + i] = __builtin_fma(Ls[V_DZ + i], ad, Ls[V_Z + i]);
         }
         qpb_wsync();

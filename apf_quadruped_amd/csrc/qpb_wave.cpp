@@ -522,8 +522,8 @@ namespace qpb {
 // LDS layout of the band kernel (qpb_band.hip), doubles per QP: packed stage blocks
 // (P_k upper triangle, strictly lower -L_k, G_k on the union of the stages' G patterns)
 struct BandLayout {
-    long PP, LP, GS, O_P, O_L, O_RD, O_Z, O_G, O_AR, O_AL, O_DUMP, O_STATIC_END;
-    long V_X, V_RX, V_DX, V_Y, V_RY, V_DY, V_Z, V_S, V_RZ, V_DZ, V_DS, LDS_QP;
+    long PP, LP, GS, O_P, O_L, O_RD, O_Y, O_G, O_AR, O_AL, O_DUMP, O_STATIC_END;
+    long V_X, V_DX, V_Y, V_RY, V_Z, V_S, V_RZ, V_DZ, LDS_QP;
 };
 
 // (row, column) pairs of the stage-relative G pattern, union over the stages, row-major
@@ -537,7 +537,7 @@ static std::vector<std::pair<long, long>> band_gunion(const Plan &pl) {
     return u;
 }
 
-static BandLayout band_layout(const Plan &pl, bool noz) {
+static BandLayout band_layout(const Plan &pl) {
     const long nb = pl.band_nb, ns = pl.band_ns, mz = pl.band_mz, my = pl.band_my;
     const long nx = nb * ns, nz = mz * ns, ny = my * ns, ny1 = ny > 0 ? ny : 1;
     BandLayout L;
@@ -547,36 +547,32 @@ static BandLayout band_layout(const Plan &pl, bool noz) {
     L.O_P = 0;
     L.O_L = L.O_P + ns * L.PP;
     L.O_RD = L.O_L + ns * L.LP;
-    L.O_Z = L.O_RD + ns * nb;
-    L.O_G = L.O_Z + (noz ? 0 : ns * nb * nb);
+    L.O_Y = L.O_RD + ns * nb;                         // stages 1 .. ns - 1
+    L.O_G = L.O_Y + (ns - 1) * my * nb;
     L.O_AR = L.O_G + ns * L.GS;
-    L.O_AL = L.O_AR + ns * my * nb;
-    L.O_DUMP = L.O_AL + ns * my * nb;                 // one slot per lane (masked stores)
-    L.O_STATIC_END = (L.O_DUMP + 64 + 1) & ~1L;       // even: 16-byte zero-fill stores
+    L.O_AL = L.O_AR + ns * my * nb;                   // stages 1 .. ns - 1
+    L.O_STATIC_END = (L.O_AL + (ns - 1) * my * nb + 1) & ~1L;   // even: 16-byte zero-fill stores
     L.V_X = L.O_STATIC_END;
-    L.V_RX = L.V_X + nx;
-    L.V_DX = L.V_RX + nx;
+    L.V_DX = L.V_X + nx;
     L.V_Y = L.V_DX + nx;
     L.V_RY = L.V_Y + ny1;
-    L.V_DY = L.V_RY + ny1;
-    L.V_Z = L.V_DY + ny1;
+    L.V_Z = L.V_RY + ny1;
     L.V_S = L.V_Z + nz;
     L.V_RZ = L.V_S + nz;
     L.V_DZ = L.V_RZ + nz;
-    L.V_DS = L.V_DZ + nz;
-    L.LDS_QP = L.V_DS + nz;
+    L.LDS_QP = L.V_DZ + nz;
+    // masked stores of the factor go to one slot per lane inside dz (dead while the
+    // factor runs), or after everything when dz is shorter than a wavefront
+    if (nz >= 64) {
+        L.O_DUMP = L.V_DZ;
+    } else {
+        L.O_DUMP = L.LDS_QP;
+        L.LDS_QP += 64;
+    }
     return L;
 }
 
-// -Z_k not stored (QPB_B_NOZ) when that, and only that, fits four QPs in a CU's 160 KB
-// (QPB_BAND_NOZ=0/1 overrides)
-static bool band_noz(const Plan &pl) {
-    if (const char *e = getenv("QPB_BAND_NOZ")) return atoi(e) != 0;
-    const long quarter = 160L * 1024 / 4;
-    return band_layout(pl, false).LDS_QP * 8 > quarter && band_layout(pl, true).LDS_QP * 8 <= quarter;
-}
-
-long band_lds_bytes(const Plan &pl) { return pl.band_nb > 0 ? band_layout(pl, band_noz(pl)).LDS_QP * 8 : 0; }
+long band_lds_bytes(const Plan &pl) { return pl.band_nb > 0 ? band_layout(pl).LDS_QP * 8 : 0; }
 
 bool band_eligible(const Plan &pl, std::string *why) {
     auto no = [&](const char *m) { if (why) *why = m; return false; };
@@ -598,8 +594,7 @@ bool band_eligible(const Plan &pl, std::string *why) {
 
 std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
     const long nb = pl.band_nb, ns = pl.band_ns, mz = pl.band_mz, my = pl.band_my;
-    const bool noz = band_noz(pl);
-    const BandLayout L = band_layout(pl, noz);
+    const BandLayout L = band_layout(pl);
     std::ostringstream o;
     o << "#define QPB_ROW_COMMON_ONLY 1\n" << kRowTemplate << "\n#undef QPB_ROW_COMMON_ONLY\n";
     o << "// generated by qpb_wave for plan " << std::hex << pl.hash << std::dec << ": n=" << pl.n << " m=" << pl.m
@@ -612,17 +607,14 @@ std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
             if (eq != std::string::npos) o << "#define " << kv.substr(0, eq) << " " << kv.substr(eq + 1) << "\n";
         }
     }
-    if (noz) o << "#define QPB_B_NOZ 1\n";
     o << "#define QPB_BNB " << nb << "\n#define QPB_BNS " << ns << "\n#define QPB_BMZ " << mz << "\n#define QPB_BMY " << my
       << "\n";
     const long nP = pl.Pin.nnz(), nA = pl.p ? pl.A.nnz() : 0, nG = pl.G.nnz();
     o << "#define QPB_NNZP " << nP << "\n#define QPB_NNZA " << nA << "\n#define QPB_NNZG " << nG << "\n";
-    const char *names[] = {"PP", "LP", "GS", "O_P", "O_L", "O_RD", "O_Z", "O_G", "O_AR", "O_AL", "O_DUMP",
-                           "O_STATIC_END", "V_X", "V_RX", "V_DX", "V_Y", "V_RY", "V_DY", "V_Z", "V_S", "V_RZ", "V_DZ",
-                           "V_DS", "LDS_QP"};
-    const long vals[] = {L.PP, L.LP, L.GS, L.O_P, L.O_L, L.O_RD, L.O_Z, L.O_G, L.O_AR, L.O_AL, L.O_DUMP,
-                         L.O_STATIC_END, L.V_X, L.V_RX, L.V_DX, L.V_Y, L.V_RY, L.V_DY, L.V_Z, L.V_S, L.V_RZ, L.V_DZ,
-                         L.V_DS, L.LDS_QP};
+    const char *names[] = {"PP", "LP", "GS", "O_P", "O_L", "O_RD", "O_Y", "O_G", "O_AR", "O_AL", "O_DUMP",
+                           "O_STATIC_END", "V_X", "V_DX", "V_Y", "V_RY", "V_Z", "V_S", "V_RZ", "V_DZ", "LDS_QP"};
+    const long vals[] = {L.PP, L.LP, L.GS, L.O_P, L.O_L, L.O_RD, L.O_Y, L.O_G, L.O_AR, L.O_AL, L.O_DUMP,
+                         L.O_STATIC_END, L.V_X, L.V_DX, L.V_Y, L.V_RY, L.V_Z, L.V_S, L.V_RZ, L.V_DZ, L.LDS_QP};
     for (size_t i = 0; i < sizeof vals / sizeof vals[0]; i++) o << "#define " << names[i] << " " << vals[i] << "\n";
     // CSC value -> LDS slot of the stage blocks
     std::vector<long> pcol(nP), acol(nA), gcol(nG);
@@ -669,7 +661,7 @@ std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
         const long l = pl.A.ir[k], j = acol[k], st = l / my;
         const bool right = j / nb == st;
         (right ? arm : alm)[l % my] |= 1u << (j % nb);
-        return (right ? L.O_AR : L.O_AL) + st * my * nb + (l % my) * nb + (j % nb);
+        return (right ? L.O_AR + st * my * nb : L.O_AL + (st - 1) * my * nb) + (l % my) * nb + (j % nb);
     });
     auto masks = [&](const char *nm, const std::vector<unsigned> &v) {
         unsigned u = 0;

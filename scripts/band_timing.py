@@ -12,7 +12,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PHASES = ("w+residuals+setup", "factor", "predictor", "corrector", "steps+update", "staging")
-PARTS = ("factor stage-parallel", "factor sequential", "solve rhs", "forward sweeps", "backward sweeps",
+PARTS = ("factor stage-parallel", "factor sequential", "solve rhs", "forward recursion", "S^-1 chains + backward recursion",
          "solve directions")
 
 
