@@ -64,7 +64,7 @@ def main():
         flops_issued = (2 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_ADD_F64"]) * 64
         wps = wc / (SIMDS * cyc)
         if band:
-            kind = (f"one QP per wavefront, two per CU: {wps:.2f} waves per SIMD on average over the launch, SIMD VALU "
+            kind = (f"one QP per wavefront, four per CU: {wps:.2f} waves per SIMD on average over the launch, SIMD VALU "
                     f"busy {c['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * cyc):.0%}, a wave waits {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.0%} "
                     f"of its cycles (LDS)")
         elif tree:
