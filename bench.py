@@ -567,8 +567,8 @@ def measured_bound(kname, B):
 
 def limiter_for(B):
     """What the SQ counters say bounds the row kernel at this batch
-    (profiles/r04_sq_row.json, else r03's; scripts/gpu_sq.sh + scripts/sq_summary.py)."""
-    name = next((n for n in ("r04_sq_row.json", "r03_sq_row.json")
+    (the newest profiles/r0N_sq_row.json; scripts/gpu_sq.sh + scripts/sq_summary.py)."""
+    name = next((n for n in ("r05_sq_row.json", "r04_sq_row.json", "r03_sq_row.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", n))), None)
     if name is None:
         return None
