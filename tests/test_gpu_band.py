@@ -167,3 +167,33 @@ def test_band_kernel_regularised_pivot_vs_oracle(oracle):
         assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (q, r["iters"][q], o["iters"])
         for k in ("x", "z", "s"):
             _close(r[k][q], o[k], f"reg[{q}].{k}", 1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tol,maxit,sigma_d", [(1e-2, 100, 0.0), (1e-6, 3, 0.0), (1e-6, 100, 0.05)])
+def test_band_kernel_mpc_options_vs_oracle(tol, maxit, sigma_d, oracle):
+    """The IPM's options on the band kernel: loose tolerance, maxit truncation (QP_MAXIT,
+    the third iterate), and sigma_d > 0 (the pure-centering branch, qpSWIFT.c:572-579)
+    -- against the oracle given the same CSC data and the plan's permutation."""
+    from apf_quadruped_amd import plans
+    from apf_quadruped_amd.batch import Plan, _gather_values
+    B = 8
+    d = plans.standard_qp("mpc_h10", np.arange(B))
+    n, m, p = d["n"], d["m"], d["p"]
+    plan = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0], p_upper=False, kernel="band")
+    assert plan.kernel_for(B) == "band"
+    r = _run(plan, d, B, reltol=tol, abstol=tol, maxit=maxit, sigma_d=sigma_d)
+    (Pjc, Pir), (Ajc, Air), (Gjc, Gir) = plan.patterns.P, plan.patterns.A, plan.patterns.G
+    Pv, Av, Gv = (_gather_values(d[k], jc, ir) for k, (jc, ir) in (("P", (Pjc, Pir)), ("A", (Ajc, Air)),
+                                                                  ("G", (Gjc, Gir))))
+    # loosely converged / truncated iterates (an ill-conditioned KKT after 3 iterations)
+    # amplify the summation-order rounding of the block form: 1e-7, still 10x inside the
+    # north-star tolerance
+    bar = 1e-9 if (tol < 1e-3 and maxit == 100) else 1e-7
+    for q in range(B):
+        o = oracle.solve_csc(n, m, p, Pjc, Pir, Pv[q], Ajc, Air, Av[q], Gjc, Gir, Gv[q], d["c"][q], d["h"][q],
+                             d["b"][q], sigma_d=sigma_d, perm=plan.perm, reltol=tol, abstol=tol, maxit=maxit)
+        assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (q, r["flag"][q], o["flag"], r["iters"][q],
+                                                                            o["iters"])
+        for k in ("x", "y", "z", "s"):
+            _close(r[k][q], o[k], f"opts[{q}].{k}", bar)
