@@ -275,7 +275,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             const double *ARr = Ls + ARB(kc) + yc * NB, *ALr = Ls + ALB(kc) + yc * NB;
 #pragma unroll
             for (int j = 0; j < NB; j++) { arr[j] = ARr[j]; alr[j] = ALr[j]; }
-            double ay = 0.0;
+            double ay = 0.0, ay2 = 0.0;
 #endif
             qpb_fence(xk, xp);
             qpb_for<0, NB>([&](auto jc) {
@@ -287,7 +287,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 });
 #if MY > 0
                 if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(ay, xk, arr[j]);       // AR_k x_k
-                if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(ay, xp, alr[j]);       // AL_k x_{k-1}
+                if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(ay2, xp, alr[j]);      // AL_k x_{k-1}
 #endif
             });
             // G'z, AR_k' y_k, AL_{k+1}' y_{k+1}: z / y lanes of the row by DPP broadcast
@@ -320,7 +320,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             }
 #if MY > 0
             if (act && isy) {
-                const double ry = by - ay;
+                const double ry = by - (ay + ay2);
                 Ls[V_RY + k * MY + c] = ry;
                 sry = __builtin_fma(ry, ry, sry);
             }
@@ -385,9 +385,13 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                     constexpr int l = decltype(lc)::value;
                     const double tr = -RDY * arc[l], an = nxt ? alnc[l] : 0.0, tn = -RDY * an;
                     qpb_fence(tr, an, tn);
+                    // the two products' FMAs on one H(c, j) NB instructions apart (not back to back)
                     qpb_for<0, NB>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
                         if constexpr ((qpb_bARm[l] >> j) & 1) qpb_fx<j>(H[j], arc[l], tr);    // 1e7 AR_k'AR_k
+                    });
+                    qpb_for<0, NB>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
                         if constexpr ((qpb_bALm[l] >> j) & 1) qpb_fx<j>(H[j], an, tn);        // 1e7 AL_{k+1}'AL_{k+1}
                     });
                 });
@@ -472,7 +476,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                     constexpr int j = decltype(jc)::value;
                     qpb_fxs<j>(Hs[j], Hs[kk], nl);
                 });
-                Hs[kk] = xc > kk ? nl : 0.0;
+                Hs[kk] = nl;        // -L(c, kk) for c > kk; the rest never reaches the packed -L rows
             });
             if (R == kr && isx) {
                 const int lrow = O_L + k * LP + c * (c - 1) / 2;
@@ -658,7 +662,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             for (int u = 0; u < ZS; u++) gz[u] = 0.0;
 #if MY > 0
             const double dxp = kc > 0 ? Ls[V_DX + (kc - 1) * NB + xc] : 0.0;
-            double arr[NB], alr[NB], gy = 0.0;
+            double arr[NB], alr[NB], gy = 0.0, gy2 = 0.0;
             const double *ARr = Ls + ARB(kc) + yc * NB, *ALr = Ls + ALB(kc) + yc * NB;
 #pragma unroll
             for (int j = 0; j < NB; j++) { arr[j] = ARr[j]; alr[j] = ALr[j]; }
@@ -674,7 +678,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 });
 #if MY > 0
                 if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(gy, dxk, arr[j]);
-                if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(gy, dxp, alr[j]);
+                if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(gy2, dxp, alr[j]);
 #endif
             });
 #pragma unroll
@@ -694,7 +698,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #if MY > 0
             if (act && isy && mode != BM_PRED) {    // dy replaces ry (the predictor's dy is unused)
                 const int iy = k * MY + c;
-                Ls[V_RY + iy] = RDY * (Ls[V_RY + iy] - gy);
+                Ls[V_RY + iy] = RDY * (Ls[V_RY + iy] - (gy + gy2));
             }
 #endif
         }
