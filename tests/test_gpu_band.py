@@ -113,6 +113,7 @@ STAGE_SHAPES = [
     (7, 5, 64, 3),       # odd width, every lane a z row
     (9, 4, 11, 0),       # no equality rows (independent stages)
     (10, 8, 3, 10),      # as many equality rows as variables per stage
+    (5, 2, 6, 2),        # two stages (the smallest horizon)
 ]
 
 
@@ -197,3 +198,24 @@ def test_band_kernel_mpc_options_vs_oracle(tol, maxit, sigma_d, oracle):
                                                                             o["iters"])
         for k in ("x", "y", "z", "s"):
             _close(r[k][q], o[k], f"opts[{q}].{k}", bar)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("horizon", [3, 16])
+def test_band_kernel_mpc_horizons_vs_oracle(horizon, oracle):
+    """MPC horizons other than configs[3]'s ten stages: a short one (three stages, a
+    single stage-parallel round) and a long one (16 stages, 69 KB of LDS per QP: two QPs
+    per CU, more than 64 KB per workgroup)."""
+    from apf_quadruped_amd import plans, workloads as W
+    from apf_quadruped_amd.batch import Plan
+    B = 5
+    d = W.mpc_qp(plans.SEED + 40 + horizon, np.arange(B), horizon=horizon)
+    n, m, p = d["n"], d["m"], d["p"]
+    plan = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0], kernel="band")
+    r = _run(plan, d, B)
+    Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    for q in range(B):
+        o = oracle.solve_dense(n, m, p, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm)
+        assert r["flag"][q] == o["flag"] == 0 and r["iters"][q] == o["iters"], (horizon, q, r["iters"][q], o["iters"])
+        for k in ("x", "y", "z", "s"):
+            _close(r[k][q], o[k], f"h{horizon}[{q}].{k}", 1e-9)
