@@ -62,3 +62,21 @@ def test_band_kernel_compiles_and_audits_clean():
     assert objs, kn
     audit = open(objs[0] + ".audit").read()
     assert audit.split("audit:")[-1].strip().startswith("clean"), audit
+
+
+def test_python_flags_match_the_header():
+    """batch.py's mirrors of the plan flags (orderings, kernels) equal the #defines of
+    include/qpswift_hip.h -- QPB_KERNEL_BAND included."""
+    import re
+    from apf_quadruped_amd import batch
+    text = open(os.path.join(ROOT, "include", "qpswift_hip.h")).read()
+    defs = {k: int(v, 0) for k, v in re.findall(r"#define (QPB_\w+)\s+(0x[0-9a-fA-F]+)", text)}
+    assert defs["QPB_KERNEL_BAND"] == batch.QPB_KERNEL_BAND == batch.KERNEL_FLAGS["band"]
+    assert defs["QPB_KERNEL_TREE"] == batch.QPB_KERNEL_TREE == batch.KERNEL_FLAGS["tree"]
+    assert defs["QPB_KERNEL_LANE"] == batch.KERNEL_FLAGS["lane"] and defs["QPB_KERNEL_WAVE"] == batch.KERNEL_FLAGS["wave"]
+    assert batch.KERNEL_FLAGS["wave1"] == defs["QPB_KERNEL_WAVE"] | defs["QPB_KERNEL_NOROW"]
+    for name, key in (("amd", "QPB_ORDER_AMD"), ("mindeg", "QPB_ORDER_MINDEG"), ("leaves", "QPB_ORDER_LEAVES")):
+        assert batch.ORDER_FLAGS[name] == defs[key], name
+    # no two plan flags share a bit
+    flags = [v for k, v in defs.items() if k.startswith(("QPB_KERNEL_", "QPB_ORDER_")) or k in ("QPB_P_UPPER", "QPB_EXACT")]
+    assert all(bin(f).count("1") == 1 for f in flags) and len(set(flags)) == len(flags)
