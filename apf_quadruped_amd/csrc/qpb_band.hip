@@ -13,17 +13,17 @@
 //   H_kk     = P_k + G_k' W_k G_k + 1e7 (AR_k' AR_k + AL_{k+1}' AL_{k+1})
 //   H_k,k-1  = X_k = 1e7 AR_k' AL_k            (AR_k / AL_k: A row group k on stage k / k-1)
 // whose LDL' in natural order is the block recurrence
-//   Z_k = X_k L_{k-1}^-T,  S_k = H_kk - Z_k D_{k-1}^-1 Z_k',  S_k = L_k D_k L_k'
+//   S_k = H_kk - X_k S_{k-1}^-1 X_k' = L_k D_k L_k'
 // -- the same factor as the reference's up-looking LDL' of the permuted KKT matrix
 // (ldl.c:253-326, pivot regularisation ldl.c:273-274), in block form, and the same
 // triangular solves (kktsolve, Auxilary.c:471-564) as block forward / backward sweeps.
 //
-// Lanes.  Work that is independent across stages (residuals, the blocks H_kk and X_k,
-// the solves' right-hand sides t_k and their dz / dy) runs stage-parallel: DPP row R of
+// Lanes.  Work that is independent across stages (residuals, the blocks H_kk, the
+// solves' right-hand sides t_k, the triangular chains S_k^-1 r_k, dz / dy) runs stage-parallel: DPP row R of
 // the wavefront takes stage 4 i + R, lane c holding x_c, y_c and the z rows c + 16 u of
 // it -- the row kernel's layout, one stage per row, products as DPP row_newbcast FMAs,
-// the neighbouring stages' x / y values loaded per lane.  The recurrences (Z_k, the
-// Schur update and pivots of each stage, the forward / backward sweeps) run stage by
+// the neighbouring stages' x / y values loaded per lane.  The recurrences (the Schur
+// update and pivots of each stage, the sweeps' short coupling products) run stage by
 // stage.  The coupling X_k = 1e7 AR_k'AL_k has rank <= MY, so the factor keeps
 // Y_k = S_{k-1}^-1 AL_k' (NB x MY) instead of the NB x NB block L_{k,k-1}: the sweeps'
 // recursions become short products and their triangular chains run stage-parallel.
@@ -48,7 +48,7 @@
 #define ZS ((MZ + 15) / 16)       // z sub-rows of a DPP row (z rows c, c + 16, ..)
 #define NR ((NS + 3) / 4)         // rounds of the stage-parallel passes (four stages each)
 // per-stage blocks and vectors (doubles; offsets emitted by the generator, qpb_wave.cpp
-// band_layout), packed by pattern so that three QPs share a CU: O_P P_k's upper triangle
+// band_layout), packed by pattern so that four QPs share a CU (MPC: 40.8 KB): O_P P_k's upper triangle
 // (PP per stage, (i, j) at j (j + 1) / 2 + i), O_L -L_k's strict lower triangle (LP per
 // stage, row c from c (c - 1) / 2), O_RD 1 / D_k, O_Y Y_k by columns (MY x NB), O_G G_k on
 // the union of the stages' G patterns (GS per stage, the last slot zero; per-lane
@@ -97,6 +97,26 @@ static __device__ __forceinline__ double qpb_bmax(double v) {
 #define QPB_BT0()
 #define QPB_BT2(k)
 #endif
+
+#ifndef QPB_B_NV
+#define QPB_B_NV 0        // 1: the stage-parallel passes issue their DPP FMAs as non-volatile asm (the
+                          // compiler may interleave rounds / hoist loads; the hazard pass pads)
+#endif
+#ifndef QPB_B_UNR
+#define QPB_B_UNR 1       // rounds of the stage-parallel passes unrolled by this factor
+#endif
+#define QPB_PRAGMA_(x) _Pragma(#x)
+#define QPB_PRAGMA(x) QPB_PRAGMA_(x)
+template <int J> static __device__ __forceinline__ void qpb_bfx(double &acc, double src, double m) {
+    if constexpr (QPB_B_NV) qpb_fxs<J>(acc, src, m);
+    else qpb_fx<J>(acc, src, m);
+}
+template <int J> static __device__ __forceinline__ void qpb_bfxd(double &t, double m) {
+    if constexpr (QPB_B_NV)
+        asm("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+            : "+v"(t) : "v"(m), "i"(J));
+    else qpb_fxd<J>(t, m);
+}
 
 // solve modes: the right-hand side's z part (bx = RX, by = RY in every mode)
 enum { BM_SETUP = 0, BM_PRED = 1, BM_CORR = 2 };
@@ -242,7 +262,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
     // four sums rx'rx, ry'ry, rz'rz, s'z
     auto residuals = [&](double (&red)[4]) -> double {
         double srx = 0.0, sry = 0.0, srz = 0.0, ssz = 0.0, sfv = 0.0;
-#pragma unroll 1
+QPB_PRAGMA(unroll QPB_B_UNR)
         for (int i = 0; i < NR; i++) {
             const int k = 4 * i + R;
             const bool act = k < NS;
@@ -280,28 +300,28 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             qpb_fence(xk, xp);
             qpb_for<0, NB>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                qpb_fx<j>(px, xk, pr[j]);                                   // P x
+                qpb_bfx<j>(px, xk, pr[j]);                                   // P x
                 qpb_for<0, ZS>([&](auto uc) {
                     constexpr int u = decltype(uc)::value;
-                    if constexpr ((qpb_bgsub(u) >> j) & 1) qpb_fx<j>(gx[u], xk, gr[u][j]);    // G x
+                    if constexpr ((qpb_bgsub(u) >> j) & 1) qpb_bfx<j>(gx[u], xk, gr[u][j]);    // G x
                 });
 #if MY > 0
-                if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(ay, xk, arr[j]);       // AR_k x_k
-                if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(ay2, xp, alr[j]);      // AL_k x_{k-1}
+                if constexpr ((qpb_bARu >> j) & 1) qpb_bfx<j>(ay, xk, arr[j]);       // AR_k x_k
+                if constexpr ((qpb_bALu >> j) & 1) qpb_bfx<j>(ay2, xp, alr[j]);      // AL_k x_{k-1}
 #endif
             });
             // G'z, AR_k' y_k, AL_{k+1}' y_{k+1}: z / y lanes of the row by DPP broadcast
             qpb_fence(zk[0]);
             qpb_for<0, MZ>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                qpb_fx<(r & 15)>(ta[r & 3], zk[r >> 4], gcl[r]);
+                qpb_bfx<(r & 15)>(ta[r & 3], zk[r >> 4], gcl[r]);
             });
 #if MY > 0
             qpb_fence(yk, yn);
             qpb_for<0, MY>([&](auto lc) {
                 constexpr int l = decltype(lc)::value;
-                qpb_fx<l>(ta[(MZ + l) & 3], yk, arc[l]);
-                qpb_fx<l>(ta[(MZ + MY + l) & 3], yn, nxt ? alnc[l] : 0.0);
+                qpb_bfx<l>(ta[(MZ + l) & 3], yk, arc[l]);
+                qpb_bfx<l>(ta[(MZ + MY + l) & 3], yn, nxt ? alnc[l] : 0.0);
             });
 #endif
             const double rx = -(((ta[0] + ta[1]) + (ta[2] + ta[3])) + px);
@@ -372,7 +392,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                         if constexpr (r < MZ) {
                             qpb_for<0, NB>([&](auto jc) {
                                 constexpr int j = decltype(jc)::value;
-                                if constexpr ((qpb_bGm[r] >> j) & 1) qpb_fxs<j>(H[j], gcl[r], cr[decltype(uc)::value]);
+                                if constexpr ((qpb_bGm[r] >> j) & 1) qpb_bfx<j>(H[j], gcl[r], cr[decltype(uc)::value]);
                             });
                         }
                     });
@@ -388,11 +408,11 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                     // the two products' FMAs on one H(c, j) NB instructions apart (not back to back)
                     qpb_for<0, NB>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
-                        if constexpr ((qpb_bARm[l] >> j) & 1) qpb_fx<j>(H[j], arc[l], tr);    // 1e7 AR_k'AR_k
+                        if constexpr ((qpb_bARm[l] >> j) & 1) qpb_bfx<j>(H[j], arc[l], tr);    // 1e7 AR_k'AR_k
                     });
                     qpb_for<0, NB>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
-                        if constexpr ((qpb_bALm[l] >> j) & 1) qpb_fx<j>(H[j], an, tn);        // 1e7 AL_{k+1}'AL_{k+1}
+                        if constexpr ((qpb_bALm[l] >> j) & 1) qpb_bfx<j>(H[j], an, tn);        // 1e7 AL_{k+1}'AL_{k+1}
                     });
                 });
 #endif
@@ -509,7 +529,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
     auto solve = [&](int mode, double smu, bool pcd) {
         QPB_BT0();
         // stage-parallel: t_k = bx_k + G_k'(w o bz) + 1e7 (AR_k' by_k + AL_{k+1}' by_{k+1}) -> DX
-#pragma unroll 1
+QPB_PRAGMA(unroll QPB_B_UNR)
         for (int i = 0; i < NR; i++) {
             const int k = 4 * i + R;
             const bool act = k < NS;
@@ -532,13 +552,13 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 row_P(kc, pr);
                 const double xk = Ls[V_X + kc * NB + xc];
                 qpb_fence(xk);
-                qpb_for<0, NB>([&](auto jc) { qpb_fx<decltype(jc)::value>(px, xk, pr[decltype(jc)::value]); });
+                qpb_for<0, NB>([&](auto jc) { qpb_bfx<decltype(jc)::value>(px, xk, pr[decltype(jc)::value]); });
                 ta[1] = -px;
             }
             qpb_fence(v[0]);
             qpb_for<0, MZ>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
-                qpb_fx<(r & 15)>(ta[r & 3], v[r >> 4], gcl[r]);
+                qpb_bfx<(r & 15)>(ta[r & 3], v[r >> 4], gcl[r]);
             });
 #if MY > 0
             double arc[MY1], alnc[MY1];
@@ -550,8 +570,8 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             qpb_fence(yr, yrn);
             qpb_for<0, MY>([&](auto lc) {
                 constexpr int l = decltype(lc)::value;
-                qpb_fx<l>(ta[(MZ + l) & 3], yr, arc[l]);
-                qpb_fx<l>(ta[(MZ + MY + l) & 3], yrn, alnc[l]);
+                qpb_bfx<l>(ta[(MZ + l) & 3], yr, arc[l]);
+                qpb_bfx<l>(ta[(MZ + MY + l) & 3], yrn, alnc[l]);
             });
 #endif
             if (act && isx) Ls[V_DX + k * NB + c] = (ta[0] + ta[1]) + (ta[2] + ta[3]);
@@ -594,7 +614,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         }
 #endif
         QPB_BT2(3);
-#pragma unroll 1
+QPB_PRAGMA(unroll QPB_B_UNR)
         for (int i = 0; i < NR; i++) {
             const int k = 4 * i + R;
             const bool act = k < NS;
@@ -605,12 +625,12 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
             col_L(kc, lt);
             const double rd = Ls[O_RD + kc * NB + xc];
             qpb_fence(r);
-            qpb_for<0, NB>([&](auto fc) { qpb_fxd<decltype(fc)::value>(r, nl[decltype(fc)::value]); });
+            qpb_for<0, NB>([&](auto fc) { qpb_bfxd<decltype(fc)::value>(r, nl[decltype(fc)::value]); });
             r *= rd;
             qpb_fence(r);
             qpb_for<0, NB>([&](auto ec) {
                 constexpr int e = NB - 1 - decltype(ec)::value;
-                qpb_fxd<e>(r, lt[e]);
+                qpb_bfxd<e>(r, lt[e]);
             });
             if (act && isx) Ls[V_DX + k * NB + c] = r;
         }
@@ -650,7 +670,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #endif
         QPB_BT2(4);
         // stage-parallel: dz = w (G dx - bz) (+ ds in the corrector), dy = -1e7 (by - A dx)
-#pragma unroll 1
+QPB_PRAGMA(unroll QPB_B_UNR)
         for (int i = 0; i < NR; i++) {
             const int k = 4 * i + R;
             const bool act = k < NS;
@@ -674,11 +694,11 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
                 constexpr int j = decltype(jc)::value;
                 qpb_for<0, ZS>([&](auto uc) {
                     constexpr int u = decltype(uc)::value;
-                    if constexpr ((qpb_bgsub(u) >> j) & 1) qpb_fx<j>(gz[u], dxk, gr[u][j]);
+                    if constexpr ((qpb_bgsub(u) >> j) & 1) qpb_bfx<j>(gz[u], dxk, gr[u][j]);
                 });
 #if MY > 0
-                if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(gy, dxk, arr[j]);
-                if constexpr ((qpb_bALu >> j) & 1) qpb_fx<j>(gy2, dxp, alr[j]);
+                if constexpr ((qpb_bARu >> j) & 1) qpb_bfx<j>(gy, dxk, arr[j]);
+                if constexpr ((qpb_bALu >> j) & 1) qpb_bfx<j>(gy2, dxp, alr[j]);
 #endif
             });
 #pragma unroll
