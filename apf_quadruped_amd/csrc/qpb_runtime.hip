@@ -447,8 +447,9 @@ int compile_plan(qpb_plan *plan) {
 }
 
 std::string wave_source_of(const qpb_plan *plan) {
-    return plan->wave_qpw == 4 ? generate_row_kernel(plan->pl, nullptr)
-                               : generate_wave_kernel(plan->pl, plan->wave_wg, nullptr);
+    return plan->wave_rowx ? generate_rowx_kernel(plan->pl, nullptr)
+           : plan->wave_qpw == 4 ? generate_row_kernel(plan->pl, nullptr)
+                                 : generate_wave_kernel(plan->pl, plan->wave_wg, nullptr);
 }
 
 int compile_wave(qpb_plan *plan) {
@@ -519,6 +520,11 @@ int compile_tree(qpb_plan *plan) {
     if (!plan->tree_ok) return fail(QPB_EINVAL, "plan is not eligible for the tree kernel");
     return compile_kernel(plan->tree_kname, [plan] { return generate_tree_kernel(plan->pl, plan->tree_wg, nullptr); },
                           false, &plan->tree_code);
+}
+
+bool rowx_auto() {
+    static const bool on = [] { const char *e = getenv("QPB_ROWX"); return !(e && atoi(e) == 0); }();
+    return on;
 }
 
 bool band_auto() {
@@ -780,6 +786,15 @@ int qpb_plan_create(qpb_plan **out, long n, long m, long p, int flags,
             if (plan->row_occ_batch >= 0) qpb::generate_row_kernel(plan->pl, &plan->row2_kname, 2);
             if (const char *e = getenv("QPB_ROW_SPLIT")) plan->row_split = atoi(e) > 0;
             if (plan->row_split) qpb::generate_row_kernel(plan->pl, &plan->rowsplit_kname, 1, true);
+        } else if (!(flags & QPB_KERNEL_NOROW) && !(er && atoi(er) == 0) && qpb::rowx_auto() &&
+                   qpb::rowx_eligible(plan->pl, nullptr)) {
+            // the wide row form (two x rows per lane) for plans up to 32 variables -- the
+            // controller's 30-variable QPs in leaves-first order (QPB_ROWX=0: the wave form)
+            plan->wave_qpw = 4;
+            plan->wave_wg = 64;
+            plan->wave_rowx = true;
+            plan->wave_max_batch = -1;
+            qpb::generate_rowx_kernel(plan->pl, &plan->wave_kname);
         } else {
             plan->wave_wg = qpb::wave_wg_for(plan->pl);
             qpb::generate_wave_kernel(plan->pl, plan->wave_wg, &plan->wave_kname);
@@ -1348,7 +1363,7 @@ int qpb_group_create(qpb_group **out, qpb_plan *const *plans, int nplans) {
     for (int i = 0; i < nplans; i++) {
         const qpb_plan *pl = plans[i];
         if (!pl) return fail(QPB_EINVAL, "NULL plan in group");
-        if (!pl->wave_ok || pl->wave_qpw != 4 || pl->gen.exact)
+        if (!pl->wave_ok || pl->wave_qpw != 4 || pl->wave_rowx || pl->gen.exact)
             return fail(QPB_EINVAL, "plan " + std::to_string(i) +
                                         " has no row-form kernel (groups need n, p <= 16, m <= 32, z/y rows leaves, fast mode)");
         pls.push_back(&pl->pl);

@@ -18,6 +18,7 @@ struct qpb_plan {
     bool wave_ok = false;                       // wave kernel (one QP per wavefront)
     int wave_wg = 256;
     int wave_qpw = 1;                           // QPs per wavefront: 1 wave form, 4 row form
+    bool wave_rowx = false;                     // row form: the wide kernel (qpb_rowx.hip, n <= 32)
     long wave_max_batch = 0;                    // auto: wave kernel for B <= this
     int kernel_pref = 0;                        // 0 auto, 1 lane only, 2 wave only, 3 tree, 4 band
     std::string wave_kname;
@@ -81,6 +82,7 @@ int compile_band(qpb_plan *plan);
 struct Pick { bool wave = false, band = false, tree = false; };   // neither: the lane kernel
 Pick pick_kernel(const qpb_plan *plan, long B, bool warm);
 bool band_auto();
+bool rowx_auto();     // QPB_ROWX=0: the wave form instead of the wide row form
 int compile_tree(qpb_plan *plan);
 int compile_warm(qpb_plan *plan, const std::string &kname, const std::function<std::string()> &gen_src, bool exact,
                  std::shared_ptr<std::vector<char>> **slot);

@@ -26,6 +26,9 @@ const char *kRowTemplate =
 const char *kBandTemplate =
 #include "qpb_band_src.inc"
     ;
+const char *kRowxTemplate =
+#include "qpb_rowx_src.inc"
+    ;
 
 template <class F>
 void table(std::ostringstream &o, const char *decl, long cnt, F f) {
@@ -674,6 +677,105 @@ std::string generate_band_kernel(const Plan &pl, std::string *name_out) {
     masks("qpb_bAL", alm);
     const std::string body = o.str() + kBandTemplate;
     const std::string name = named(body, "qpb_band", pl, 64);
+    if (name_out) *name_out = name;
+    return "#define QPB_KERNEL_NAME " + name + "\n" + body;
+}
+
+// ---- wide row form (qpb_rowx.hip): one 16-lane row per QP, up to 32 variables
+
+// leading dimensions of the row's dense copies: 2 mod 4 doubles, so that the 16 lanes
+// of a row reading a column (stride ld) hit distinct bank pairs
+static long rowx_ld(long v) { return v + ((2 - v % 4) + 4) % 4; }
+
+RowxLayout rowx_layout(const Plan &pl) {
+    RowxLayout L;
+    const long n = pl.n;
+    L.LDG = rowx_ld(pl.m);
+    L.LDA = rowx_ld(std::max(pl.p, 1L));
+    L.LDP = rowx_ld(n);
+    L.OFF_G = 0;
+    L.OFF_A = L.OFF_G + n * L.LDG;
+    L.OFF_P = L.OFF_A + (pl.p ? n * L.LDA : 0);
+    L.STG_END = (L.OFF_P + n * L.LDP + 1) & ~1L;
+    // H0 and -L by rows padded to the end of their x slot's column range (row e: 16 (e / 16)
+    // + 16 entries, stride 17 / 33 so the 16 lanes' row stores spread over the banks), the
+    // entries beyond the diagonal zero (-L: from the diagonal on): the factor starts from
+    // rows whose upper part is zero, the backward solves read -L's columns without masks
+    const long rows = n <= 16 ? 17 * n : 17 * 16 + 33 * (n - 16);
+    L.OFF_H0 = L.STG_END;
+    L.OFF_L = L.OFF_H0 + rows;
+    L.O_DUMP = L.OFF_L + rows;
+    // LDS_QP = 17 mod 32 doubles: the two QPs of a 32-lane half (rows 0 / 1, 2 / 3: the
+    // bank-conflict groups of ds_read_b64) then sit 34 banks apart -- 2 mod 4 keeps their
+    // column reads (lane strides LDG, LDA: multiples of 4 banks) on disjoint banks, 32 mod
+    // 64 their row reads (consecutive lanes)
+    L.LDS_QP = L.O_DUMP + 16;
+    const char *e = getenv("QPB_WAVE_OPTS");
+    if (e && strstr(e, "QPB_X_EVEN=1"))
+        L.LDS_QP = (L.LDS_QP + 1) & ~1L;                 // (A/B: an even stride)
+    else
+        L.LDS_QP += ((17 - L.LDS_QP % 32) + 32) % 32;
+    return L;
+}
+
+bool rowx_eligible(const Plan &pl, std::string *why) {
+    auto no = [&](const char *m) { if (why) *why = m; return false; };
+    if (pl.n > 32 || pl.p > 32 || pl.m > 128) return no("need n, p <= 32, m <= 128");
+    if (!wave_eligible(pl, why)) return false;
+    const WaveLayout L = wave_layout(pl);
+    if ((long)L.dense.size() != pl.n) return no("a z or y row is not a leaf of the plan's ordering");
+    for (long d = 0; d < pl.n; d++)
+        if (L.dense[d] != d) return no("the x block is not in natural order (leaves-first ordering needed)");
+    if (4 * rowx_layout(pl).LDS_QP * 8 > 160L * 1024) return no("four QPs' dense copies exceed the LDS of a CU");
+    if (why) why->clear();
+    return true;
+}
+
+std::string generate_rowx_kernel(const Plan &pl, std::string *name_out) {
+    const long n = pl.n, m = pl.m, p = pl.p;
+    const RowxLayout L = rowx_layout(pl);
+    std::ostringstream o;
+    o << "#define QPB_ROW_COMMON_ONLY 1\n" << kRowTemplate << "\n#undef QPB_ROW_COMMON_ONLY\n";
+    std::vector<long> gcol;
+    common_header(o, pl, 64, "row-cooperative, two x rows per lane", &gcol, L.LDP, L.LDA, L.LDG);
+    const char *names[] = {"LDG", "LDA", "LDP", "OFF_G", "OFF_A", "OFF_P", "STG_END", "OFF_H0", "OFF_L", "O_DUMP",
+                           "LDS_QP"};
+    const long vals[] = {L.LDG, L.LDA, L.LDP, L.OFF_G, L.OFF_A, L.OFF_P, L.STG_END, L.OFF_H0, L.OFF_L, L.O_DUMP,
+                         L.LDS_QP};
+    for (size_t i = 0; i < sizeof vals / sizeof vals[0]; i++) o << "#define " << names[i] << " " << vals[i] << "\n";
+    auto bools = [&](const char *nm, long rows, long cols, const std::vector<std::vector<int>> &v) {
+        o << "static constexpr bool " << nm << "[" << std::max(rows, 1L) << "][" << cols << "] = {";
+        for (long r = 0; r < std::max(rows, 1L); r++) {
+            o << (r ? "," : "") << "{";
+            for (long j = 0; j < cols; j++) o << (j ? "," : "") << (r < rows ? v[r][j] : 0);
+            o << "}";
+        }
+        o << "};\n";
+    };
+    std::vector<std::vector<int>> gnz(m, std::vector<int>(n, 0)), anz(std::max(p, 1L), std::vector<int>(n, 0)),
+        pnz(n, std::vector<int>(n, 0)), lnz(n, std::vector<int>(n, 0));
+    for (long k = 0; k < pl.G.nnz(); k++) gnz[pl.G.ir[k]][gcol[k]] = 1;
+    for (long j = 0; j < n; j++) {
+        if (p)
+            for (long k = pl.A.jc[j]; k < pl.A.jc[j + 1]; k++) anz[pl.A.ir[k]][j] = 1;
+        for (long k = pl.Pin.jc[j]; k < pl.Pin.jc[j + 1]; k++) pnz[pl.Pin.ir[k]][j] = pnz[j][pl.Pin.ir[k]] = 1;
+    }
+    // L(j, k), j > k, of the x block: the plan's symbolic factor (x rows in natural order
+    // after the leaves, so KKT position p_x + j is x_j)
+    for (long cpos = 0; cpos < pl.N; cpos++) {
+        const long kx = pl.perm[cpos];
+        if (kx >= n) continue;
+        for (long q = pl.Lp[cpos]; q < pl.Lp[cpos + 1]; q++) {
+            const long jx = pl.perm[pl.Li[q]];
+            if (jx < n && jx > kx) lnz[jx][kx] = 1;
+        }
+    }
+    bools("qpb_Gnz", m, n, gnz);
+    bools("qpb_Anz", p, n, anz);
+    bools("qpb_Pnz", n, n, pnz);
+    bools("qpb_lnz", n, n, lnz);
+    const std::string body = o.str() + kRowxTemplate;
+    const std::string name = named(body, "qpb_rowx", pl, 64);
     if (name_out) *name_out = name;
     return "#define QPB_KERNEL_NAME " + name + "\n" + body;
 }

@@ -38,4 +38,14 @@ std::string generate_row_group_kernel(const std::vector<const Plan *> &pls, std:
 bool band_eligible(const Plan &pl, std::string *why);
 long band_lds_bytes(const Plan &pl);
 std::string generate_band_kernel(const Plan &pl, std::string *name_out);
+// Wide row form (qpb_rowx.hip, one QP per 16-lane row, four per wavefront, two x rows
+// per lane): the row form's structure for n, p <= 32, m <= 128 (the controller's
+// 30-variable QPs).  Per-QP LDS doubles: dense column-major G, A, P, H0 (leading
+// dimensions LDG / LDA / LDP), packed strictly-lower -L, 16 dump slots.
+struct RowxLayout {
+    long LDG, LDA, LDP, OFF_G, OFF_A, OFF_P, STG_END, OFF_H0, OFF_L, O_DUMP, LDS_QP;
+};
+RowxLayout rowx_layout(const Plan &pl);
+bool rowx_eligible(const Plan &pl, std::string *why);
+std::string generate_rowx_kernel(const Plan &pl, std::string *name_out);
 }  // namespace qpb

@@ -19,6 +19,8 @@ def qp(name, ids):
     from apf_quadruped_amd import plans, workloads as W
     if name == "c30":
         return W.controller_qp(plans.SEED + 30, ids)
+    if name in ("c30_trot", "c30_crawl"):             # swing-phase controller shapes 30/70/12, 30/69/15
+        return W.controller_qp(plans.SEED + 30, ids, phase=name[4:])
     return plans.standard_qp(name, ids)
 
 

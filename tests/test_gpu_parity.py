@@ -298,7 +298,7 @@ def test_solve_best_fused_argmin(kernel):
 @pytest.mark.parametrize("B", [1, 5, 257, 1024])
 def test_controller_shape_batch_auto_dispatch(B, oracle):
     """Controller stance QPs (30/68/18) as the bench runs them: auto dispatch (the
-    wave kernel with its MFMA G'diag(w)G at every batch size, four QPs per CU),
+    wide row kernel, four QPs per wavefront, at every batch size),
     ragged and full batches; a strided sample vs the oracle run with the plan's
     order: same flags and iteration counts, x / z / s within 1e-9 relative;
     deterministic across launches."""
@@ -366,7 +366,7 @@ def test_wave_two_rows_per_lane_factor_bit_identical(monkeypatch):
     res = {}
     for opt in ("", "QPB_W_DUP=0"):
         monkeypatch.setenv("QPB_WAVE_OPTS", opt)
-        plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], kernel="wave")
+        plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], kernel="wave1")
         assert "#define QPB_ND 30" in plan.wave_source()
         vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
         res[opt] = plan.unpack(plan.solve(**vals, B=B), B)
@@ -393,7 +393,7 @@ def test_wave_structure_knobs_match_plain_build(monkeypatch, order):
     res = {}
     for opt in ("", plain):
         monkeypatch.setenv("QPB_WAVE_OPTS", opt)
-        plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], kernel="wave", order=order)
+        plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], kernel="wave1", order=order)
         vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
         res[opt] = plan.unpack(plan.solve(**vals, B=B), B)
     np.testing.assert_array_equal(res[""]["flag"], res[plain]["flag"])

@@ -1,0 +1,137 @@
+"""GPU parity of the wide row kernel (qpb_rowx.hip: one QP per 16-lane row, four per
+wavefront, two x rows per lane) through the C ABI: the controller's 30-variable QPs
+(stance 30/68/18, trot 30/70/12, crawl 30/69/15; main.cpp:1649, 2005, 3232) and
+synthetic shapes beyond the row kernel's 16/32/16, against the oracle run in the
+plan's own (leaves-first) order.
+
+Bar: identical flags and iteration counts, x / y / z / s and fval within 1e-9 relative
+-- the same factorisation as the oracle's, a different summation order.  (The
+reference goldens of the controller shapes run through the same kernel in
+test_gpu_parity.py::test_wave_kernel_controller_shape_vs_reference.)"""
+import numpy as np
+import pytest
+
+from rowx_cases import dense_qp
+
+
+def _close(got, ref, what, tol=1e-9):
+    scale = max(1.0, float(np.max(np.abs(ref)))) if ref.size else 1.0
+    err = float(np.max(np.abs(got - ref))) if ref.size else 0.0
+    assert err <= tol * scale, (what, err, scale)
+
+
+def _plan(d, **kw):
+    from apf_quadruped_amd.batch import Plan
+    return Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0] if d["p"] else None, d["G"][0],
+                           p_upper=False, **kw)
+
+
+def _run(plan, d, B, **kw):
+    import torch
+    vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"] if d["p"] else None, d["G"], d["c"],
+                                                                d["h"], d["b"] if d["p"] else None).items()}
+    return plan.unpack(plan.solve(**vals, B=B, **kw), B)
+
+
+def _vs_oracle(oracle, plan, d, r, qs, tol=1e-6, maxit=100, sigma_d=0.0, bar=1e-9):
+    """The oracle given the same CSC values and the plan's permutation."""
+    from apf_quadruped_amd.batch import _gather_values
+    n, m, p = d["n"], d["m"], d["p"]
+    (Pjc, Pir), (Gjc, Gir) = plan.patterns.P, plan.patterns.G
+    Pv, Gv = _gather_values(d["P"], Pjc, Pir), _gather_values(d["G"], Gjc, Gir)
+    if p:
+        Ajc, Air = plan.patterns.A
+        Av = _gather_values(d["A"], Ajc, Air)
+    for q in qs:
+        o = oracle.solve_csc(n, m, p, Pjc, Pir, Pv[q], Ajc if p else None, Air if p else None, Av[q] if p else None,
+                             Gjc, Gir, Gv[q], d["c"][q], d["h"][q], d["b"][q] if p else None, sigma_d=sigma_d,
+                             perm=plan.perm, reltol=tol, abstol=tol, maxit=maxit)
+        assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (q, r["flag"][q], o["flag"],
+                                                                           r["iters"][q], o["iters"])
+        keys = ("x", "z", "s")
+        if p:
+            Aq = d["A"][q]
+            if np.linalg.matrix_rank(Aq) < p:          # y unique only modulo null(A')
+                _close(Aq.T @ r["y"][q], Aq.T @ o["y"], f"[{q}].A'y", bar)
+            else:
+                keys = keys + ("y",)
+        for k in keys:
+            _close(r[k][q], o[k], f"[{q}].{k}", bar)
+        _close(np.array([r["fval"][q]]), np.array([o["fval"]]), f"[{q}].fval", bar)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("phase", ["stance", "trot", "crawl"])
+@pytest.mark.parametrize("B", [1, 3, 64, 65, 1024])
+def test_rowx_controller_shapes_vs_oracle(phase, B, oracle):
+    from apf_quadruped_amd import plans, workloads as W
+    d = W.controller_qp(plans.SEED + 30, np.arange(B), phase=phase)
+    plan = _plan(d)
+    assert plan.kernel_for(B) == "wave" and plan.kernel_name(B).startswith("qpb_rowx_"), plan.kernel_name(B)
+    r = _run(plan, d, B)
+    r2 = _run(plan, d, B)
+    for k in ("x", "y", "z", "s", "iters", "fval"):
+        np.testing.assert_array_equal(r[k], r2[k])          # deterministic
+    assert (r["flag"] == 0).all()
+    _vs_oracle(oracle, plan, d, r, sorted(set(range(0, B, max(1, B // 9))) | {B - 1}))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(20, 40, 10), (32, 48, 16), (17, 33, 0), (12, 40, 6), (16, 20, 20), (30, 24, 30)])
+def test_rowx_synthetic_shapes_vs_oracle(shape, oracle):
+    n, m, p = shape
+    B = 70
+    d = dense_qp(n, m, p, B=B, seed=n * 1000 + m * 10 + p)
+    plan = _plan(d)
+    assert plan.kernel_name(B).startswith("qpb_rowx_"), (shape, plan.kernel_name(B))
+    r = _run(plan, d, B)
+    _vs_oracle(oracle, plan, d, r, range(0, B, 5))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tol,maxit,sigma_d", [(1e-2, 100, 0.0), (1e-6, 3, 0.0), (1e-6, 100, 0.2)])
+def test_rowx_options_vs_oracle(tol, maxit, sigma_d, oracle):
+    """Loose tolerance (the controller's 1e-2), truncated maxit (QP_MAXIT with partial
+    iterates) and a sigma_d floor: every option reaches the kernel as the oracle's."""
+    from apf_quadruped_amd import plans, workloads as W
+    B = 40
+    d = W.controller_qp(plans.SEED + 31, np.arange(B))
+    plan = _plan(d)
+    r = _run(plan, d, B, reltol=tol, abstol=tol, maxit=maxit, sigma_d=sigma_d)
+    # loosely converged / truncated iterates (an ill-conditioned KKT far from the
+    # solution) amplify the summation-order rounding: measured 9e-9 at tol 1e-2 and
+    # 1.3e-7 after three iterations (z up to 1e3); bars 1e-7 / 1e-6, the latter the
+    # north-star tolerance itself
+    bar = 1e-9 if (tol < 1e-3 and maxit == 100) else (1e-7 if maxit == 100 else 1e-6)
+    _vs_oracle(oracle, plan, d, r, range(0, B, 4), tol=tol, maxit=maxit, sigma_d=sigma_d, bar=bar)
+
+
+@pytest.mark.gpu
+def test_rowx_zero_pivot_refactor_vs_oracle(oracle):
+    """Force the lazily regularised pivot (QPB_X_LAZYREG): variable 3 decoupled (its P
+    row / column, G and A columns and c entry zeroed), so its pivot is exactly 0 in
+    every factor and the factor is redone with the regularised reciprocals."""
+    B = 40
+    d = dense_qp(24, 40, 8, B=B, seed=5, zero_var=3)
+    plan = _plan(d)
+    assert plan.kernel_name(B).startswith("qpb_rowx_")
+    r = _run(plan, d, B)
+    _vs_oracle(oracle, plan, d, r, range(0, B, 7))
+
+
+@pytest.mark.gpu
+def test_rowx_against_the_wave_form(oracle):
+    """The wide row form and the one-QP-per-wavefront wave form (QPB_KERNEL_NOROW) on the
+    same plan and batch: the same flags and iteration counts, iterates within 2e-9 of
+    each other (each is within 1e-9 of the oracle, in its own summation order)."""
+    from apf_quadruped_amd import plans, workloads as W
+    B = 257
+    d = W.controller_qp(plans.SEED + 32, np.arange(B))
+    rx = _run(_plan(d), d, B)
+    pw = _plan(d, kernel="wave1")
+    assert pw.kernel_name(B).startswith("qpb_wave_")
+    rw = _run(pw, d, B)
+    np.testing.assert_array_equal(rx["flag"], rw["flag"])
+    np.testing.assert_array_equal(rx["iters"], rw["iters"])
+    for k in ("x", "z", "s"):
+        _close(rx[k], rw[k], k, 2e-9)

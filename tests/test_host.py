@@ -120,11 +120,17 @@ def test_wave_kernel_form(name, kernel, qpw):
     plan.compile()                     # hiprtc for gfx950 (or cache hit), no GPU needed
 
 
-def test_controller_shape_keeps_one_qp_per_wave():
+def test_controller_shape_row_forms():
+    """30/68/18: leaves first it takes the wide row form (four QPs per wavefront,
+    qpb_rowx.hip); in the reference's AMD order (51 dense rows) and with
+    QPB_KERNEL_NOROW one QP per wavefront."""
     from apf_quadruped_amd import plans, workloads as W
     d = W.controller_qp(plans.SEED + 30, [0])
     plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], kernel="wave")
-    assert plan.info.wave_ok == 1 and plan.info.wave_qpw == 1
+    assert plan.info.wave_ok == 1 and plan.info.wave_qpw == 4
+    for kw in (dict(kernel="wave1"), dict(order="amd")):
+        plan = Plan.from_dense(d["n"], d["m"], d["p"], d["P"][0], d["A"][0], d["G"][0], **kw)
+        assert plan.info.wave_ok == 1 and plan.info.wave_qpw == 1, kw
 
 
 @pytest.mark.parametrize("name,mask,ok", [("c1", 0b1111, True), ("trot_blfr", 0b1010, True),
