@@ -527,8 +527,8 @@ def apf_leg(tol, dev, B=8192, steps=50, warmup=5):
 def _sq_record(kname, B):
     """The newest SQ-counter summary for this kernel at this batch (profiles/r0N_sq_*.json,
     scripts/gpu_sq*.sh + scripts/sq_summary.py): row-kernel files key "B=<B>", the tree
-    and band files "B=<B>", the wave file "<kernel> B=<B>"."""
-    kind = next((k for k in ("row", "tree", "wave", "band") if kname.startswith("qpb_" + k)), None)
+    and band files "B=<B>", the wave and wide-row files "<kernel> B=<B>"."""
+    kind = next((k for k in ("rowx", "row", "tree", "wave", "band") if kname.startswith("qpb_" + k)), None)
     if kind is None:
         return None, None
     for rnd in ("r05", "r04", "r03"):
@@ -537,7 +537,7 @@ def _sq_record(kname, B):
         if not os.path.exists(f):
             continue
         d = json.load(open(f))
-        r = d.get(f"{kname} B={B}") or (d.get(f"B={B}") if kind != "wave" else None)
+        r = d.get(f"{kname} B={B}") or (d.get(f"B={B}") if kind not in ("wave", "rowx") else None)
         if r:
             return r, "profiles/" + name
     return None, None
@@ -583,19 +583,21 @@ def limiter_for(B):
             "source": "profiles/" + name}
 
 
-def controller_apf_leg(dev, K=8192, steps=20, warmup=3):
+def controller_apf_leg(dev, K=8192, steps=20, warmup=3, order="amd"):
     """The controller's own call, batched: one tick of one robot,
     K APF-sampled candidate targets (main.cpp:1263-1422).  A step = the candidates'
     desired wrenches (qpb_apf_wrench) + their 30/68/18 stance QPs assembled from the
     robot terms (qpb_assemble_controller, shared terms, main.cpp:1471-1647) + one
-    solve with the fused argmin (qpb_solve_best) at the controller's tol 1e-2, with
-    the reference's AMD ordering (QPB_ORDER_AMD: the pivots of qpSWIFT's Permut =
-    NULL, so the answers are the reference's to 1e-6)."""
+    solve with the fused argmin (qpb_solve_best) at the controller's tol 1e-2.
+    order "amd": the reference's AMD ordering (QPB_ORDER_AMD: the pivots of qpSWIFT's
+    Permut = NULL, so the answers are the reference's to 1e-6; one QP per wavefront);
+    "own": the plan's leaves-first ordering (the wide row kernel, four QPs per
+    wavefront; the same QPs, the factor in another pivot order)."""
     import torch
     from apf_quadruped_amd import workloads as W
     from apf_quadruped_amd.batch import Plan, apf_state, apf_wrench, to_tiled
     d = W.controller_qp(0xD06B07 + 30, np.arange(1))
-    plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], order="amd")
+    plan = Plan.from_dense(30, 68, 18, d["P"][0], d["A"][0], d["G"][0], order=order)
     plan.compile()
     st = apf_state(**W.apf_tick_state())      # a plausible synthetic tick state
     rng = np.random.default_rng(11)
@@ -622,7 +624,8 @@ def controller_apf_leg(dev, K=8192, steps=20, warmup=3):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     return {"workload": f"controller call batched: {K} APF-sampled candidates of one tick, wrench + 30/68/18 "
-                        "assembly on the device + solve (AMD order, tol 1e-2) + argmin",
+                        f"assembly on the device + solve ({'AMD' if order == 'amd' else 'leaves-first'} order, "
+                        "tol 1e-2) + argmin",
             "batch": K, "value": K * steps / el, "unit": "QP solves/s", "ms_per_step": el * 1e3 / steps,
             "kernel": plan.kernel_name(K), "traffic": traffic_for(plan.kernel_name(K), K),
             "algorithmic_bytes_per_launch": plan.bytes_per_qp() * K, "input_bytes_per_candidate": 16,
@@ -737,6 +740,7 @@ def main():
                       cpu=None if args.no_cpu else (512, 16)),
             apf_leg(args.tol, dev),
             controller_apf_leg(dev),
+            controller_apf_leg(dev, order="own"),
             trace_leg(args.tol, dev),
         ]
 

@@ -1,6 +1,7 @@
-# SQ / GRBM counter passes (kernel-trace only) of the wave kernels the bench line names:
-# the leaves-first controller shapes (1 024 QPs) and the AMD-ordered controller call
-# (8 192 QPs) -> scripts/sq_summary.py <dir> <out> wave.
+# SQ / GRBM counter passes (kernel-trace only) of the wave and wide-row kernels the bench
+# line names: the leaves-first controller shapes (1 024 QPs, wide row form), the controller
+# call in AMD order (wave form) and leaves first (wide row form), 8 192 QPs
+# -> scripts/sq_summary.py <dir> <out> wave | rowx.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/sqw; export TMPDIR=/tmp
 G1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
 G2="SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU_MUL_F64"
@@ -12,3 +13,4 @@ for grp in "$G1" "$G2" "$G3"; do i=$((i+1))
   case $rc in 124|134|137|139) exit $rc;; esac
 done
 python3 scripts/sq_summary.py gpurun_out/sqw gpurun_out/sqw/sq_wave.json wave > gpurun_out/sqw/summary.log; echo "summary rc=$?"
+python3 scripts/sq_summary.py gpurun_out/sqw gpurun_out/sqw/sq_rowx.json rowx > gpurun_out/sqw/summary_rowx.log; echo "rowx summary rc=$?"

@@ -29,7 +29,7 @@ def load(d, prefix="qpb_row", by_name=False):
     wgs = {}
     for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if not r["Kernel_Name"].startswith(prefix):
+            if not r["Kernel_Name"].startswith(prefix) or (prefix == "qpb_row" and r["Kernel_Name"].startswith("qpb_rowx")):
                 continue
             key = (r["Kernel_Name"].split("(")[0], int(r["Grid_Size"])) if by_name else int(r["Grid_Size"])
             wgs[key] = int(r["Workgroup_Size"])
@@ -43,13 +43,17 @@ def main():
     band = len(sys.argv) > 3 and sys.argv[3] == "band"     # one MPC QP per wavefront (block-tridiagonal)
     tree = (len(sys.argv) > 3 and sys.argv[3] == "tree") or band
     wave = len(sys.argv) > 3 and sys.argv[3] == "wave"      # one QP per wavefront (controller shapes)
-    vals, dur, wgs = load(src, "qpb_band" if band else ("qpb_tree" if tree else ("qpb_wave" if wave else "qpb_row")),
-                          by_name=wave)
+    rowx = len(sys.argv) > 3 and sys.argv[3] == "rowx"      # four QPs per wavefront, up to 32 variables
+    vals, dur, wgs = load(src, "qpb_band" if band else ("qpb_tree" if tree else ("qpb_wave" if wave else
+                                                                                 ("qpb_rowx" if rowx else "qpb_row"))),
+                          by_name=wave or rowx)
     res = {}
     for grid in sorted({g for g, _ in vals}):
         c = {n: sum(v) / len(v) for (g, n), v in vals.items() if g == grid}
         if wave:
             B = grid[1] // 64
+        elif rowx:
+            B = grid[1] // 64 * QPS_PER_WAVE
         elif tree:
             B = grid // wgs[grid]
             B = 1 if B == 8 else B          # one QP: the grid is padded to 8 blocks (one per XCD)
@@ -75,10 +79,13 @@ def main():
         if wave:
             kind = (f"one QP per wavefront: {wps:.2f} waves per SIMD on average, SIMD VALU busy {c['SQ_ACTIVE_INST_VALU'] * 4 / (SIMDS * cyc):.0%}, "
                     f"a wave waits {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.0%} of its cycles (LDS / memory)")
-        kind = kind if (tree or wave) else (f"VALU issue at {wps:.1f} waves per SIMD (SIMD VALU busy {simd_valu:.0%}; neither HBM nor FP64 peak)"
+        if rowx:
+            kind = (f"four QPs per wavefront (wide row form): {wps:.2f} waves per SIMD on average, SIMD VALU busy "
+                    f"{simd_valu:.0%}, a wave waits {c['SQ_WAIT_ANY'] / c['SQ_WAVE_CYCLES']:.0%} of its cycles (LDS)")
+        kind = kind if (tree or wave or rowx) else (f"VALU issue at {wps:.1f} waves per SIMD (SIMD VALU busy {simd_valu:.0%}; neither HBM nor FP64 peak)"
                 if wps > 1.5 else
                 f"latency: one wave on {wps:.0%} of the SIMDs, VALU issue + LDS/memory waits (neither HBM nor FP64 peak)")
-        res[f"{grid[0]} B={B}" if wave else f"B={B}"] = {
+        res[f"{grid[0]} B={B}" if (wave or rowx) else f"B={B}"] = {
             "kind": kind, "simd_valu_busy": simd_valu,
             "kernel_s": t, "clock_ghz": clock / 1e9, "waves": waves,
             "waves_per_simd_avg": wc / (SIMDS * cyc),
@@ -94,7 +101,9 @@ def main():
             "fp64_issue_frac_of_peak": flops_issued / (FP64_PEAK_FLOP_PER_CYC_SIMD * SIMDS * cyc),
             "counters": c,
         }
-    res["reading"] = ("MPC (N = 380) on the band kernel: one QP per wavefront, LDS-resident state (80 KB: two QPs "
+    res["reading"] = ("controller-shape QPs (30 variables) on the wide row form: four QPs per wavefront, one per "
+                      "16-lane row, the per-pass chain of one wave (LDS-bound to one wave per CU); see DESIGN "
+                      "§4c'") if rowx else ("MPC (N = 380) on the band kernel: one QP per wavefront, LDS-resident state (80 KB: two QPs "
                       "per CU, two SIMDs of four busy); the stage recurrences (Schur complement, pivots, sweeps) are "
                       "the chain; no descriptor tables (SALU = loop control only)") if band else ("controller-shape QPs (30 variables), one QP per wavefront: the dense LDL' and the "
                       "triangular solves are one wave's dependency chain; see DESIGN §4b") if wave else ("MPC (N = 380): one QP alone runs 6 passes of ~118 gather / panel steps each (~1 us per "
