@@ -158,17 +158,27 @@ static constexpr int qpb_lst_at(int fams, int k) {
                     if (qpb_has(f, s, i) && k-- == 0) return (s << 12) | (f << 8) | i;
     return 0;
 }
+#ifndef QPB_X_WLDS
+#define QPB_X_WLDS 0      // 1: G'WG reads w_r from LDS (the -L area, dead while H is formed) as a
+                          // row-uniform load in its pipeline instead of a DPP broadcast per G row
+#endif
+static_assert(!QPB_X_WLDS || NZ <= O_DUMP - OFF_L, "QPB_X_WLDS: w does not fit the -L area");
 // G'WG's terms, row-major: (row r, x slot s) with G(r, .) structural in slot s's columns
+// (QPB_X_WLDS: each row led by its w term, slot code 7)
 static constexpr int qpb_gw_n() {
     int n = 0;
-    for (int r = 0; r < NZ; r++)
+    for (int r = 0; r < NZ; r++) {
+        n += QPB_X_WLDS ? 1 : 0;
         for (int s = 0; s < XS; s++) n += qpb_gxs(r, s);
+    }
     return n;
 }
 static constexpr int qpb_gw_at(int k) {
-    for (int r = 0; r < NZ; r++)
+    for (int r = 0; r < NZ; r++) {
+        if (QPB_X_WLDS && k-- == 0) return (7 << 12) | r;
         for (int s = 0; s < XS; s++)
             if (qpb_gxs(r, s) && k-- == 0) return (s << 12) | r;
+    }
     return -1;
 }
 // for k in [0, N): coef_k = ld(k) (an LDS load), fx(k, coef_k); loads CH terms ahead
@@ -262,7 +272,7 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
         for (int u = 0; u < NPL; u++) {
             const int k = c + 16 * u;
             const bool ok = k < QPB_NNZP;
-            vP[u] = ok ? QPB_LDS(&tP[k * QPB_TSTR]) : 0.0;
+            vP[u] = ok ? QPB_LDS(&tP[(ok ? k : QPB_NNZP - 1) * QPB_TSTR]) : 0.0;   // in-bounds address either way
             iP[u] = ok ? qpb_scP[k] : -1;
             iP2[u] = ok ? qpb_scP2[k] : -1;
         }
@@ -270,7 +280,7 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
         for (int u = 0; u < NGL; u++) {
             const int k = c + 16 * u;
             const bool ok = k < QPB_NNZG;
-            vG[u] = ok ? QPB_LDS(&tG[k * QPB_TSTR]) : 0.0;
+            vG[u] = ok ? QPB_LDS(&tG[(ok ? k : QPB_NNZG - 1) * QPB_TSTR]) : 0.0;   // in-bounds address either way
             iG[u] = ok ? qpb_scG[k] : -1;
         }
 #if NY > 0
@@ -279,7 +289,7 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
         for (int u = 0; u < NAL; u++) {
             const int k = c + 16 * u;
             const bool ok = k < QPB_NNZA;
-            vA[u] = ok ? QPB_LDS(&tA[k * QPB_TSTR]) : 0.0;
+            vA[u] = ok ? QPB_LDS(&tA[(ok ? k : QPB_NNZA - 1) * QPB_TSTR]) : 0.0;   // in-bounds address either way
             iA[u] = ok ? qpb_scA[k] : -1;
         }
 #endif
@@ -315,12 +325,13 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
     }
     double cx[XS], hz[ZS], by[YS1];
 #pragma unroll
-    for (int s = 0; s < XS; s++) cx[s] = isx[s] ? QPB_LDS(&a.c[tile * (NX * QPB_TSTR) + (16 * s + c) * QPB_TSTR + ql]) : 0.0;
+    // (clamped row indices: every address in bounds even if the load is issued for a masked lane)
+    for (int s = 0; s < XS; s++) cx[s] = isx[s] ? QPB_LDS(&a.c[tile * (NX * QPB_TSTR) + ixc[s] * QPB_TSTR + ql]) : 0.0;
 #pragma unroll
-    for (int u = 0; u < ZS; u++) hz[u] = isz[u] ? QPB_LDS(&a.h[tile * (NZ * QPB_TSTR) + (16 * u + c) * QPB_TSTR + ql]) : 0.0;
+    for (int u = 0; u < ZS; u++) hz[u] = isz[u] ? QPB_LDS(&a.h[tile * (NZ * QPB_TSTR) + izc[u] * QPB_TSTR + ql]) : 0.0;
 #pragma unroll
     for (int v = 0; v < YS1; v++)
-        by[v] = (NY > 0 && isy[v]) ? QPB_LDS(&a.b[tile * (NY1 * QPB_TSTR) + (16 * v + c) * QPB_TSTR + ql]) : 0.0;
+        by[v] = (NY > 0 && isy[v]) ? QPB_LDS(&a.b[tile * (NY1 * QPB_TSTR) + iyc[v] * QPB_TSTR + ql]) : 0.0;
     QPB_TM(5);
     const double *const Pd = Ls + OFF_P, *const Ad = Ls + OFF_A, *const Gd = Ls + OFF_G;
     // Pd[j LDP + i] = P(i, j) (both triangles); Ad[j LDA + l] = A(l, j); Gd[j LDG + r] = G(r, j)
@@ -383,17 +394,25 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
         // += G(r, row) w_r G(r, j): lane j's G(r, j) by DPP broadcast against the lane's own
         // G(r, row) w_r -- the same LDS values serve as source and coefficient; the loads
         // pipelined ahead of the rows' FMAs
-        double gc[XS];
+        double gc[XS], wl = 0.0;
+        if constexpr (QPB_X_WLDS) {
+#pragma unroll
+            for (int u = 0; u < ZS; u++)
+                if (isz[u]) Ls[OFF_L + 16 * u + c] = w[u];
+            qpb_wsync();
+        }
         qpb_xpipe<qpb_gw_n()>(
             [&](auto kc) -> double {
                 constexpr int t = qpb_gw_at(decltype(kc)::value), ts = t >> 12, r = t & 4095;
-                return Gd[ixc[ts] * LDG + r];
+                if constexpr (ts == 7) return Ls[OFF_L + r];
+                else return Gd[ixc[ts] * LDG + r];
             },
             [&](auto kc, double cf) {
                 constexpr int k = decltype(kc)::value, t = qpb_gw_at(k), ts = t >> 12, r = t & 4095;
-                gc[ts] = cf;
+                if constexpr (ts == 7) wl = cf;
+                else gc[ts] = cf;
                 if constexpr (k + 1 == qpb_gw_n() || (qpb_gw_at(k + 1) & 4095) != r) {   // the row's last term
-                    const double wr = qpb_nb<(r & 15)>(w[r >> 4]);
+                    const double wr = QPB_X_WLDS ? wl : qpb_nb<(r & 15)>(w[r >> 4]);
                     double cr[XS];
                     qpb_for<0, XS>([&](auto sc) {
                         constexpr int s2 = decltype(sc)::value;
@@ -590,26 +609,26 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
 #if QPB_SERVE
     const double *wi = a.win;                  // the host's block (KernelArgs::win, QP 0)
 #pragma unroll
-    for (int s = 0; s < XS; s++) if (isx[s]) x[s] = QPB_LDS(&wi[16 * s + c]);
+    for (int s = 0; s < XS; s++) if (isx[s]) x[s] = QPB_LDS(&wi[ixc[s]]);
 #pragma unroll
-    for (int v = 0; v < YS; v++) if (isy[v]) y[v] = QPB_LDS(&wi[NX + 16 * v + c]);
+    for (int v = 0; v < YS; v++) if (isy[v]) y[v] = QPB_LDS(&wi[NX + iyc[v]]);
 #pragma unroll
     for (int u = 0; u < ZS; u++)
-        if (isz[u]) { z[u] = QPB_LDS(&wi[NX + NY + 16 * u + c]); sl[u] = QPB_LDS(&wi[NX + NY + NZ + 16 * u + c]); }
+        if (isz[u]) { z[u] = QPB_LDS(&wi[NX + NY + izc[u]]); sl[u] = QPB_LDS(&wi[NX + NY + NZ + izc[u]]); }
     const int *wfl = reinterpret_cast<const int *>(wi + NX + NY + 2 * NZ);
     const long it0 = QPB_LDS(&wfl[1]);
     const int flag0 = QPB_LDS(&wfl[0]);
     sigma = QPB_LDS(&wi[NX + NY + 2 * NZ + 1]);
 #else
 #pragma unroll
-    for (int s = 0; s < XS; s++) if (isx[s]) x[s] = QPB_LDS(&a.x[tile * (NX * 64) + (16 * s + c) * 64 + ql]);
+    for (int s = 0; s < XS; s++) if (isx[s]) x[s] = QPB_LDS(&a.x[tile * (NX * 64) + ixc[s] * 64 + ql]);
 #pragma unroll
-    for (int v = 0; v < YS; v++) if (isy[v]) y[v] = QPB_LDS(&a.y[tile * (NY1 * 64) + (16 * v + c) * 64 + ql]);
+    for (int v = 0; v < YS; v++) if (isy[v]) y[v] = QPB_LDS(&a.y[tile * (NY1 * 64) + iyc[v] * 64 + ql]);
 #pragma unroll
     for (int u = 0; u < ZS; u++)
         if (isz[u]) {
-            z[u] = QPB_LDS(&a.z[tile * (NZ * 64) + (16 * u + c) * 64 + ql]);
-            sl[u] = QPB_LDS(&a.s[tile * (NZ * 64) + (16 * u + c) * 64 + ql]);
+            z[u] = QPB_LDS(&a.z[tile * (NZ * 64) + izc[u] * 64 + ql]);
+            sl[u] = QPB_LDS(&a.s[tile * (NZ * 64) + izc[u] * 64 + ql]);
         }
     const long it0 = QPB_LDS(&a.iters[qc]);   // IterationCount the QP enters with
     const int flag0 = QPB_LDS(&a.flag[qc]);   // stats->Flag it enters with (QP_FATAL after setup)

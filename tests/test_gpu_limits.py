@@ -1,24 +1,30 @@
 """GPU parity at the size limits of each kernel form, on random dense QPs.
 
 The dispatch rules (include/qpswift_hip.h, qpb_plan_info): the row form of the
-wave kernel holds n, p <= 16, m <= 32 (four QPs per wavefront); the one-QP-per-
-wavefront form holds n, p <= 64, m <= 256 with every G row non-empty; beyond
-that a plan runs the lane or tree kernel.  Each case sits on or just past one of
-those edges and is checked against the oracle run with the plan's own KKT
-permutation (same factorisation, so rounding-level agreement: 1e-9 relative, the
-bar of test_gpu_parity.py) with identical flags and iteration counts, on a
-ragged batch of 5 QPs.
+wave kernel holds n, p <= 16, m <= 32 (four QPs per wavefront); the wide row form
+n, p <= 32, m <= 128 in leaves-first order while four QPs' dense copies fit the LDS
+(four QPs per wavefront, two x rows per lane), except an upper-triangle P with
+off-diagonal entries past 16 variables (not validated); the one-QP-per-wavefront form holds
+n, p <= 64, m <= 256 with every G row non-empty; beyond that a plan runs the lane or
+tree kernel.  Each case sits on or just past one of those edges and is checked
+against the oracle run with the plan's own KKT permutation (same factorisation, so
+rounding-level agreement: 1e-9 relative, the bar of test_gpu_parity.py) with
+identical flags and iteration counts, on a ragged batch of 5 QPs.
 
 The QPs: P = M M' + n I (dense SPD), A dense with full row rank, G dense, and
 h = G x0 + slack, b = A x0 for a random x0 (feasible, strictly inside)."""
 import numpy as np
 import pytest
 
-# (n, m, p, expected kernel form: "row" | "wave" | "other")
+# (n, m, p, expected kernel form: "row" | "rowx" | "wave" | "other")
 LIMIT_CASES = [
     (16, 32, 16, "row"),     # the row form at its limit
-    (16, 33, 6, "wave"),     # one inequality too many for a 16-lane row
-    (17, 20, 6, "wave"),     # one variable too many
+    (16, 33, 6, "rowx"),     # one inequality too many for a 16-lane row: the wide row form
+    (17, 20, 6, "wave"),     # one variable too many; dense upper-triangle P past 16 variables: wave form
+    (32, 48, 16, "wave"),    # ditto (the wide row form's variable limit: tests/test_gpu_rowx.py, P full)
+    (12, 128, 6, "rowx"),    # ... and at its inequality limit
+    (12, 129, 6, "wave"),    # one inequality past it
+    (32, 64, 16, "wave"),    # four QPs' dense copies past the LDS of a CU
     (48, 96, 24, "wave"),
     (64, 128, 8, "wave"),    # the one-QP-per-wavefront form at its variable limit
     (65, 40, 10, "other"),   # past it: lane or tree kernel
@@ -53,7 +59,9 @@ def test_kernel_limits_match_oracle(n, m, p, form, oracle):
     d = random_qps(n, m, p, B, seed=1000 * n + m + p)
     plan = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0])
     info = plan.info
-    got_form = ("row" if info.wave_qpw == 4 else "wave") if info.wave_ok else "other"
+    kn = plan.kernel_name(B)
+    got_form = ("rowx" if kn.startswith("qpb_rowx_") else "row" if info.wave_qpw == 4 else "wave") \
+        if info.wave_ok else "other"
     assert got_form == form, (n, m, p, got_form)
     vals = plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"])
     r = plan.unpack(plan.solve(**vals, B=B, reltol=1e-6, abstol=1e-6), B)

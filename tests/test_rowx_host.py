@@ -42,7 +42,18 @@ def test_row_kernel_keeps_the_small_plans():
                                       ((24, 130, 4), False)])
 def test_eligibility_by_shape(shape, ok):
     d = dense_qp(*shape, B=1, seed=sum(shape))
-    name = _plan(d).kernel_name(64)
+    name = _plan(d, p_upper=False).kernel_name(64)
+    assert name.startswith("qpb_rowx_") == ok, (shape, name)
+
+
+@pytest.mark.parametrize("shape,ok", [((20, 40, 10), False), ((17, 20, 6), False), ((16, 33, 6), True),
+                                      ((12, 40, 6), True)])
+def test_upper_p_eligibility(shape, ok):
+    """An upper-triangle P whose off-diagonal entries reach rows < 16 keeps plans past
+    16 variables on the wave form (not validated on the GPU); n <= 16 is validated,
+    and so is the controller's upper P (test_controller_shapes_take_the_wide_row_kernel)."""
+    d = dense_qp(*shape, B=1, seed=sum(shape))
+    name = _plan(d, p_upper=True).kernel_name(64)
     assert name.startswith("qpb_rowx_") == ok, (shape, name)
 
 
