@@ -4,6 +4,7 @@
 #   PART=2: the rocprofv3 kernel trace of the same bench (per-kernel, per-grid durations),
 #           one FETCH_SIZE and one WRITE_SIZE pass over a short bench (-> traffic.json), SQ
 #           counter passes of the row kernel (headline) and of the band kernel (configs[3])
+#   PART=3: SQ counter passes of the wave and wide-row kernels the bench names (gpu_sq_wave.sh)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/fin; export TMPDIR=/tmp
 fatal() { case "$1" in 124|134|137|139) echo "fatal rc=$1 at $2"; exit $1;; esac; }
 if [ "${PART:-1}" = 1 ]; then
@@ -15,6 +16,9 @@ for sh in c1 c30 c30_trot c30_crawl; do
   timeout -k 10 200 python -u scripts/dropin_latency.py --shape $sh --mode fast >> gpurun_out/fin/dropin_latency.jsonl 2>> gpurun_out/fin/dropin_latency.err; rc=$?
   echo "dropin latency $sh rc=$rc"; fatal $rc dropin_$sh
 done
+elif [ "${PART}" = 3 ]; then
+bash scripts/gpu_sq_wave.sh > gpurun_out/fin/sq_wave.log 2>&1; rc=$?; echo "sq wave rc=$rc"; cat gpurun_out/fin/sq_wave.log | tail -6; fatal $rc sq_wave
+cp gpurun_out/sqw/sq_wave.json gpurun_out/fin/sq_wave.json; cp gpurun_out/sqw/sq_rowx.json gpurun_out/fin/sq_rowx.json
 else
 rm -rf gpurun_out/fin/prof; timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/fin/prof -o run -- python3 bench.py --no-cpu > gpurun_out/fin/prof.log 2>&1; rc=$?; echo "rocprof rc=$rc"; fatal $rc rocprof
 python3 scripts/prof_summary.py gpurun_out/fin/prof/run_results.db gpurun_out/fin/kernel_by_grid.csv gpurun_out/fin/kernel_stats.csv > /dev/null; rc=$?; echo "summary rc=$rc"

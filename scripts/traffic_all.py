@@ -6,7 +6,7 @@ command (FETCH_SIZE, WRITE_SIZE) -> profiles/traffic.json, keyed "<kernel>@<batc
 bytes per launch = 2 * FETCH_SIZE + WRITE_SIZE (KiB units), the MI355X_MICROARCH.md
 HBM-section correction (gfx950 FETCH_SIZE counts half the bytes of coalesced reads;
 WRITE_SIZE is exact for streaming stores).  The batch of a launch follows from its grid:
-QPs per workgroup = 4 per wave (row form), 1 per wave (wave form), 1 per workgroup
+QPs per workgroup = 4 per wave (row and wide row forms), 1 per wave (wave form), 1 per workgroup
 (tree, band), 1 per lane (lane kernels, qpb_ipm_*); groups (qpb_rowgroup*) and helper kernels
 are keyed by their grid in threads ("<kernel>@grid<threads>").  bench.py reads the
 entry of the kernel and batch each leg launches (traffic_for)."""
@@ -19,7 +19,7 @@ from collections import defaultdict
 
 def batch_of(kname, grid, wg):
     blocks = grid // wg
-    if kname.startswith("qpb_row_"):
+    if kname.startswith("qpb_row_") or kname.startswith("qpb_rowx_"):
         return blocks * 4 * (wg // 64)
     if kname.startswith("qpb_wave_"):
         return blocks * (wg // 64)
