@@ -171,11 +171,22 @@ double kkt_slot_value(const qpb::Slot &sl, const double *P, const double *A, con
     return 0.0;
 }
 
+// QPSWIFT_HIP_ORDER=own: with Permut = NULL the plan takes its own KKT ordering (z and
+// y rows first where the pattern allows: the wide row kernel for the controller's
+// 30-variable QPs, DESIGN.md 4c') instead of the reference's AMD (qpSWIFT.c:424-440).
+// Same QP, same algorithm, another elimination order: x agrees to rounding, not bit
+// for bit, and an iteration count can differ where a stopping test is marginal.
+bool own_order() {
+    const char *e = std::getenv("QPSWIFT_HIP_ORDER");
+    return e && std::strcmp(e, "own") == 0;
+}
+
 PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const long *Ajc, const long *Air,
                  const long *Gjc, const long *Gir, const long *perm, bool exact, std::string &err) {
     std::string key;
-    const long hdr[5] = {n, m, p, exact ? 1L : 0L, perm ? 1L : 0L};
-    key_append(key, hdr, 5);
+    const bool own = !perm && own_order();
+    const long hdr[6] = {n, m, p, exact ? 1L : 0L, perm ? 1L : 0L, own ? 1L : 0L};
+    key_append(key, hdr, 6);
     key_append(key, Pjc, n + 1);
     key_append(key, Pir, Pjc[n]);
     if (p > 0) {
@@ -191,7 +202,7 @@ PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const
         if (it != g_cache.end()) return it->second;
     }
     qpb_plan *raw = nullptr;
-    int rc = qpb_plan_create(&raw, n, m, p, QPB_P_FULL | QPB_ORDER_AMD | (exact ? QPB_EXACT : 0), Pjc, Pir, p > 0 ? Ajc : nullptr,
+    int rc = qpb_plan_create(&raw, n, m, p, QPB_P_FULL | (own ? 0 : QPB_ORDER_AMD) | (exact ? QPB_EXACT : 0), Pjc, Pir, p > 0 ? Ajc : nullptr,
                              p > 0 ? Air : nullptr, Gjc, Gir, perm);
     if (rc) {
         err = qpb_last_error();

@@ -3,11 +3,13 @@ does (QP_SETUP_dense -> options -> QP_SOLVE -> read x -> QP_CLEANUP_dense,
 main.cpp:1649-1663), next to the reference qpSWIFT on the host CPU (oracle/_ref,
 when present).
 
-    python scripts/dropin_latency.py [--ticks N] [--shape c1|c30] [--mode exact|fast] [--permut amd|leaves]
+    python scripts/dropin_latency.py [--ticks N] [--shape c1|c30] [--mode exact|fast] [--permut amd|leaves|own]
 
 --permut leaves passes the leaves-first KKT ordering (z rows, y rows, then x) through
 QP_SETUP_dense's own Permut argument (qpSWIFT.c:296-303) to both the drop-in and the CPU
-reference, instead of NULL (-> AMD, what the controller passes).
+reference, instead of NULL (-> AMD, what the controller passes).  --permut own passes NULL
+(as the controller does) with QPSWIFT_HIP_ORDER=own: the drop-in then orders the KKT its own
+way, while the CPU reference runs its AMD order (max_rel_x_diff: the two orders' agreement).
 """
 import argparse
 import ctypes as C
@@ -29,13 +31,17 @@ def main():
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--tol", type=float, default=1e-2)        # the controller's (main.cpp:1651)
     ap.add_argument("--setup-init", type=int, default=1, help="QPSWIFT_HIP_SETUP_INIT (recorded only)")
-    ap.add_argument("--permut", default="amd", choices=["amd", "leaves"])
+    ap.add_argument("--permut", default="amd", choices=["amd", "leaves", "own"])
     a = ap.parse_args()
     from apf_quadruped_amd import _lib, plans, qpswift_abi as abi, workloads as W
     if a.mode == "exact":
         os.environ["QPSWIFT_HIP_EXACT"] = "1"
     else:
         os.environ.pop("QPSWIFT_HIP_EXACT", None)
+    if a.permut == "own":
+        os.environ["QPSWIFT_HIP_ORDER"] = "own"
+    else:
+        os.environ.pop("QPSWIFT_HIP_ORDER", None)
     gen = {"c1": lambda ids: W.contact_force_qp(plans.SEED + 1, ids),
            "c30": lambda ids: W.controller_qp(plans.SEED + 30, ids),
            "c30_trot": lambda ids: W.controller_qp(plans.SEED + 31, ids, phase="trot"),

@@ -166,6 +166,23 @@ def test_setup_null_permut_fills_reference_perm_and_amd_result():
     _lib.lib().QP_CLEANUP_dense(qp)
 
 
+def test_setup_null_permut_own_order(monkeypatch):
+    """QPSWIFT_HIP_ORDER=own: with Permut = NULL the plan orders the KKT its own way --
+    for the controller's 30-variable QP the leaves-first order (z rows, y rows, then x)
+    of the wide row kernel -- and mirrors that permutation in kkt->P; AMD_RESULT stays 0."""
+    monkeypatch.setenv("QPSWIFT_HIP_ORDER", "own")
+    g = golden("c30_tol1e-2")
+    n, m, p = int(g["n"]), int(g["m"]), int(g["p"])
+    qp, keep = dropin.setup_dense(*_golden_dense_args(g, 0))
+    q = qp.contents
+    perm = _arr(q.kkt.contents.P, n + m + p)
+    assert not np.array_equal(perm, g["perm"][0])
+    assert np.array_equal(np.sort(perm), np.arange(n + m + p))
+    assert np.array_equal(perm[m + p:], np.arange(n))           # the x block last, natural order
+    assert q.stats.contents.AMD_RESULT == 0
+    _lib.lib().QP_CLEANUP_dense(qp)
+
+
 def _no_gpu():
     try:
         import torch
@@ -229,6 +246,29 @@ def test_dropin_leaves_first_permut_matches_oracle(name, oracle):
         for k in ("x", "z", "s") + (("y",) if p else ()):
             scale = max(1.0, float(np.abs(o[k]).max()))
             assert np.abs(r[k] - o[k]).max() <= 1e-6 * scale, (name, q, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c30_tol1e-2", "c30_trot_tol1e-2", "c30_crawl_tol1e-2", "c30_tol1e-6", "c1_tol1e-2"])
+def test_dropin_own_order_null_permut(name, monkeypatch):
+    """The controller's call (Permut = NULL) under QPSWIFT_HIP_ORDER=own: the drop-in
+    factors in its own (leaves-first) order on the wide row kernel while the goldens
+    come from the reference's AMD order.  Another elimination order of the same QP:
+    flag and iteration count equal, x within 1e-6 (north-star tolerance), z, s within
+    1e-5 (the orders regularise different y pivots: INTEGRATION.md); y is not compared
+    (rank-deficient A: not unique)."""
+    monkeypatch.setenv("QPSWIFT_HIP_ORDER", "own")
+    g = golden(name)
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    for q in range(g["x"].shape[0]):
+        r = dropin.solve_dense(*_golden_dense_args(g, q), ordering=int(g["ordering"]), reltol=tol, abstol=tol,
+                               maxit=maxit)
+        assert r["flag"] == int(g["flag"][q]), r["error"]
+        assert r["iters"] == int(g["iters"][q]), (name, q)
+        assert r["amd_result"] == 0
+        for k, bar in (("x", 1e-6), ("z", 1e-5), ("s", 1e-5)):
+            scale = max(1.0, float(np.abs(g[k][q]).max()))
+            assert np.abs(r[k] - g[k][q]).max() <= bar * scale, (name, q, k)
 
 
 DENSE = ["c1_tol1e-6", "c1_tol1e-2", "c1_rowmajor", "c1_noeq", "edge_zero_g_row", "mixed_stance4",
