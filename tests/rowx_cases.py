@@ -5,9 +5,11 @@ beyond the row kernel's n, p <= 16, m <= 32.  Feasible by construction
 import numpy as np
 
 
-def dense_qp(n, m, p, B=4, seed=0, g_density=0.3, a_density=0.6, p_density=0.3, zero_var=None):
+def dense_qp(n, m, p, B=4, seed=0, g_density=0.3, a_density=0.6, p_density=0.3, zero_var=None, p_offdiag_from=0):
     """zero_var: a variable decoupled from everything (its P row / column, G and A
-    columns, c entry zero) -- its pivot is exactly 0 in every factor."""
+    columns, c entry zero) -- its pivot is exactly 0 in every factor.
+    p_offdiag_from: P's off-diagonal entries only among variables >= it (the
+    controller's skyline P: its coupled block sits in variables 18-29)."""
     rng = np.random.default_rng(seed)
     others = np.array([j for j in range(n) if j != zero_var])
     # one sparsity pattern per plan (every QP of the batch shares it), values per QP
@@ -16,7 +18,9 @@ def dense_qp(n, m, p, B=4, seed=0, g_density=0.3, a_density=0.6, p_density=0.3, 
     apat = rng.random((p, n)) < a_density
     apat[np.arange(p), others[np.arange(p) % len(others)]] = True
     ppat = rng.random((n, n)) < p_density
-    ppat = ppat | ppat.T | np.eye(n, dtype=bool)
+    ppat = ppat | ppat.T
+    ppat[:p_offdiag_from, :] = ppat[:, :p_offdiag_from] = False
+    ppat = ppat | np.eye(n, dtype=bool)
     if zero_var is not None:
         gpat[:, zero_var] = apat[:, zero_var] = ppat[zero_var, :] = ppat[:, zero_var] = False
     M = rng.standard_normal((B, n, n)) * 0.4

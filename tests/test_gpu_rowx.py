@@ -135,3 +135,27 @@ def test_rowx_against_the_wave_form(oracle):
     np.testing.assert_array_equal(rx["iters"], rw["iters"])
     for k in ("x", "z", "s"):
         _close(rx[k], rw[k], k, 2e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(24, 40, 8), (20, 40, 10), (30, 68, 18)])
+def test_rowx_upper_p_past_16_vs_oracle(shape, oracle):
+    """P stored as its upper triangle with off-diagonal entries only among variables
+    >= 16 (the controller's skyline class, which the wide row form accepts past 16
+    variables; rowx_eligible), a ragged batch of 65: against the oracle on the dense
+    QP in the plan's own order, same flags and iterations, 1e-9 relative."""
+    from apf_quadruped_amd.batch import Plan
+    n, m, p = shape
+    B = 65
+    d = dense_qp(n, m, p, B=B, seed=7 * n + m, p_offdiag_from=16)
+    plan = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0], p_upper=True)
+    assert plan.kernel_name(B).startswith("qpb_rowx_")
+    r = _run(plan, d, B, reltol=1e-6, abstol=1e-6)
+    cm = lambda M: np.ascontiguousarray(M.transpose(0, 2, 1)).reshape(M.shape[0], -1)
+    Pc, Ac, Gc = cm(d["P"]), cm(d["A"]), cm(d["G"])
+    for q in range(0, B, 4):
+        o = oracle.solve_dense(n, m, p, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm,
+                               reltol=1e-6, abstol=1e-6)
+        assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (shape, q)
+        for k in ("x", "z", "s"):
+            _close(r[k][q], o[k], f"[{q}].{k}")
