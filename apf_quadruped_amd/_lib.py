@@ -67,6 +67,8 @@ def lib() -> C.CDLL:
     L.qpb_version.restype = C.c_char_p
     L.qpb_compiler.restype = C.c_char_p
     L.qpb_audit_dpp.argtypes = [vp, C.c_long, C.c_char_p, C.c_long]
+    L.qpb_join_fixup.argtypes = [C.c_char_p, C.c_long, C.c_char_p, C.c_long]
+    L.qpb_join_fixup.restype = C.c_long
     L.qpb_default_settings.argtypes = [C.POINTER(QpbSettings)]
     L.qpb_plan_create.restype = C.c_int
     L.qpb_plan_create.argtypes = [C.POINTER(vp), C.c_long, C.c_long, C.c_long, C.c_int,

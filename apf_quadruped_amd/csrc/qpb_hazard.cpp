@@ -290,12 +290,232 @@ int asm_fixup(std::string &s, std::string *report) {
     return sites;
 }
 
+// ---- lane-partial code at a divergent region's join -------------------------------
+// LLVM lowers `if (divergent) {...}` to
+//     s_and_saveexec_b64 s[a:b], cond ; s_cbranch_execz J ; <then> ; J: s_or_b64 exec, exec, s[a:b]
+// The register allocator treats J as the join block, i.e. code there runs for every
+// lane -- but anything it places at J *before* the EXEC restore runs with the then
+// region's EXEC (the skip path arrives with EXEC = 0).  The ROCm 7.2 backend does place
+// live-range-split copies there, next to SGPR spills (v_writelane, which it counts as
+// the block's prologue): e.g. `v_accvgpr_write_b32 a18, v124` parking a value every lane
+// reads later, made only for the then-lanes.  The wide row kernel's memory-aperture
+// violation was exactly that.  Moving those instructions to just after
+// the restore gives them the semantics the allocator assumed.
+namespace {
+
+struct Ops {
+    std::string mn;
+    std::vector<std::pair<int, int>> defs, uses;   // v: 0..511, a: 512.., s: 1024.. (vcc 2024, exec 2026, m0 2028)
+    bool mem = false, wait = false, valu_like = false, exec_def = false, trans = false, branch = false;
+};
+
+bool parse_reg(const std::string &tok, std::pair<int, int> &r) {
+    size_t i = 0;
+    while (i < tok.size() && (tok[i] == ' ' || tok[i] == '\t' || tok[i] == '-' || tok[i] == '|' || tok[i] == '!'))
+        i++;
+    const std::string t = tok.substr(i);
+    if (t.rfind("vcc", 0) == 0) { r = {2024, 2025}; return true; }
+    if (t.rfind("exec", 0) == 0) { r = {2026, 2027}; return true; }
+    if (t.rfind("m0", 0) == 0) { r = {2028, 2028}; return true; }
+    if (t.size() < 2) return false;
+    const int base = t[0] == 'v' ? 0 : t[0] == 'a' ? 512 : t[0] == 's' ? 1024 : -1;
+    if (base < 0) return false;
+    int a = 0, b = 0;
+    if (t[1] == '[') {
+        if (sscanf(t.c_str() + 2, "%d:%d]", &a, &b) != 2) return false;
+    } else if (isdigit((unsigned char)t[1])) {
+        a = b = atoi(t.c_str() + 1);
+    } else {
+        return false;
+    }
+    r = {base + a, base + b};
+    return true;
+}
+
+Ops parse_ops(const std::string &text) {
+    Ops o;
+    std::istringstream ts(text);
+    ts >> o.mn;
+    std::string rest;
+    std::getline(ts, rest);
+    std::vector<std::string> ops;
+    std::string cur;
+    for (char ch : rest) {
+        if (ch == ',') { ops.push_back(cur); cur.clear(); }
+        else cur += ch;
+    }
+    if (!cur.empty()) {
+        std::istringstream ls(cur);
+        std::string first;
+        ls >> first;
+        ops.push_back(first);
+    }
+    const std::string &m = o.mn;
+    auto starts = [&](const char *p) { return m.rfind(p, 0) == 0; };
+    const bool store = starts("global_store") || starts("buffer_store") || starts("scratch_store") ||
+                       starts("flat_store") || starts("ds_write") || starts("global_atomic") ||
+                       starts("buffer_atomic") || starts("ds_add") || starts("s_store");
+    const bool nodef = store || starts("s_cmp") || starts("s_bitcmp") || starts("s_waitcnt") || starts("s_nop") ||
+                       starts("s_branch") || starts("s_cbranch") || starts("s_endpgm") || starts("s_barrier") ||
+                       starts("s_setprio") || starts("s_sleep");
+    o.mem = starts("global_") || starts("buffer_") || starts("scratch_") || starts("flat_") || starts("ds_") ||
+            starts("s_load") || starts("s_buffer_load") || starts("s_store");
+    o.wait = starts("s_waitcnt");
+    o.branch = starts("s_branch") || starts("s_cbranch") || starts("s_endpgm") || starts("s_setpc");
+    o.valu_like = (starts("v_") || o.mem) && !starts("s_");
+    for (const char *t : {"v_rcp_", "v_rsq_", "v_sqrt_", "v_exp_", "v_log_", "v_sin_", "v_cos_"})
+        if (starts(t)) o.trans = true;
+    const bool reads_dst = m.find("mac") != std::string::npos || m.find("_dpp") != std::string::npos ||
+                           starts("v_writelane") || m.find("saveexec") != std::string::npos;
+    for (size_t k = 0; k < ops.size(); k++) {
+        std::pair<int, int> r;
+        if (!parse_reg(ops[k], r)) continue;
+        if (k == 0 && !nodef) {
+            o.defs.push_back(r);
+            if (reads_dst) o.uses.push_back(r);
+        } else {
+            o.uses.push_back(r);
+        }
+        if (k == 1 && m.find("_co_") != std::string::npos && r.first >= 1024) o.defs.push_back(r);   // carry-out
+    }
+    if (m.find("saveexec") != std::string::npos) { o.defs.push_back({2026, 2027}); o.uses.push_back({2026, 2027}); }
+    for (auto &d : o.defs)
+        if (d.first == 2026) o.exec_def = true;
+    if (starts("v_cmpx")) o.exec_def = true;
+    return o;
+}
+
+bool any_overlap(const std::vector<std::pair<int, int>> &a, const std::vector<std::pair<int, int>> &b) {
+    for (auto &x : a)
+        for (auto &y : b)
+            if (x.first <= y.second && y.first <= x.second) return true;
+    return false;
+}
+
+}  // namespace
+
+int join_fixup(std::string &s, std::string *report) {
+    std::vector<std::string> lines;
+    {
+        std::istringstream in(s);
+        std::string l;
+        while (std::getline(in, l)) lines.push_back(l);
+    }
+    auto code_of = [&](size_t li) -> std::string {      // instruction text, "" for non-instructions
+        std::string t = lines[li];
+        const size_t c = t.find(';');
+        if (c != std::string::npos) t = t.substr(0, c);
+        const size_t b0 = t.find_first_not_of(" \t");
+        if (b0 == std::string::npos) return "";
+        t = t.substr(b0);
+        while (!t.empty() && (t.back() == ' ' || t.back() == '\t' || t.back() == '\r')) t.pop_back();
+        if (t.empty() || t[0] == '.' || t.back() == ':') return "";
+        return t;
+    };
+    auto label_of = [&](size_t li) -> std::string {
+        std::string t = lines[li];
+        const size_t c = t.find(';');
+        if (c != std::string::npos) t = t.substr(0, c);
+        while (!t.empty() && (t.back() == ' ' || t.back() == '\t' || t.back() == '\r')) t.pop_back();
+        if (!t.empty() && t.back() == ':' && t[0] != ' ' && t[0] != '\t') return t.substr(0, t.size() - 1);
+        return "";
+    };
+    std::map<std::string, size_t> label_line;
+    for (size_t li = 0; li < lines.size(); li++) {
+        const std::string lb = label_of(li);
+        if (!lb.empty()) label_line[lb] = li;
+    }
+    struct Move { size_t restore; std::vector<size_t> moved; int pad; };
+    std::map<size_t, Move> moves;                            // keyed by the restore line
+    int fixed = 0, unfixed = 0, insns = 0;
+    std::ostringstream why;
+    for (size_t li = 0; li < lines.size(); li++) {
+        const std::string t = code_of(li);
+        if (t.rfind("s_cbranch_execz", 0) != 0) continue;
+        std::istringstream ts(t);
+        std::string mn, tgt;
+        ts >> mn >> tgt;
+        auto it = label_line.find(tgt);
+        if (it == label_line.end()) continue;
+        std::vector<size_t> cand, other;                      // lines before the restore
+        size_t restore = 0;
+        bool ok = true;
+        for (size_t k = it->second + 1; k < lines.size(); k++) {
+            if (!label_of(k).empty()) { ok = false; break; }  // another block starts: not this pattern
+            const std::string c = code_of(k);
+            if (c.empty()) continue;
+            const Ops o = parse_ops(c);
+            if (o.exec_def) {
+                if (o.mn == "s_or_b64" && c.find("exec, exec,") != std::string::npos) restore = k;
+                else ok = false;
+                break;
+            }
+            if (o.branch) { ok = false; break; }
+            const bool lane_masked = o.valu_like && o.mn.rfind("v_writelane", 0) != 0 &&
+                                     o.mn.rfind("v_readlane", 0) != 0 && o.mn.rfind("v_readfirstlane", 0) != 0 &&
+                                     o.mn.rfind("v_cmp", 0) != 0;
+            (lane_masked ? cand : other).push_back(k);
+        }
+        if (!ok || !restore || cand.empty()) continue;
+        // may each candidate move past the instructions after it (and the restore)?
+        bool movable = true;
+        for (size_t a : cand) {
+            const Ops A = parse_ops(code_of(a));
+            if (A.trans) movable = false;
+            std::vector<size_t> past;
+            for (size_t b : other)
+                if (b > a) past.push_back(b);
+            past.push_back(restore);
+            for (size_t b : past) {
+                const Ops Bo = parse_ops(code_of(b));
+                if (any_overlap(A.uses, Bo.defs) || any_overlap(A.defs, Bo.uses) || any_overlap(A.defs, Bo.defs))
+                    movable = false;
+                if (A.mem && (Bo.mem || Bo.wait)) movable = false;
+            }
+        }
+        if (!movable) {
+            unfixed++;
+            why << "join " << tgt << " (line " << it->second + 1 << ") not movable; ";
+            continue;
+        }
+        int npast = 1;                                       // the restore itself
+        for (size_t b : other)
+            if (b > cand.front()) npast++;
+        moves[restore] = Move{restore, cand, std::min(npast, 16)};
+        fixed++;
+        insns += (int)cand.size();
+    }
+    if (!moves.empty()) {
+        std::map<size_t, bool> drop;
+        for (auto &kv : moves)
+            for (size_t a : kv.second.moved) drop[a] = true;
+        std::ostringstream o;
+        for (size_t li = 0; li < lines.size(); li++) {
+            if (drop.count(li)) continue;
+            o << lines[li] << '\n';
+            auto mv = moves.find(li);
+            if (mv != moves.end()) {
+                for (size_t a : mv->second.moved)
+                    o << lines[a] << "    ; qpb_hazard: moved past the EXEC restore (join_fixup)\n";
+                // keep every moved result at least as far from its readers as before
+                o << "\ts_nop " << (mv->second.pad - 1) << "    ; qpb_hazard: join_fixup distance\n";
+            }
+        }
+        s = o.str();
+    }
+    if (report)
+        *report = std::to_string(fixed) + " join(s) repaired (" + std::to_string(insns) + " instruction(s) moved past "
+                  "the EXEC restore)" + (unfixed ? ", " + std::to_string(unfixed) + " not movable: " + why.str() : "");
+    return unfixed ? -unfixed : fixed;
+}
+
 int audit_disassembly(const std::string &dis, std::string *report) {
     std::vector<Insn> ins;
     std::map<size_t, std::string> label_at;
     std::map<std::string, std::vector<size_t>> preds_of;
     std::map<uint64_t, size_t> at;
     std::vector<std::pair<size_t, uint64_t>> branches;
+    std::vector<std::string> texts;
     uint64_t fbase = 0;
     std::istringstream in(dis);
     std::string line;
@@ -319,6 +539,7 @@ int audit_disassembly(const std::string &dis, std::string *report) {
         }
         at[addr] = ins.size();
         ins.push_back(std::move(a));
+        texts.push_back(line.substr(1, cm - 1));
     }
     if (ins.empty()) {
         *report = "empty disassembly";
@@ -347,10 +568,37 @@ int audit_disassembly(const std::string &dis, std::string *report) {
         else other++;
         if (hazards + other <= 8) rep << D.mn << " needs " << n << " more wait state(s) after " << where << "; ";
     }
-    *report = (hazards || other) ? std::to_string(hazards) + " DPP hazard(s), " + std::to_string(other) +
-                                       " trans-forwarding / SGPR->VMEM hazard(s): " + rep.str()
-                                 : "clean (DPP, trans forwarding, VALU SGPR -> VMEM)";
-    return (hazards || other) ? 0 : 1;
+    // lane-partial code at a join (join_fixup's pattern): a lane-masked instruction
+    // between an s_cbranch_execz target and the EXEC restore that follows it
+    int joins = 0;
+    for (auto &[i, tgt] : branches) {
+        if (ins[i].mn != "s_cbranch_execz") continue;
+        auto it = at.find(tgt);
+        if (it == at.end()) continue;
+        int masked = 0;
+        for (size_t k = it->second; k < ins.size(); k++) {
+            if (k > it->second && label_at.count(k)) break;
+            const Ops o = parse_ops(texts[k]);
+            if (o.exec_def) {
+                if (masked && o.mn == "s_or_b64" && texts[k].find("exec, exec,") != std::string::npos) {
+                    joins++;
+                    if (hazards + other + joins <= 8)
+                        rep << masked << " lane-masked instruction(s) before the EXEC restore at join +" << k << "; ";
+                }
+                break;
+            }
+            if (o.branch) break;
+            if (o.valu_like && o.mn.rfind("v_writelane", 0) != 0 && o.mn.rfind("v_readlane", 0) != 0 &&
+                o.mn.rfind("v_readfirstlane", 0) != 0 && o.mn.rfind("v_cmp", 0) != 0)
+                masked++;
+        }
+    }
+    *report = (hazards || other || joins)
+                  ? std::to_string(hazards) + " DPP hazard(s), " + std::to_string(other) +
+                        " trans-forwarding / SGPR->VMEM hazard(s), " + std::to_string(joins) +
+                        " lane-partial join(s): " + rep.str()
+                  : "clean (DPP, trans forwarding, VALU SGPR -> VMEM, EXEC-restore joins)";
+    return (hazards || other || joins) ? 0 : 1;
 }
 
 }  // namespace qpb

@@ -299,8 +299,12 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
         {
             const int a0 = (row * LDS_QP) & 1;
             double2 *z2 = reinterpret_cast<double2 *>(Ls + a0);
+            // (STG_END is even: rows with a0 = 0 need STG_END / 2 pairs -- one more than the
+            // (STG_END - 1) / 2 round 5 sized the loop for, which missed the last pair when
+            // STG_END = 2 mod 32)
+            static_assert(STG_END % 2 == 0, "staged area ends on a pair");
 #pragma unroll
-            for (int i = 0; i < ((STG_END - 1) / 2 + 15) / 16; i++) {
+            for (int i = 0; i < (STG_END / 2 + 15) / 16; i++) {
                 const int k = c + 16 * i;
                 if (2 * k + 1 < STG_END - a0) z2[k] = double2{0.0, 0.0};
             }

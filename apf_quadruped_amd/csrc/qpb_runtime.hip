@@ -286,10 +286,12 @@ static std::vector<std::string> compile_options(bool exact) {
     return o;
 }
 
-// Kernels with DPP inline asm are compiled through assembly: clang -S, then
-// qpb_hazard's asm_fixup pads every DPP instruction of an asm region with the
-// wait states its operands' producers require (qpb_hazard.cpp), then the text is
-// assembled and linked into the code object.  Others compile straight to it.
+// Every kernel is compiled through assembly: clang -S, then qpb_hazard's join_fixup
+// moves lane-masked instructions the register allocator left ahead of an EXEC restore
+// to just after it (the wide row kernel's aperture violation), and
+// asm_fixup pads every DPP instruction of an inline-asm region with the wait states its
+// operands' producers require (qpb_hazard.cpp); then the text is assembled and linked
+// into the code object.
 static int compile_with_clang(const std::string &clang, const std::string &kname, const std::string &src,
                               bool exact, std::vector<char> &code, std::string *fixup_report = nullptr) {
     std::string dir = getenv("TMPDIR") && *getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp";
@@ -301,8 +303,8 @@ static int compile_with_clang(const std::string &clang, const std::string &kname
         if (!f) return fail(QPB_ECOMPILE, "cannot write " + sp);
         f << src;
     }
-    // QPB_NO_ASM_FIXUP=1: experiments only (A/B of the padding's cost); part of the cache key
-    const bool via_asm = src.find("_dpp ") != std::string::npos && !getenv("QPB_NO_ASM_FIXUP");
+    // QPB_NO_ASM_FIXUP=1: experiments only (no assembly pass at all); part of the cache key
+    const bool via_asm = !getenv("QPB_NO_ASM_FIXUP");
     const std::string bindir = clang.substr(0, clang.rfind('/'));
     std::vector<std::string> argv = {clang, "-x", "hip", "--cuda-device-only", "--no-gpu-bundle-output",
                                      "-I" + clang.substr(0, clang.rfind("/lib/llvm/bin/")) + "/include",
@@ -320,9 +322,14 @@ static int compile_with_clang(const std::string &clang, const std::string &kname
         if (!read_file(ap, txt)) st = -1;
         else {
             std::string as(txt.begin(), txt.end());
-            std::string rep;
+            std::string rep, jrep;
+            const int jr = join_fixup(as, &jrep);
             asm_fixup(as, &rep);
-            if (fixup_report) *fixup_report = rep;
+            if (fixup_report) *fixup_report = jrep + "; " + rep;
+            if (jr < 0) {
+                unlink(ap.c_str());
+                return fail(QPB_ECOMPILE, "kernel " + kname + ": " + jrep);
+            }
             write_file(ap, std::vector<char>(as.begin(), as.end()));
             st = run_child({bindir + "/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-c",
                             ap, "-o", obp}, &log);
@@ -401,7 +408,7 @@ int compile_kernel(const std::string &kname, const std::function<std::string()> 
     const Compiler &cc = compiler();
     std::string id = cc.ident;
     for (auto &o : compile_options(exact)) id += " " + o;
-    id += getenv("QPB_NO_ASM_FIXUP") ? " no-dpp-fixup" : " dpp-wait-states-v2";   // qpb_hazard.cpp's rules
+    id += getenv("QPB_NO_ASM_FIXUP") ? " no-dpp-fixup" : " dpp-wait-states-v2 join-fixup-v1";   // qpb_hazard.cpp's rules
     char tag[17];
     snprintf(tag, sizeof tag, "%016llx", (unsigned long long)fnv1a(id));
     const std::string dir = cache_dir();
@@ -417,21 +424,26 @@ int compile_kernel(const std::string &kname, const std::function<std::string()> 
     int rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
                               : compile_with_clang(cc.clang, kname, src, exact, *code, &fix);
     if (rc) return rc;
-    std::string audit = "no DPP asm";
-    if (src.find("v_fmac_f64_dpp") != std::string::npos) {
-        // DPP from inline asm: the clang path padded it (asm_fixup); verify the
-        // wait states in the code object either way; on a hazard (or no way to
-        // check) rebuild with wait states inside every DPP asm (QPB_DPP_NOP = 2),
-        // which is hazard-free by construction
-        const int ok = dpp_audit(*code, &audit);
-        if (!fix.empty()) audit = fix + "; audit: " + audit;
-        if (ok != 1) {
-            src = "#define QPB_DPP_NOP 2\n" + src;
-            rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
-                                  : compile_with_clang(cc.clang, kname, src, exact, *code, &fix);
-            if (rc) return rc;
-            audit += " -> rebuilt with QPB_DPP_NOP=2";
-        }
+    // every code object is audited (qpb_hazard.cpp): DPP wait states, trans forwarding,
+    // VALU SGPR -> VMEM, and lane-masked code ahead of an EXEC restore at a join
+    std::string audit;
+    const int ok = dpp_audit(*code, &audit);
+    if (!fix.empty()) audit = fix + "; audit: " + audit;
+    auto join_bad = [](const std::string &a) {
+        return a.find("lane-partial join") != std::string::npos && a.find(" 0 lane-partial join(s)") == std::string::npos;
+    };
+    if (ok != 1 && src.find("v_fmac_f64_dpp") != std::string::npos && !join_bad(audit)) {
+        // DPP from inline asm: on a hazard (or no way to check) rebuild with wait
+        // states inside every DPP asm (QPB_DPP_NOP = 2), hazard-free by construction
+        src = "#define QPB_DPP_NOP 2\n" + src;
+        rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
+                              : compile_with_clang(cc.clang, kname, src, exact, *code, &fix);
+        if (rc) return rc;
+        audit += " -> rebuilt with QPB_DPP_NOP=2";
+    } else if (ok != 1 && join_bad(audit)) {
+        // a lane-partial join the assembly pass could not repair (or no assembly pass:
+        // hiprtc): the code object would read stale registers in some lanes -- refuse it
+        return fail(QPB_ECOMPILE, "kernel " + kname + " failed the audit: " + audit);
     }
     mkdir(dir.c_str(), 0755);
     write_file(path, *code);
@@ -694,6 +706,20 @@ int qpb_audit_dpp(const void *code, long size, char *report, long cap) {
         std::memcpy(report, rep.data(), (size_t)k);
         report[k] = 0;
     }
+    return r;
+}
+
+long qpb_join_fixup(char *text, long cap, char *report, long rcap) {
+    if (!text || cap <= 0) return fail(QPB_EINVAL, "no text");
+    std::string s(text), rep;
+    const int r = qpb::join_fixup(s, &rep);
+    if (report && rcap > 0) {
+        const long k = std::min<long>(rcap - 1, (long)rep.size());
+        std::memcpy(report, rep.data(), (size_t)k);
+        report[k] = 0;
+    }
+    if ((long)s.size() + 1 > cap) return fail(QPB_EINVAL, "repaired text does not fit");
+    std::memcpy(text, s.c_str(), s.size() + 1);
     return r;
 }
 

@@ -727,17 +727,9 @@ bool rowx_eligible(const Plan &pl, std::string *why) {
     for (long d = 0; d < pl.n; d++)
         if (L.dense[d] != d) return no("the x block is not in natural order (leaves-first ordering needed)");
     if (4 * rowx_layout(pl).LDS_QP * 8 > 160L * 1024) return no("four QPs' dense copies exceed the LDS of a CU");
-    // Only configurations validated on the GPU: with more than 16 variables (two x
-    // slots) an upper-triangle P whose off-diagonal entries reach the first slot's rows
-    // (a dense 17-variable P) faulted once (DESIGN.md 4c') and stays on the wave form
-    // until the cause is found; the controller's P (off-diagonal block in rows 18-29),
-    // full-storage P and n <= 16 are validated
-    if (pl.pmode == P_UPPER && pl.n > 16) {
-        for (long j = 0; j < pl.n; j++)
-            for (long k = pl.Pin.jc[j]; k < pl.Pin.jc[j + 1]; k++)
-                if (pl.Pin.ir[k] != j && std::min<long>(pl.Pin.ir[k], j) < 16)
-                    return no("upper-triangle P with off-diagonal entries in rows < 16 and n > 16 (not validated)");
-    }
+    // (round 5 kept upper-triangle P with off-diagonals in rows < 16 off this kernel after
+    // a memory-aperture violation at 17 / 20 / 6; the cause was a register-allocator copy
+    // placed ahead of an EXEC restore, now repaired in every kernel -- DESIGN.md §3)
     if (why) why->clear();
     return true;
 }

@@ -311,6 +311,14 @@ const char *qpb_compiler(void);
  * instruction's VGPR operand within 2 wait states or a VALU EXEC write within 5
  * (report says where), -1 cannot audit (no llvm-objdump). */
 int qpb_audit_dpp(const void *code, long size, char *report, long cap);
+/* The assembly-level repair every generated kernel goes through (qpb_hazard.cpp
+ * join_fixup): in the gfx950 assembly text (NUL-terminated, rewritten in place, at
+ * most cap bytes including the NUL), move lane-masked instructions the register
+ * allocator placed between a divergent region's skip target (s_cbranch_execz) and its
+ * EXEC restore (s_or_b64 exec, exec, ..) to just after the restore.  Returns the number
+ * of repaired joins, -k when k could not be repaired, QPB_EINVAL when the result does
+ * not fit cap. */
+long qpb_join_fixup(char *text, long cap, char *report, long rcap);
 /* The drop-in's persistent solvers on the calling thread (include/qpSWIFT.h):
  * out[0] = device solves they answered, out[1] = kernel launches they took
  * (first use, relaunch after an idle exit or new arguments), out[2] / out[3] =

@@ -139,3 +139,72 @@ def test_audit_clean_on_every_cached_kernel():
         if r == 0:
             bad.append((os.path.basename(f), rep))
     assert not bad, bad[:3]
+
+
+JOIN_SNIPPET = r"""
+#include <hip/hip_runtime.h>
+extern "C" __global__ void k(double *p, const double *q) {
+    double a = p[threadIdx.x];
+    if (threadIdx.x < 6) a += q[threadIdx.x];          // divergent: s_and_saveexec / s_cbranch_execz
+    p[threadIdx.x] = a * 3.0;
+}
+"""
+
+
+def _assemble(tmp_path, text, tag):
+    bindir = os.path.dirname(CLANG)
+    s, o, co = tmp_path / f"{tag}.s", tmp_path / f"{tag}.o", tmp_path / f"{tag}.co"
+    s.write_text(text)
+    subprocess.run([os.path.join(bindir, "clang"), "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950",
+                    "-c", str(s), "-o", str(o)], check=True)
+    subprocess.run([os.path.join(bindir, "ld.lld"), "-shared", str(o), "-o", str(co)], check=True)
+    return co.read_bytes()
+
+
+@pytest.mark.skipif(not os.path.exists(CLANG), reason="ROCm clang not present")
+def test_audit_flags_and_join_fixup_repairs_lane_partial_join(tmp_path):
+    """The wide row kernel's aperture violation: the register allocator
+    left `v_accvgpr_write_b32 a18, v124` (a value every lane reads later) between a
+    divergent region's s_cbranch_execz target and its `s_or_b64 exec, exec, ..` restore,
+    so only the region's lanes got the copy.  The same shape is injected here into a
+    small kernel: the audit flags it, join_fixup moves the copy past the restore, and
+    the repaired object audits clean.  (Compiled and audited, never run.)"""
+    import re
+    src = tmp_path / "k.hip"
+    src.write_text(JOIN_SNIPPET)
+    asm = tmp_path / "k.s"
+    subprocess.run([CLANG, "-x", "hip", "--cuda-device-only", "--no-gpu-bundle-output", "--offload-arch=gfx950",
+                    "-O3", "-S", "-o", str(asm), str(src)], check=True)
+    text = asm.read_text()
+    r, rep = _audit(_assemble(tmp_path, text, "clean"))
+    assert r == 1, rep                                        # the compiler's own output: clean
+    m = re.search(r"s_cbranch_execz (\.LBB\w+)", text)
+    assert m, "no divergent region in the snippet"
+    lab = m.group(1)
+    bad = text.replace(f"\n{lab}:", f"\n{lab}:\n\tv_accvgpr_write_b32 a0, v0\n\ts_mov_b32 s40, s41", 1)
+    assert re.search(re.escape(lab) + r":[^\n]*\n\tv_accvgpr_write_b32 a0, v0\n\ts_mov_b32 s40, s41\n(\s*;[^\n]*\n)*"
+                     r"\s*s_or_b64 exec, exec", bad), "the join does not start with the EXEC restore"
+    r, rep = _audit(_assemble(tmp_path, bad, "bad"))
+    assert r == 0 and "1 lane-partial join(s)" in rep, rep
+    buf = C.create_string_buffer(bad.encode(), len(bad) + 4096)
+    jrep = C.create_string_buffer(1024)
+    n = _lib.lib().qpb_join_fixup(buf, len(bad) + 4096, jrep, 1024)
+    assert n == 1, jrep.value
+    fixed = buf.value.decode()
+    assert re.search(r"s_or_b64 exec, exec, [^\n]*\n\tv_accvgpr_write_b32 a0, v0", fixed), fixed[:3000]
+    r, rep = _audit(_assemble(tmp_path, fixed, "fixed"))
+    assert r == 1, rep
+
+
+def test_join_fixup_refuses_a_dependent_move():
+    """An instruction that reads an SGPR written after it (before the restore) cannot
+    move past that write: join_fixup reports the join as not repairable (negative)."""
+    text = ("k:\n\ts_and_saveexec_b64 s[0:1], vcc\n\ts_cbranch_execz .LBB0_2\n\tv_mov_b32 v1, 0\n.LBB0_2:\n"
+            "\tv_mov_b32 v2, s3\n\ts_mov_b32 s3, s4\n\ts_or_b64 exec, exec, s[0:1]\n\ts_endpgm\n")
+    buf = C.create_string_buffer(text.encode(), len(text) + 1024)
+    jrep = C.create_string_buffer(1024)
+    assert _lib.lib().qpb_join_fixup(buf, len(text) + 1024, jrep, 1024) == -1, jrep.value
+    ok = text.replace("\tv_mov_b32 v2, s3\n\ts_mov_b32 s3, s4\n", "\tv_mov_b32 v2, s5\n\ts_mov_b32 s3, s4\n")
+    buf = C.create_string_buffer(ok.encode(), len(ok) + 1024)
+    assert _lib.lib().qpb_join_fixup(buf, len(ok) + 1024, jrep, 1024) == 1, jrep.value
+    assert "s_or_b64 exec, exec, s[0:1]\n\tv_mov_b32 v2, s5" in buf.value.decode()

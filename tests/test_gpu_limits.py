@@ -3,8 +3,9 @@
 The dispatch rules (include/qpswift_hip.h, qpb_plan_info): the row form of the
 wave kernel holds n, p <= 16, m <= 32 (four QPs per wavefront); the wide row form
 n, p <= 32, m <= 128 in leaves-first order while four QPs' dense copies fit the LDS
-(four QPs per wavefront, two x rows per lane), except an upper-triangle P with
-off-diagonal entries past 16 variables (not validated); the one-QP-per-wavefront form holds
+(four QPs per wavefront, two x rows per lane; round 6 lifted round 5's exclusion of
+upper-triangle P past 16 variables once its fault was root-caused, DESIGN.md §3);
+the one-QP-per-wavefront form holds
 n, p <= 64, m <= 256 with every G row non-empty; beyond that a plan runs the lane or
 tree kernel.  Each case sits on or just past one of those edges and is checked
 against the oracle run with the plan's own KKT permutation (same factorisation, so
@@ -20,8 +21,9 @@ import pytest
 LIMIT_CASES = [
     (16, 32, 16, "row"),     # the row form at its limit
     (16, 33, 6, "rowx"),     # one inequality too many for a 16-lane row: the wide row form
-    (17, 20, 6, "wave"),     # one variable too many; dense upper-triangle P past 16 variables: wave form
-    (32, 48, 16, "wave"),    # ditto (the wide row form's variable limit: tests/test_gpu_rowx.py, P full)
+    (17, 20, 6, "rowx"),     # one variable too many: the wide row form (dense upper-triangle P; the
+                             # round-5 aperture-violation case)
+    (32, 48, 16, "rowx"),    # the wide row form's variable limit (dense upper-triangle P)
     (12, 128, 6, "rowx"),    # ... and at its inequality limit
     (12, 129, 6, "wave"),    # one inequality past it
     (32, 64, 16, "wave"),    # four QPs' dense copies past the LDS of a CU

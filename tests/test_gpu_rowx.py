@@ -85,6 +85,9 @@ def test_rowx_synthetic_shapes_vs_oracle(shape, oracle):
     plan = _plan(d)
     assert plan.kernel_name(B).startswith("qpb_rowx_"), (shape, plan.kernel_name(B))
     r = _run(plan, d, B)
+    r2 = _run(plan, d, B)
+    for k in ("x", "y", "z", "s", "iters", "fval"):
+        np.testing.assert_array_equal(r[k], r2[k])          # deterministic (30 / 24 / 30: DESIGN §4c')
     _vs_oracle(oracle, plan, d, r, range(0, B, 5))
 
 
@@ -138,16 +141,21 @@ def test_rowx_against_the_wave_form(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(24, 40, 8), (20, 40, 10), (30, 68, 18)])
-def test_rowx_upper_p_past_16_vs_oracle(shape, oracle):
-    """P stored as its upper triangle with off-diagonal entries only among variables
-    >= 16 (the controller's skyline class, which the wide row form accepts past 16
-    variables; rowx_eligible), a ragged batch of 65: against the oracle on the dense
-    QP in the plan's own order, same flags and iterations, 1e-9 relative."""
+@pytest.mark.parametrize("shape,offdiag_from,linear", [((24, 40, 8), 16, None), ((20, 40, 10), 16, None),
+                                                       ((30, 68, 18), 16, None), ((17, 20, 6), 0, None),
+                                                       ((24, 40, 8), 0, None), ((17, 40, 5), 0, 16)])
+def test_rowx_upper_p_past_16_vs_oracle(shape, offdiag_from, linear, oracle):
+    """P stored as its upper triangle past 16 variables, a ragged batch of 65: against
+    the oracle on the dense QP in the plan's own order, same flags and iterations,
+    1e-9 relative.  Off-diagonal entries only among variables >= 16 (the controller's
+    skyline class), or anywhere (round 5 kept those off the wide row form after its
+    aperture violation at 17 / 20 / 6; root-caused and lifted in round 6),
+    and 17 / 40 / 5 with a linear-cost variable 16 (P(16, 16) structurally absent; the
+    staging zero-fill's last pair, STG_END = 1122 = 2 mod 32)."""
     from apf_quadruped_amd.batch import Plan
     n, m, p = shape
     B = 65
-    d = dense_qp(n, m, p, B=B, seed=7 * n + m, p_offdiag_from=16)
+    d = dense_qp(n, m, p, B=B, seed=7 * n + m, p_offdiag_from=offdiag_from, linear_var=linear)
     plan = Plan.from_dense(n, m, p, d["P"][0], d["A"][0], d["G"][0], p_upper=True)
     assert plan.kernel_name(B).startswith("qpb_rowx_")
     r = _run(plan, d, B, reltol=1e-6, abstol=1e-6)
