@@ -550,7 +550,10 @@ Pick pick_kernel(const qpb_plan *plan, long B, bool warm) {
     const int pref = plan->kernel_pref;
     k.wave = plan->wave_ok && (pref == 2 || (pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
     k.band = !k.wave && !warm && plan->band_ok && (pref == 4 || (pref == 0 && plan->large_tree && band_auto()));
-    k.tree = !k.wave && !k.band && (pref == 3 || ((pref == 0 || pref == 4) && plan->large_tree));
+    // QPB_KERNEL_BAND: warm solves (and a plan the band kernel cannot take) go to the tree
+    // kernel whenever it can run the plan, as the header says (they fell to the
+    // lane kernel for N <= 64)
+    k.tree = !k.wave && !k.band && (pref == 3 || (pref == 4 && plan->tree_ok) || (pref == 0 && plan->large_tree));
     return k;
 }
 

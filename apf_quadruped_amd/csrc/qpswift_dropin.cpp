@@ -176,15 +176,26 @@ double kkt_slot_value(const qpb::Slot &sl, const double *P, const double *A, con
 // 30-variable QPs, DESIGN.md 4c') instead of the reference's AMD (qpSWIFT.c:424-440).
 // Same QP, same algorithm, another elimination order: x agrees to rounding, not bit
 // for bit, and an iteration count can differ where a stopping test is marginal.
-bool own_order() {
+// Exact mode (QPSWIFT_HIP_EXACT=1) promises the reference's bits, which need the
+// reference's AMD order: the own order is then ignored, with one warning.
+bool own_order(bool exact) {
     const char *e = std::getenv("QPSWIFT_HIP_ORDER");
-    return e && std::strcmp(e, "own") == 0;
+    const bool own = e && std::strcmp(e, "own") == 0;
+    if (own && exact) {
+        static std::once_flag warned;
+        std::call_once(warned, [] {
+            std::fprintf(stderr, "qpswift-hip: QPSWIFT_HIP_ORDER=own ignored under QPSWIFT_HIP_EXACT=1 "
+                                 "(exact mode keeps the reference's AMD order)\n");
+        });
+        return false;
+    }
+    return own;
 }
 
 PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const long *Ajc, const long *Air,
                  const long *Gjc, const long *Gir, const long *perm, bool exact, std::string &err) {
     std::string key;
-    const bool own = !perm && own_order();
+    const bool own = !perm && own_order(exact);
     const long hdr[6] = {n, m, p, exact ? 1L : 0L, perm ? 1L : 0L, own ? 1L : 0L};
     key_append(key, hdr, 6);
     key_append(key, Pjc, n + 1);
