@@ -478,7 +478,11 @@ def trace_leg(tol, dev, steps=20, warmup=3):
     flags = torch.cat([o["flag"][:B] for o, B in zip(outs, Bs)])
     iters = torch.cat([o["iters"][:B] for o, B in zip(outs, Bs)]).float()
     Bt = sum(Bs)
+    maxit_frac = float((flags == 2).float().mean().item())
     return {"workload": f"recorded Gazebo traces: {Bt} logged steps of 5 DogBot runs, {len(Bs)} stance sets, one group launch",
+            "label": f"maxit-dominated: {100 * maxit_frac:.0f} % of the QPs are infeasible two-foot phases that run to "
+                     "maxit (100 iterations, QP_MAXIT) as in qpSWIFT; the rate measures that grinding, not the solver",
+            "maxit_frac": maxit_frac,
             "batch": Bt, "value": Bt * steps / el, "unit": "QP solves/s", "ms_per_step": el * 1e3 / steps,
             "kernel": grp.kernel_name(), "traffic": traffic_for(grp.kernel_name()),
             "stance_sets": [int(b[0]) for b in batches],
