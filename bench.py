@@ -535,7 +535,7 @@ def _sq_record(kname, B):
     kind = next((k for k in ("rowx", "row", "tree", "wave", "band") if kname.startswith("qpb_" + k)), None)
     if kind is None:
         return None, None
-    for rnd in ("r05", "r04", "r03"):
+    for rnd in ("r06", "r05", "r04", "r03"):
         name = f"{rnd}_sq_{kind}.json"
         f = os.path.join(ROOT, "profiles", name)
         if not os.path.exists(f):
@@ -572,7 +572,7 @@ def measured_bound(kname, B):
 def limiter_for(B):
     """What the SQ counters say bounds the row kernel at this batch
     (the newest profiles/r0N_sq_row.json; scripts/gpu_sq.sh + scripts/sq_summary.py)."""
-    name = next((n for n in ("r05_sq_row.json", "r04_sq_row.json", "r03_sq_row.json")
+    name = next((n for n in ("r06_sq_row.json", "r05_sq_row.json", "r04_sq_row.json", "r03_sq_row.json")
                  if os.path.exists(os.path.join(ROOT, "profiles", n))), None)
     if name is None:
         return None
