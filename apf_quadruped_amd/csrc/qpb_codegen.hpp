@@ -55,7 +55,7 @@ struct KernelArgs {
     // {flag, iters} (two ints in one double), sigma -- instead of the output slots.  A
     // resident wave re-reading a host-memory line it wrote itself during an earlier
     // request was measured to get its own old bytes, not the host's later write
-    // (DESIGN §4i); NULL: read the output slots (launched kernels)
+    // (DESIGN_HISTORY §4i); NULL: read the output slots (launched kernels)
     const double *win = nullptr;
 };
 constexpr int QPB_TRACE_MAX = 256;

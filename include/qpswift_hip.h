@@ -335,7 +335,7 @@ int qpb_dropin_quiesce(void);
  * environment): idle_ms = QPSWIFT_HIP_SERVE_IDLE_MS (default 20), life_ms = the
  * multi-request lifetime -- 0 (one request per wave, the shipped mode) unless
  * QPSWIFT_HIP_SERVE_LIFE_MS > 0 AND QPB_SERVE_DIAG=1 (a diagnostics-only mode with an
- * open defect).  Needs no GPU. */
+ * open defect, DESIGN_HISTORY §7.5).  Needs no GPU. */
 int qpb_serve_config(double *idle_ms, double *life_ms);
 
 #ifdef __cplusplus

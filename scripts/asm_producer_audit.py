@@ -1,4 +1,4 @@
-"""Resident-solver diagnostics: DPP inline-asm results consumed by
+"""Resident-solver diagnostics (DESIGN_HISTORY §4i): DPP inline-asm results consumed by
 compiler-emitted instructions within the hazard window, by consumer kind and wait
 states (clang -S output of scripts/serve_variant_src.py)."""
 import re, sys

@@ -1,4 +1,4 @@
-"""Diagnose the leaves-first wave-kernel NaN under the pinned
+"""Diagnose the leaves-first wave-kernel NaN (DESIGN_HISTORY §7 item 4) under the pinned
 ROCm 7.2 clang: one child process per compile variant (a process keeps one code
 object per kernel name), each solving trot / stance / crawl controller QPs in
 leaves-first order on the wave kernel and comparing with the oracle run in the

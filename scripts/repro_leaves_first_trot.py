@@ -1,4 +1,4 @@
-"""Reproducer (parked): the wave kernel on the trot controller QP
+"""Reproducer (parked, DESIGN_HISTORY.md §7): the wave kernel on the trot controller QP
 (30/70/12) with a leaves-first KKT order (z rows, y rows, then x -- pass it as the
 plan's permutation) goes NaN at IPM iteration 1 when QPB_W_MFMA, QPB_W_LDSB and
 QPB_W_LTLDS are all on; turning any one off (QPB_WAVE_OPTS) gives the oracle's

@@ -1,4 +1,4 @@
-"""Resident-solver diagnostics: SGPR spill slots (v254/v255 lanes)
+"""Resident-solver diagnostics (DESIGN_HISTORY §4i): SGPR spill slots (v254/v255 lanes)
 written before the request loop and rewritten inside it (clang -S output of
 scripts/serve_variant_src.py)."""
 import re, sys

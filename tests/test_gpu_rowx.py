@@ -87,7 +87,7 @@ def test_rowx_synthetic_shapes_vs_oracle(shape, oracle):
     r = _run(plan, d, B)
     r2 = _run(plan, d, B)
     for k in ("x", "y", "z", "s", "iters", "fval"):
-        np.testing.assert_array_equal(r[k], r2[k])          # deterministic (30 / 24 / 30: DESIGN §4c')
+        np.testing.assert_array_equal(r[k], r2[k])          # deterministic (30 / 24 / 30: DESIGN_HISTORY §4c')
     _vs_oracle(oracle, plan, d, r, range(0, B, 5))
 
 

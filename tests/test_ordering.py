@@ -1,4 +1,4 @@
-"""Why the drop-in keeps the reference's AMD ordering for Permut = NULL.
+"""Why the drop-in keeps the reference's AMD ordering for Permut = NULL (DESIGN_HISTORY §4i).
 
 The leaves-first ordering runs the 30-variable controller QPs ~1.7x faster per
 iteration on the device, but the ordering decides which y pivots hit the

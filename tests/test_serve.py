@@ -242,7 +242,7 @@ def _serve_config(env):
 
 
 def test_multi_request_wave_refused_without_diag_guard():
-    """The multi-request persistent wave has an open defect: a lifetime
+    """The multi-request persistent wave has an open defect (DESIGN_HISTORY §7.5): a lifetime
     (QPSWIFT_HIP_SERVE_LIFE_MS > 0) alone is refused -- one request per wave, with a
     message -- and only QPB_SERVE_DIAG=1 turns the diagnostics mode on.  No GPU needed."""
     (idle, life), _ = _serve_config({})
