@@ -208,3 +208,17 @@ def test_join_fixup_refuses_a_dependent_move():
     buf = C.create_string_buffer(ok.encode(), len(ok) + 1024)
     assert _lib.lib().qpb_join_fixup(buf, len(ok) + 1024, jrep, 1024) == 1, jrep.value
     assert "s_or_b64 exec, exec, s[0:1]\n\tv_mov_b32 v2, s5" in buf.value.decode()
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc not present")
+@pytest.mark.parametrize("src", ["qpb_comm.hip", "qpb_assemble.hip", "qpb_runtime.hip"])
+def test_static_device_code_passes_the_audit(tmp_path, src):
+    """The kernels compiled into libqpswift_hip.so itself (argmin, winner payload, strided
+    copies, assembly, the RCCL gather's device reduce) pass the same code-object audit as
+    the generated ones -- in particular no lane-masked copy ahead of an EXEC restore."""
+    co = tmp_path / "k.co"
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "--cuda-device-only",
+                    "--no-gpu-bundle-output", "-o", str(co), os.path.join(ROOT, "apf_quadruped_amd", "csrc", src)],
+                   check=True, capture_output=True)
+    r, rep = _audit(co.read_bytes())
+    assert r == 1, rep
