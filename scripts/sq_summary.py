@@ -103,10 +103,10 @@ def main():
         }
     res["reading"] = ("controller-shape QPs (30 variables) on the wide row form: four QPs per wavefront, one per "
                       "16-lane row, the per-pass chain of one wave (LDS-bound to one wave per CU); see DESIGN "
-                      "§4c'") if rowx else ("MPC (N = 380) on the band kernel: one QP per wavefront, LDS-resident state (80 KB: two QPs "
-                      "per CU, two SIMDs of four busy); the stage recurrences (Schur complement, pivots, sweeps) are "
+                      "§4.4") if rowx else ("MPC (N = 380) on the band kernel: one QP per wavefront, LDS-resident state (40.8 KB: four QPs "
+                      "per CU, one per SIMD); the stage recurrences (Schur complement, pivots, sweeps) are "
                       "the chain; no descriptor tables (SALU = loop control only)") if band else ("controller-shape QPs (30 variables), one QP per wavefront: the dense LDL' and the "
-                      "triangular solves are one wave's dependency chain; see DESIGN_HISTORY §4b") if wave else ("MPC (N = 380): one QP alone runs 6 passes of ~118 gather / panel steps each (~1 us per "
+                      "triangular solves are one wave's dependency chain; see DESIGN §4.2") if wave else ("MPC (N = 380): one QP alone runs 6 passes of ~118 gather / panel steps each (~1 us per "
                       "step: descriptor wait, LDS terms, butterfly, epilogue, barrier); at 1 024 QPs (4 per CU) the "
                       "average wave lives ~0.98 ms of the 1.65 ms launch -- the launch is as long as the slowest QP "
                       "(10-11 iterations vs a mean of 5.7), which runs alone at the end: latency, not throughput"
