@@ -31,7 +31,8 @@
 // iterate, residuals and directions -- stays in the workgroup's LDS for the whole
 // solve, packed by pattern; inputs are read once, outputs written once.
 //
-// The loop is the row kernel's (qpSWIFT.c:473-644): kkt_initialize as iteration -1,
+// The loop is the row kernel's (qpSWIFT.c:473-644): kkt_initialize as iteration -1 (the
+// warm variant, QPB_WARM = 1, continues from the QP object's state instead),
 // residuals + exit test, factor, predictor, corrector, step lengths (Auxilary.c:359-393),
 // update; fast mode (FMA contraction, reciprocal pivots).
 #pragma clang fp contract(fast)
@@ -205,6 +206,16 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
 #if MY > 0
         for (int i = lane; i < BNY; i += 64) Ls[V_RY + i] = QPB_LDS(&gb[i * QPB_TSTR]);
 #endif
+#if QPB_WARM
+        // warm variant (qpb_solve_warm): QP_SOLVE continues from the object's iterate
+        // (qpSWIFT.c:502-596 never re-initialises); rz / ry are formed by the first pass
+        for (int i = lane; i < BNZ; i += 64) {
+            Ls[V_Z + i] = QPB_LDS(&a.z[tile * (BNZ * QPB_TSTR) + i * QPB_TSTR + ql]);
+            Ls[V_S + i] = QPB_LDS(&a.s[tile * (BNZ * QPB_TSTR) + i * QPB_TSTR + ql]);
+        }
+        for (int i = lane; i < BNX; i += 64) Ls[V_X + i] = QPB_LDS(&a.x[tile * (BNX * QPB_TSTR) + i * QPB_TSTR + ql]);
+        for (int i = lane; i < BNY; i += 64) Ls[V_Y + i] = QPB_LDS(&a.y[tile * (BNY * QPB_TSTR) + i * QPB_TSTR + ql]);
+#else
         for (int i = lane; i < BNZ; i += 64) {
             Ls[V_RZ + i] = QPB_LDS(&gh[i * QPB_TSTR]);
             Ls[V_Z + i] = 1.0;
@@ -212,6 +223,7 @@ static __device__ __forceinline__ void qpb_band_body(const qpb_args &a, long q, 
         }
         for (int i = lane; i < BNX; i += 64) Ls[V_X + i] = 0.0;
         for (int i = lane; i < BNY; i += 64) Ls[V_Y + i] = 0.0;
+#endif
     }
     qpb_wsync();
     QPB_BT(5);
@@ -746,10 +758,33 @@ QPB_PRAGMA(unroll QPB_B_UNR)
     const double tol2 = a.tol > 0.0 ? a.tol * a.tol : -1.0;
     double sigma = 100.0;      // options->sigma (GlobalOptions.h:49)
     long it = -1, itq = 0;
-    int flag = 3;
+#if QPB_WARM
+    // the warm variant: IterationCount, stats->Flag and options->sigma the QP enters with
+    // (the row kernels' semantics: QP_MAXIT only when IterationCount reaches maxit,
+    // qpSWIFT.c:598-601), and the drop-in's timers / per-iteration trace (KernelArgs::trace)
+    const long it_in = QPB_LDS(&a.iters[q]);
+    const int flag_in = QPB_LDS(&a.flag[q]);
+    sigma = QPB_LDS(&a.sig[q]);
+    it = 0;
+    double sigf = sigma;
+    double *const trc = (a.trace && lane == 0) ? a.trace + q * QPB_TRACE_STRIDE : nullptr;
+    long t_fac = 0, t_kkt = 0, n_top = 0, n_it = 0;
+#define QPB_BSIGF sigf = sigma
+#define QPB_BCLK() ((long)__builtin_amdgcn_s_memrealtime())
+#else
+    constexpr long it_in = 0;
+    constexpr int flag_in = 3;
+#define QPB_BSIGF (void)0
+#endif
+    int flag = flag_in;
     double fv = 0.0, st_rx2 = 0.0, st_ry2 = 0.0, st_rz2 = 0.0, st_mu = 0.0, ap = 0.0, ad = 0.0;
     for (;;) {
-        if (it >= 0 && it >= a.maxit) { itq = it; flag = 2; break; }
+        if ((QPB_WARM || it >= 0) && it >= a.maxit) {
+            itq = it_in + it;
+            flag = (!QPB_WARM || itq == a.maxit) ? 2 : flag_in;
+            QPB_BSIGF;
+            break;
+        }
         wset = it < 0;
         double red[4] = {0.0, 0.0, 0.0, 1.0};
         double mu = 0.0;
@@ -758,9 +793,18 @@ QPB_PRAGMA(unroll QPB_B_UNR)
             fv = residuals(red);
             const double mu_it = red[3] * (1.0 / BNZ);
             st_rx2 = red[0]; st_ry2 = BNY > 0 ? red[1] : 0.0; st_rz2 = red[2]; st_mu = mu_it;
+#if QPB_WARM
+            if (trc && it < QPB_TRACE_MAX) {
+                double *e = trc + 4 + 7 * it;
+                e[0] = fv; e[1] = __builtin_sqrt(red[0]); e[2] = BNY > 0 ? __builtin_sqrt(red[1]) : 0.0;
+                e[3] = __builtin_sqrt(red[2]); e[4] = mu_it;
+                n_top = it + 1;
+            }
+#endif
             if (red[0] < tol2 && red[2] < tol2 && (BNY == 0 || red[1] < tol2) && mu_it < a.abstol) {
-                itq = it;
-                flag = 0;
+                itq = it_in + it;
+                flag = (QPB_WARM && itq == a.maxit) ? 2 : 0;
+                QPB_BSIGF;
                 break;
             }
             mu = mu_it;
@@ -768,12 +812,18 @@ QPB_PRAGMA(unroll QPB_B_UNR)
         }
         const double rsz = qpb_rcp(red[3]);
         QPB_BT(0);
+#if QPB_WARM
+        const long tf0 = QPB_BCLK();
+#endif
         factor(qpb_ic<0>{});
         {
             bool tiny = false;      // any |D| <= 1e-14: |1/D| >= 1e14 (or not finite)
             for (int i = lane; i < BNX; i += 64) tiny |= !(__builtin_fabs(Ls[O_RD + i]) < 1e14);
             if (qpb_any(tiny)) factor(qpb_ic<1>{});
         }
+#if QPB_WARM
+        { const long d_ = QPB_BCLK() - tf0; t_fac += d_; t_kkt += d_; }
+#endif
         QPB_BT(1);
         if (it < 0) {
             // setup solve, rhs [-c; b; h]: x0, y0; s0, z0 from -dz (Auxilary.c:1010-1040)
@@ -801,7 +851,13 @@ QPB_PRAGMA(unroll QPB_B_UNR)
         bool pcd = false;
         if (pc) {
             // predictor (kktsolve_1, Auxilary.c:471-515), ds = -s o z
+#if QPB_WARM
+            const long ts0 = QPB_BCLK();
             solve(BM_PRED, 0.0, false);
+            t_kkt += QPB_BCLK() - ts0;
+#else
+            solve(BM_PRED, 0.0, false);
+#endif
             step_length(false, ap, ad);
             double rr = 0.0;
             for (int i = lane; i < BNZ; i += 64) {
@@ -817,11 +873,24 @@ QPB_PRAGMA(unroll QPB_B_UNR)
         }
         QPB_BT(2);
         // corrector / centering (kktsolve_2, Auxilary.c:524-564)
+#if QPB_WARM
+        const long tc0 = QPB_BCLK();
         solve(BM_CORR, sigma * mu, pcd);
+        t_kkt += QPB_BCLK() - tc0;
+#else
+        solve(BM_CORR, sigma * mu, pcd);
+#endif
         QPB_BT(3);
         step_length(true, ap, ad);
         ap = 0.99 * ap > 1.0 ? 1.0 : 0.99 * ap;
         ad = 0.99 * ad > 1.0 ? 1.0 : 0.99 * ad;
+#if QPB_WARM
+        if (trc && it < QPB_TRACE_MAX) {
+            trc[4 + 7 * it + 5] = ap;
+            trc[4 + 7 * it + 6] = ad;
+            n_it = it + 1;
+        }
+#endif
         for (int i = lane; i < BNX; i += 64) Ls[V_X + i] = __builtin_fma(Ls[V_DX + i], ap, Ls[V_X + i]);
         for (int i = lane; i < BNY; i += 64) Ls[V_Y + i] = __builtin_fma(Ls[V_RY + i], ad, Ls[V_Y + i]);
         for (int i = lane; i < BNZ; i += 64) {
@@ -844,7 +913,12 @@ QPB_PRAGMA(unroll QPB_B_UNR)
         QPB_STS(&a.flag[q], flag);
         QPB_STS(&a.iters[q], (int)itq);
         QPB_STS(&a.fval[q], fv);
+#if QPB_WARM
+        QPB_STS(&a.sig[q], sigf);
+        if (trc) { trc[0] = (double)t_fac; trc[1] = (double)t_kkt; trc[2] = (double)n_top; trc[3] = (double)n_it; }
+#else
         if (a.sig) QPB_STS(&a.sig[q], sigma);
+#endif
 #if QPB_B_TIMING
         if (a.stats) {
             double *o = a.stats + tile * 6 * QPB_TSTR + ql;
@@ -864,3 +938,5 @@ extern "C" __global__ void __launch_bounds__(64, 1) QPB_KERNEL_NAME(qpb_args a) 
     __shared__ __attribute__((aligned(16))) double qpb_lds[LDS_QP];
     qpb_band_body(a, qpb_xcd_block(), qpb_lds);
 }
+#undef QPB_BSIGF
+#undef QPB_BCLK

@@ -549,10 +549,10 @@ Pick pick_kernel(const qpb_plan *plan, long B, bool warm) {
     Pick k;
     const int pref = plan->kernel_pref;
     k.wave = plan->wave_ok && (pref == 2 || (pref == 0 && (plan->wave_max_batch < 0 || B <= plan->wave_max_batch)));
-    k.band = !k.wave && !warm && plan->band_ok && (pref == 4 || (pref == 0 && plan->large_tree && band_auto()));
-    // QPB_KERNEL_BAND: warm solves (and a plan the band kernel cannot take) go to the tree
-    // kernel whenever it can run the plan, as the header says (they fell to the
-    // lane kernel for N <= 64)
+    // cold and warm solves alike (the band kernel's QPB_WARM variant, round 6)
+    k.band = !k.wave && plan->band_ok && (pref == 4 || (pref == 0 && plan->large_tree && band_auto()));
+    // QPB_KERNEL_BAND on a plan the band kernel cannot take: the tree kernel whenever it can
+    // run the plan (such solves fell to the lane kernel for N <= 64)
     k.tree = !k.wave && !k.band && (pref == 3 || (pref == 4 && plan->tree_ok) || (pref == 0 && plan->large_tree));
     return k;
 }
@@ -935,19 +935,20 @@ int qpb_plan_compile_warm(qpb_plan *plan, long B) {
     if (!plan) return fail(QPB_EINVAL, "NULL plan");
     if (B < 1) B = 1;
     const qpb::Pick pk = qpb::pick_kernel(plan, B, true);
-    const bool wave = pk.wave, tree = pk.tree;
+    const bool wave = pk.wave, tree = pk.tree, band = pk.band;
     const bool row2 = wave && plan->row_occ_batch >= 0 && B > plan->row_occ_batch;
     const bool tree2 = tree && plan->tree_occ_batch >= 0 && B > plan->tree_occ_batch;
-    const std::string &kn = row2 ? plan->row2_kname : wave ? plan->wave_kname : tree2 ? plan->tree2_kname
-                          : tree ? plan->tree_kname : plan->kname;
+    const std::string &kn = band ? plan->band_kname : row2 ? plan->row2_kname : wave ? plan->wave_kname
+                          : tree2 ? plan->tree2_kname : tree ? plan->tree_kname : plan->kname;
     std::function<std::string()> gen =
-        row2 ? std::function<std::string()>([plan] { return qpb::generate_row_kernel(plan->pl, nullptr, 2); })
+        band ? std::function<std::string()>([plan] { return qpb::generate_band_kernel(plan->pl, nullptr); })
+        : row2 ? std::function<std::string()>([plan] { return qpb::generate_row_kernel(plan->pl, nullptr, 2); })
         : wave ? std::function<std::string()>([plan] { return qpb::wave_source_of(plan); })
         : tree2 ? std::function<std::string()>([plan] { return qpb::generate_tree_kernel(plan->pl, plan->tree2_wg, nullptr); })
         : tree ? std::function<std::string()>([plan] { return qpb::generate_tree_kernel(plan->pl, plan->tree_wg, nullptr); })
                : std::function<std::string()>([plan] { return qpb::generate_kernel(plan->pl, plan->gen); });
     std::shared_ptr<std::vector<char>> *slot = nullptr;
-    return qpb::compile_warm(plan, kn, gen, !wave && !tree && plan->gen.exact, &slot);
+    return qpb::compile_warm(plan, kn, gen, !wave && !tree && !band && plan->gen.exact, &slot);
 }
 
 int qpb_plan_compile_serve(qpb_plan *plan) {
@@ -1014,16 +1015,17 @@ int qpb::solve_ex(qpb_plan *plan, long B, const double *P, const double *A, cons
     } else {
         if (wave && !plan->wave_ok) return fail(QPB_EINVAL, "plan is not eligible for the wave kernel");
         if (tree && !plan->tree_ok) return fail(QPB_EINVAL, "plan is not eligible for the tree kernel");
-        const std::string &kn = row2 ? plan->row2_kname : wave ? plan->wave_kname : tree2 ? plan->tree2_kname
-                              : tree ? plan->tree_kname : plan->kname;
+        const std::string &kn = band ? plan->band_kname : row2 ? plan->row2_kname : wave ? plan->wave_kname
+                              : tree2 ? plan->tree2_kname : tree ? plan->tree_kname : plan->kname;
         std::function<std::string()> gen =
-            row2 ? std::function<std::string()>([plan] { return qpb::generate_row_kernel(plan->pl, nullptr, 2); })
+            band ? std::function<std::string()>([plan] { return qpb::generate_band_kernel(plan->pl, nullptr); })
+            : row2 ? std::function<std::string()>([plan] { return qpb::generate_row_kernel(plan->pl, nullptr, 2); })
             : wave ? std::function<std::string()>([plan] { return qpb::wave_source_of(plan); })
             : tree2 ? std::function<std::string()>([plan] { return qpb::generate_tree_kernel(plan->pl, plan->tree2_wg, nullptr); })
             : tree ? std::function<std::string()>([plan] { return qpb::generate_tree_kernel(plan->pl, plan->tree_wg, nullptr); })
                    : std::function<std::string()>([plan] { return qpb::generate_kernel(plan->pl, plan->gen); });
         std::shared_ptr<std::vector<char>> *slot = nullptr;
-        rc = qpb::compile_warm(plan, kn, gen, !wave && !tree && plan->gen.exact, &slot);
+        rc = qpb::compile_warm(plan, kn, gen, !wave && !tree && !band && plan->gen.exact, &slot);
         if (!rc) rc = qpb::load_function(kn + "_w", *slot, &fn);
     }
     if (rc) return rc;

@@ -68,9 +68,10 @@ typedef struct qpb_plan qpb_plan;
                                   where the row form (four QPs per wavefront) fits */
 #define QPB_KERNEL_TREE 0x800  /* always the tree kernel (one QP per workgroup,
                                   level-scheduled sparse LDL'; any pattern)        */
-#define QPB_KERNEL_BAND 0x1000 /* the band kernel for cold solves (one QP per wavefront,
-                                  block-tridiagonal LDL' over the stages of a multi-stage
-                                  pattern, e.g. an MPC horizon; warm solves: tree) */
+#define QPB_KERNEL_BAND 0x1000 /* the band kernel for cold and warm solves (one QP per
+                                  wavefront, block-tridiagonal LDL' over the stages of a
+                                  multi-stage pattern, e.g. an MPC horizon; a plan without
+                                  that structure: tree) */
 
 /* error codes */
 #define QPB_OK        0

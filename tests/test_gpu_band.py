@@ -219,3 +219,55 @@ def test_band_kernel_mpc_horizons_vs_oracle(horizon, oracle):
         assert r["flag"][q] == o["flag"] == 0 and r["iters"][q] == o["iters"], (horizon, q, r["iters"][q], o["iters"])
         for k in ("x", "y", "z", "s"):
             _close(r[k][q], o[k], f"h{horizon}[{q}].{k}", 1e-9)
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cut", [0, 2, 4])
+def test_band_kernel_warm_solve_continues_the_cold_one(cut, oracle):
+    """Warm solves of multi-stage plans run on the band kernel's QPB_WARM variant (round 6;
+    the tree kernel before).  The drop-in's sequence on one QP object: QP_SETUP
+    (kkt_initialize: a cold launch with maxit 0), a first QP_SOLVE stopped after `cut`
+    passes, a second QP_SOLVE continuing from the object's x, y, z, s, IterationCount,
+    Flag and sigma (qpSWIFT.c:502-601) -- the same passes as one uninterrupted cold solve:
+    identical flags and iteration counts, iterates within 1e-12 (the two variants are
+    separate compilations of the same source); the tree kernel's warm variant continuing
+    from the same state agrees to 1e-9."""
+    import torch
+    from apf_quadruped_amd import plans, workloads as W
+    from apf_quadruped_amd.batch import Plan
+    B = 65
+    d = W.mpc_qp(plans.SEED + 4, np.arange(B))
+    plan = plans.standard_plan("mpc_h10")
+    assert plan.kernel_for(B) == "band"
+    vals = {k: torch.from_numpy(v).cuda() for k, v in plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"]).items()}
+    full = plan.unpack(plan.solve(**vals, B=B), B)
+    out = plan.solve(**vals, B=B, maxit=0)                     # QP_SETUP's initial point
+    sig = torch.full((B,), 100.0, dtype=torch.float64, device="cuda")
+    if cut:
+        plan.solve_warm(**vals, B=B, maxit=cut, out=out, sigma=sig)
+        torch.cuda.synchronize()
+        first = plan.unpack(out, B)
+        assert (first["iters"] == cut).all() and (first["flag"] == 2).all()
+    tree = Plan(120, 200, 60, *plan.patterns.P, *plan.patterns.A, *plan.patterns.G, perm=plan.perm,
+                p_upper=plan.p_upper, kernel="tree")
+    tout = {k: v.clone() for k, v in out.items()}
+    tsig = sig.clone()
+    plan.solve_warm(**vals, B=B, maxit=100, out=out, sigma=sig)
+    tree.solve_warm(**vals, B=B, maxit=100, out=tout, sigma=tsig)
+    torch.cuda.synchronize()
+    w, t = plan.unpack(out, B), tree.unpack(tout, B)
+    np.testing.assert_array_equal(w["flag"], full["flag"])
+    np.testing.assert_array_equal(w["iters"], full["iters"])
+    np.testing.assert_array_equal(t["iters"], w["iters"])
+    for k in ("x", "y", "z", "s"):
+        _close(w[k], full[k], f"warm vs cold .{k}", 1e-12)
+        for q in range(0, B, 8):
+            _close(t[k][q], w[k][q], f"tree vs band warm [{q}].{k}", 1e-9)
+    # and against the oracle in the plan's order (the cold path's bar)
+    Pc, Ac, Gc = W.to_colmajor(d["P"]), W.to_colmajor(d["A"]), W.to_colmajor(d["G"])
+    for q in (0, B - 1):
+        o = oracle.solve_dense(120, 200, 60, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], d["b"][q], perm=plan.perm)
+        assert o["iters"] == w["iters"][q] and o["flag"] == w["flag"][q]
+        for k in ("x", "y", "z", "s"):
+            _close(w[k][q], o[k], f"mpc warm[{q}].{k}", 1e-9)
