@@ -271,6 +271,35 @@ def test_dropin_own_order_null_permut(name, monkeypatch):
             assert np.abs(r[k] - g[k][q]).max() <= bar * scale, (name, q, k)
 
 
+@pytest.mark.gpu
+def test_dropin_mpc_own_order_on_the_band_kernel(monkeypatch):
+    """The MPC-horizon golden (120 / 200 / 60, 10 stages) through the drop-in in its own
+    (leaves-first) order: QP_SETUP's initial point on the band kernel (a cold maxit-0
+    launch) and QP_SOLVE on the band kernel's warm variant (round 6; the tree kernel
+    before), with its timers from the warm kernel's trace.  Flag and iteration count
+    equal the reference's, x within 1e-6, z and s within 1e-5 (another elimination
+    order than the golden's AMD); a second QP_SOLVE at a tighter tolerance continues from
+    the object's state and does not go backwards."""
+    monkeypatch.setenv("QPSWIFT_HIP_ORDER", "own")
+    g = golden("mpc_h10")
+    tol, maxit = float(g["tol"]), int(g["maxit"])
+    for q in (0, g["x"].shape[0] - 1):
+        qp, keep = dropin.setup_dense(*_golden_dense_args(g, q), ordering=int(g["ordering"]))
+        r = dropin.solve_again(qp, int(g["n"]), int(g["m"]), reltol=tol, abstol=tol, maxit=maxit)
+        assert r["rc"] == 0 and r["flag"] == int(g["flag"][q]), r["error"]
+        assert r["iters"] == int(g["iters"][q]), (q, r["iters"], int(g["iters"][q]))
+        for k, bar in (("x", 1e-6), ("z", 1e-5), ("s", 1e-5)):
+            scale = max(1.0, float(np.abs(g[k][q]).max()))
+            assert np.abs(r[k] - g[k][q]).max() <= bar * scale, (q, k)
+        st = qp.contents.stats.contents
+        assert st.kkt_time > 0 and st.ldl_numeric > 0 and st.kkt_time >= st.ldl_numeric
+        r2 = dropin.solve_again(qp, int(g["n"]), int(g["m"]), reltol=tol * 1e-2, abstol=tol * 1e-2, maxit=maxit)
+        assert r2["flag"] == 0 and r2["iters"] >= r["iters"]
+        assert r2["n_rx"] <= max(r["n_rx"], tol * 1e-2) * 10
+        _lib.lib().QP_CLEANUP_dense(qp)
+        del keep
+
+
 DENSE = ["c1_tol1e-6", "c1_tol1e-2", "c1_rowmajor", "c1_noeq", "edge_zero_g_row", "mixed_stance4",
          "mixed_trot_blfr", "mixed_crawl_blflfr", "c1_maxit0", "c1_maxit2", "c1_maxit5", "edge_infeasible",
          "edge_infeasible_maxit8"]
