@@ -220,13 +220,17 @@ PlanPtr get_plan(long n, long m, long p, const long *Pjc, const long *Pir, const
         return nullptr;
     }
     PlanPtr plan(raw, PlanDeleter());
-    // compile only the kernel a batch of one runs (the wave kernel when the plan
-    // is eligible, else the lane kernel): large lane kernels take minutes.  With
-    // no GPU QP_SOLVE fails anyway (QP_FATAL), so setup does not JIT at all.
+    // compile only the kernel a batch of one runs (qpb::pick_kernel: the wave / row form
+    // when the plan is eligible, the band or tree kernel for the plans that take them,
+    // else the lane kernel -- round 5 compiled the lane kernel for band / tree plans too,
+    // which takes minutes at N = 380).  With no GPU QP_SOLVE fails anyway (QP_FATAL), so
+    // setup does not JIT at all.
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) rc = 0;
     else {
-        rc = raw->wave_ok && raw->kernel_pref != 1 ? qpb::compile_wave(raw) : qpb::compile_plan(raw);
+        const qpb::Pick pk = qpb::pick_kernel(raw, 1, false);
+        rc = pk.wave ? qpb::compile_wave(raw) : pk.band ? qpb::compile_band(raw) : pk.tree ? qpb::compile_tree(raw)
+                                                                                        : qpb::compile_plan(raw);
         // QP_SOLVE continues from the QP's state: the warm-solve variant
         if (!rc) rc = qpb_plan_compile_warm(raw, 1);
         // ... and the persistent forms the device solves go to (none: tree / lane)
