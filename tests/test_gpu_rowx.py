@@ -167,3 +167,36 @@ def test_rowx_upper_p_past_16_vs_oracle(shape, offdiag_from, linear, oracle):
         assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (shape, q)
         for k in ("x", "z", "s"):
             _close(r[k][q], o[k], f"[{q}].{k}")
+
+
+# random shapes past 16 variables with P stored as its upper triangle (seed 606, the
+# draws the wide row form accepts: four QPs' dense copies in one CU's LDS)
+RANDOM_UPPER = [(28, 15, 1, 0.5), (25, 23, 10, 0.2), (17, 51, 10, 1.0), (29, 32, 6, 1.0), (24, 75, 20, 0.2),
+                (25, 55, 10, 0.5)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m,p,dens", RANDOM_UPPER)
+def test_rowx_random_upper_p_vs_oracle(n, m, p, dens, oracle):
+    """A sweep of random upper-triangle-P plans on the wide row kernel after the round-6
+    repair of its aperture violation: ragged batch of 65, deterministic,
+    against the oracle in the plan's order (1e-9, identical flags and iterations)."""
+    from apf_quadruped_amd.batch import Plan
+    B = 65
+    d = dense_qp(n, m, p, B=B, seed=n * 10000 + m * 100 + p, p_density=dens)
+    plan = Plan.from_dense(n, m, p, d["P"][0], d["A"][0] if p else None, d["G"][0], p_upper=True)
+    assert plan.kernel_name(B).startswith("qpb_rowx_")
+    r = _run(plan, d, B, reltol=1e-6, abstol=1e-6)
+    r2 = _run(plan, d, B, reltol=1e-6, abstol=1e-6)
+    for k in ("x", "z", "s", "iters", "fval"):
+        np.testing.assert_array_equal(r[k], r2[k])
+    cm = lambda M: np.ascontiguousarray(M.transpose(0, 2, 1)).reshape(M.shape[0], -1)
+    Pc, Gc = cm(d["P"]), cm(d["G"])
+    Ac = cm(d["A"]) if p else np.zeros((B, 0))
+    bb = d["b"] if p else np.zeros((B, 0))
+    for q in range(0, B, 8):
+        o = oracle.solve_dense(n, m, p, Pc[q], Ac[q], Gc[q], d["c"][q], d["h"][q], bb[q], perm=plan.perm,
+                               reltol=1e-6, abstol=1e-6)
+        assert r["flag"][q] == o["flag"] and r["iters"][q] == o["iters"], (q, r["iters"][q], o["iters"])
+        for k in ("x", "z", "s"):
+            _close(r[k][q], o[k], f"[{q}].{k}")
