@@ -154,6 +154,9 @@ struct qpb_args {
 #endif
 #define QPB_TRACE_MAX 256                       // = qpb::QPB_TRACE_MAX (qpb_codegen.hpp)
 #define QPB_TRACE_STRIDE (4 + 7 * QPB_TRACE_MAX)
+#ifndef QPB_R_SELSLICE
+#define QPB_R_SELSLICE 1  // 1: the static slices loaded unconditionally + select (0: the round-5 branchy form)
+#endif
 #ifndef QPB_R_TIMING
 #define QPB_R_TIMING 0    // 2: per-QP start / end (realtime, cycles), iterations, hardware ids into stats;
                           // 3: cycles per phase (H0 + setup solve, residuals, factor, predictor,
@@ -519,7 +522,11 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     //   x_c: -P(c,:), -G(:,c), -A(:,c);  z_c / z_{16+c}: -G(c,:), -G(16+c,:);  y_c: -A(c,:)
     // (-P rows and H0 rows are used once per iteration: parked in LDS, one
     // contiguous run per lane, read where they are needed)
+    // Every load unconditional (the indices are clamped in range), then a select: a
+    // load under `cond ? -X[i] : 0` became a branch with its own s_waitcnt -- some
+    // 40 LDS round trips in series before the setup pass (QPB_R_SELSLICE=0: that form).
     double nGc[NZ], nAc[NY1], nGl[NX], nGh[ZH ? NX : 1], nAr[NX];
+#if !QPB_R_SELSLICE
 #pragma unroll
     for (int j = 0; j < NX; j++) {
         nGl[j] = isz0 ? -Gd[j * NZ + iz0] : 0.0;
@@ -530,6 +537,39 @@ static __device__ __forceinline__ void qpb_row_body(const qpb_args &a, long lb, 
     for (int r = 0; r < NZ; r++) nGc[r] = isx ? -Gd[ix * NZ + r] : 0.0;
 #pragma unroll
     for (int l = 0; l < NY1; l++) nAc[l] = (isx && NY > 0) ? -Ad[ix * NY + l] : 0.0;
+#else
+#pragma unroll
+    for (int j = 0; j < NX; j++) {
+        const double gl = Gd[j * NZ + iz0], ar = Ad[j * NY + iy];
+        nGl[j] = isz0 ? -gl : 0.0;
+        if constexpr (ZH) {
+            const double gh = Gd[j * NZ + iz1];
+            nGh[j] = isz1 ? -gh : 0.0;
+        }
+        nAr[j] = isy ? -ar : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < NZ; r++) {
+        const double g = Gd[ix * NZ + r];
+        nGc[r] = isx ? -g : 0.0;
+    }
+#pragma unroll
+    for (int l = 0; l < NY1; l++) {
+        const double av = Ad[ix * NY + (NY > 0 ? l : 0)];
+        nAc[l] = (isx && NY > 0) ? -av : 0.0;
+    }
+    // pinned: otherwise the compiler keeps the loaded value and redoes the negation
+    // and select (v_xor + v_mov) in front of every use inside the iteration loop
+#pragma unroll
+    for (int j = 0; j < NX; j++) {
+        asm volatile("" : "+v"(nGl[j]), "+v"(nAr[j]));
+        if constexpr (ZH) asm volatile("" : "+v"(nGh[j]));
+    }
+#pragma unroll
+    for (int r = 0; r < NZ; r++) asm volatile("" : "+v"(nGc[r]));
+#pragma unroll
+    for (int l = 0; l < NY1; l++) asm volatile("" : "+v"(nAc[l]));
+#endif
 #if QPB_R_GATHER || QPB_R_PIVLDS || QPB_R_RDLDS
     // gathered products: per-lane slot pointers into the vector area and the negated
     // coefficients of this lane's terms (padding: the zero slot, coefficient 0)
