@@ -46,6 +46,10 @@ static_assert(NX >= 1 && NX <= 32 && NY <= 32 && NZ >= 1 && NZ <= 128, "rowx ker
                           // 2: cycles per part instead (G'WG, pivots, -L parking, the solves'
                           //    right-hand sides, triangular chains, dz / dy)
 #endif
+#ifndef QPB_X_PINH0
+#define QPB_X_PINH0 1     // 1: H0's rows and A's columns loaded before the first DPP FMA (0: round 5's
+                          // schedule, one LDS round trip per FMA)
+#endif
 #ifndef QPB_X_DBG
 #define QPB_X_DBG 0       // (diagnostic: stop after the setup factor, its pivots D in x)
 #endif
@@ -213,6 +217,10 @@ static __device__ __forceinline__ void qpb_xpipe(LD &&ld, FX &&fx) {
     constexpr int ts_ = t_ >> 12, tf_ = (t_ >> 8) & 15, ti_ = t_ & 255; (void)ts_; (void)tf_; (void)ti_
 
 // one logical block `lb` of the plan's batch (QPs 4 lb .. 4 lb + 3)
+// the value is needed here (an empty asm that reads and writes it: its load is issued and
+// waited for before this point, not sunk next to a later use)
+static __device__ __forceinline__ void qpb_xpin(double &v) { asm volatile("" : "+v"(v)); }
+
 static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb, double *qpb_lds) {
     const int lane = threadIdx.x & 63, row = lane >> 4, c = lane & 15;
 #if QPB_X_TIMING
@@ -352,13 +360,38 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
                 H[s][j] = Pd[j * LDP + ixc[s]];
             });
         });
+        // every load of the H0 rows and A columns issued before the first DPP FMA (one
+        // LDS wait): left to the scheduler each load sat in front of its own FMA, some
+        // 45 round trips in series
+        double al0[NY > 0 ? NY : 1][XS];
+        qpb_for<0, NY>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            qpb_for<0, XS>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                if constexpr (qpb_axs(l, s)) al0[l][s] = Ad[ixc[s] * LDA + l];
+            });
+        });
+#if QPB_X_PINH0
+#pragma unroll
+        for (int s = 0; s < XS; s++)
+#pragma unroll
+            for (int j = 0; j < NX; j++)
+                if (j < qpb_xhw(s)) qpb_xpin(H[s][j]);
+        qpb_for<0, NY>([&](auto lc) {
+            constexpr int l = decltype(lc)::value;
+            qpb_for<0, XS>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                if constexpr (qpb_axs(l, s)) qpb_xpin(al0[l][s]);
+            });
+        });
+#endif
         qpb_for<0, NY>([&](auto lc) {
             constexpr int l = decltype(lc)::value;
             double al[XS], qa[XS];
             qpb_for<0, XS>([&](auto sc) {
                 constexpr int s = decltype(sc)::value;
                 if constexpr (qpb_axs(l, s)) {
-                    al[s] = Ad[ixc[s] * LDA + l];
+                    al[s] = al0[l][s];
                     qa[s] = -RDY * al[s];                  // 1e7 A(l, row)
                 }
             });

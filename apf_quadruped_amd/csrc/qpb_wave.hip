@@ -130,6 +130,9 @@ struct qpb_args {
 #ifndef QPB_W_LDSB_SYNC     // 1: a wave fence between publishing column k+1 and reading it (diagnostic)
 #define QPB_W_LDSB_SYNC 0
 #endif
+#ifndef QPB_W_RCH          // residual / solve products G x, A x, P x in chunks of this many columns,
+#define QPB_W_RCH 4        // each chunk's LDS loads issued together (0: per column -- the allocator
+#endif                     // then kept one load in flight: an LDS round trip per column)
 #ifndef QPB_W_TIMING
 #define QPB_W_TIMING 0    // 1: phase timestamps (s_memtime) of QP 0 of each tile into stats (debug)
 #endif
@@ -272,6 +275,8 @@ template <int J> static __device__ __forceinline__ double qpb_fmac_xb_dep(double
 template <int CTRL> static __device__ __forceinline__ double qpb_dpp(double v) {
     return __builtin_amdgcn_update_dpp(0.0, v, CTRL, 0xf, 0xf, true);
 }
+// the value is needed here: its load is issued and waited for before this point
+static __device__ __forceinline__ void qpb_wpin(double &v) { asm volatile("" : "+v"(v)); }
 
 // sums / maxima over the first R 16-lane rows (result wave-uniform); lanes
 // outside the data range must contribute 0 (sum) or a neutral value (max)
@@ -1024,6 +1029,36 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
             for (int u = 0; u < ZC; u++) gza[u][k] = 0.0;
         }
+#if QPB_W_RCH > 0
+#pragma unroll
+        for (int j0 = 0; j0 < NX; j0 += QPB_W_RCH) {
+            double xv[QPB_W_RCH], gv[ZC][QPB_W_RCH], av[QPB_W_RCH];
+#pragma unroll
+            for (int k = 0; k < QPB_W_RCH; k++)
+                if (j0 + k < NX) {
+                    xv[k] = Vb[VBO + j0 + k];
+#pragma unroll
+                    for (int u = 0; u < ZC; u++) gv[u][k] = GR(u, j0 + k);
+                    if constexpr (NY > 0) av[k] = AR(j0 + k);
+                }
+#pragma unroll
+            for (int k = 0; k < QPB_W_RCH; k++)
+                if (j0 + k < NX) {
+                    qpb_wpin(xv[k]);
+#pragma unroll
+                    for (int u = 0; u < ZC; u++) qpb_wpin(gv[u][k]);
+                    if constexpr (NY > 0) qpb_wpin(av[k]);
+                }
+#pragma unroll
+            for (int k = 0; k < QPB_W_RCH; k++)
+                if (j0 + k < NX) {
+                    const int j = j0 + k;
+#pragma unroll
+                    for (int u = 0; u < ZC; u++) gza[u][j % QPB_W_SPLIT] = __builtin_fma(gv[u][k], xv[k], gza[u][j % QPB_W_SPLIT]);
+                    if constexpr (NY > 0) gya[j % QPB_W_SPLIT] = __builtin_fma(av[k], xv[k], gya[j % QPB_W_SPLIT]);
+                }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < NX; j++) {
             const double xj = Vb[VBO + j];
@@ -1031,6 +1066,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             for (int u = 0; u < ZC; u++) gza[u][j % QPB_W_SPLIT] = __builtin_fma(GR(u, j), xj, gza[u][j % QPB_W_SPLIT]);
             if constexpr (NY > 0) gya[j % QPB_W_SPLIT] = __builtin_fma(AR(j), xj, gya[j % QPB_W_SPLIT]);
         }
+#endif
         double gy = gya[0];
 #pragma unroll
         for (int k = 1; k < QPB_W_SPLIT; k++) gy += gya[k];
@@ -1162,6 +1198,40 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
 #pragma unroll
         for (int t = 0; t < ZC; t++) rz[t] = hz[t] - s[t];
         if constexpr (!(QPB_W_ABL & 8)) {
+#if QPB_W_RCH > 0
+        // chunks of QPB_W_RCH columns: every load of a chunk issued before its first FMA
+        // (the same FMAs in the same order)
+#pragma unroll
+        for (int j0 = 0; j0 < NX; j0 += QPB_W_RCH) {
+            double xv[QPB_W_RCH], pv[QPB_W_RCH], gv[ZC][QPB_W_RCH], av[QPB_W_RCH];
+#pragma unroll
+            for (int k = 0; k < QPB_W_RCH; k++)
+                if (j0 + k < NX) {
+                    xv[k] = Vb[j0 + k];
+                    pv[k] = PR(j0 + k);
+#pragma unroll
+                    for (int t = 0; t < ZC; t++) gv[t][k] = GR(t, j0 + k);
+                    if constexpr (NY > 0) av[k] = AR(j0 + k);
+                }
+#pragma unroll
+            for (int k = 0; k < QPB_W_RCH; k++)
+                if (j0 + k < NX) {
+                    qpb_wpin(xv[k]);
+                    qpb_wpin(pv[k]);
+#pragma unroll
+                    for (int t = 0; t < ZC; t++) qpb_wpin(gv[t][k]);
+                    if constexpr (NY > 0) qpb_wpin(av[k]);
+                }
+#pragma unroll
+            for (int k = 0; k < QPB_W_RCH; k++)
+                if (j0 + k < NX) {
+                    tp = __builtin_fma(-pv[k], xv[k], tp);
+#pragma unroll
+                    for (int t = 0; t < ZC; t++) rz[t] = __builtin_fma(-gv[t][k], xv[k], rz[t]);
+                    if constexpr (NY > 0) ry = __builtin_fma(-av[k], xv[k], ry);
+                }
+        }
+#else
 #pragma unroll
         for (int j = 0; j < NX; j++) {
             const double xj = Vb[j];
@@ -1170,6 +1240,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             for (int t = 0; t < ZC; t++) rz[t] = __builtin_fma(-GR(t, j), xj, rz[t]);
             if constexpr (NY > 0) ry = __builtin_fma(-AR(j), xj, ry);
         }
+#endif
         {
             double ra[QPB_W_SPLIT];
 #pragma unroll
