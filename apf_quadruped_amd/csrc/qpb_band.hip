@@ -108,6 +108,33 @@ static __device__ __forceinline__ double qpb_bmax(double v) {
 #endif
 #define QPB_PRAGMA_(x) _Pragma(#x)
 #define QPB_PRAGMA(x) QPB_PRAGMA_(x)
+// the rows lane, lane + 64, .. (< N) of a per-row pass, unrolled, each index clamped to N - 1
+// (ok_ false on the clamped ones) so that every LDS access is unconditional: a rolled
+// `for (i = lane; i < N; i += 64)` waited for each row's loads in turn
+#ifndef QPB_B_ROWS
+#define QPB_B_ROWS 1      // 0: the rolled per-row loops (round 5)
+#endif
+#if QPB_B_ROWS
+#define QPB_BROWS(N, i, ...)                                                            \
+    do {                                                                                \
+        QPB_PRAGMA(unroll)                                                              \
+        for (int k_ = 0; k_ < ((N) + 63) / 64; k_++) {                                  \
+            const bool ok_ = lane + 64 * k_ < (N);                                      \
+            const int i = ok_ ? lane + 64 * k_ : (N) - 1;                               \
+            (void)ok_;                                                                  \
+            __VA_ARGS__                                                                 \
+        }                                                                               \
+    } while (0)
+#else
+#define QPB_BROWS(N, i, ...)                                                            \
+    do {                                                                                \
+        for (int i = lane; i < (N); i += 64) {                                          \
+            const bool ok_ = true;                                                      \
+            (void)ok_;                                                                  \
+            __VA_ARGS__                                                                 \
+        }                                                                               \
+    } while (0)
+#endif
 template <int J> static __device__ __forceinline__ void qpb_bfx(double &acc, double src, double m) {
     if constexpr (QPB_B_NV) qpb_fxs<J>(acc, src, m);
     else qpb_fx<J>(acc, src, m);
@@ -741,13 +768,15 @@ QPB_PRAGMA(unroll QPB_B_UNR)
     // step lengths (Auxilary.c:359-393): alpha = 1 / max(-d / v) over d < 0, 1 if none
     auto step_length = [&](bool corr, double &ap, double &ad) {
         double bp = 0.0, bd = 0.0;
-        for (int i = lane; i < BNZ; i += 64) {
+        // unrolled over the lane's rows with the index clamped (QPB_BROWS): the loads of all
+        // rows issue together; a clamped row repeats row BNZ - 1, harmless in a maximum
+        QPB_BROWS(BNZ, i, {
             const double s = Ls[V_S + i], z = Ls[V_Z + i], dz = Ls[V_DZ + i];
             const double rzi = qpb_rcp(z);
             const double dsl = corr ? Ls[V_RZ + i] : -s * __builtin_fma(dz, rzi, 1.0);
             bp = __builtin_fmax(bp, -dsl * __builtin_amdgcn_rcp(s));
             bd = __builtin_fmax(bd, -dz * rzi);
-        }
+        });
         bp = qpb_bmax(bp);
         bd = qpb_bmax(bd);
         ap = bp > 1e-10 ? __builtin_amdgcn_rcp(bp) : 1.0;
@@ -818,7 +847,7 @@ QPB_PRAGMA(unroll QPB_B_UNR)
         factor(qpb_ic<0>{});
         {
             bool tiny = false;      // any |D| <= 1e-14: |1/D| >= 1e14 (or not finite)
-            for (int i = lane; i < BNX; i += 64) tiny |= !(__builtin_fabs(Ls[O_RD + i]) < 1e14);
+            QPB_BROWS(BNX, i, { tiny |= !(__builtin_fabs(Ls[O_RD + i]) < 1e14); });
             if (qpb_any(tiny)) factor(qpb_ic<1>{});
         }
 #if QPB_WARM
@@ -860,11 +889,12 @@ QPB_PRAGMA(unroll QPB_B_UNR)
 #endif
             step_length(false, ap, ad);
             double rr = 0.0;
-            for (int i = lane; i < BNZ; i += 64) {
+            QPB_BROWS(BNZ, i, {
                 const double s = Ls[V_S + i], z = Ls[V_Z + i], dz = Ls[V_DZ + i];
                 const double dsl = -s * __builtin_fma(dz, qpb_rcp(z), 1.0);
-                rr += (s + ap * dsl) * (z + ad * dz);
-            }
+                const double t = (s + ap * dsl) * (z + ad * dz);
+                if (ok_) rr += t;                   // a sum: the clamped repeat is left out
+            });
             const double rho = qpb_bsum(rr) * rsz;      // formrho
             const double r1 = 1 > rho ? rho : 1;
             const double cube = r1 * r1 * r1;
@@ -891,12 +921,16 @@ QPB_PRAGMA(unroll QPB_B_UNR)
             n_it = it + 1;
         }
 #endif
-        for (int i = lane; i < BNX; i += 64) Ls[V_X + i] = __builtin_fma(Ls[V_DX + i], ap, Ls[V_X + i]);
-        for (int i = lane; i < BNY; i += 64) Ls[V_Y + i] = __builtin_fma(Ls[V_RY + i], ad, Ls[V_Y + i]);
-        for (int i = lane; i < BNZ; i += 64) {
-            Ls[V_S + i] = __builtin_fma(Ls[V_RZ + i], ap, Ls[V_S + i]);
-            Ls[V_Z + i] = __builtin_fma(Ls[V_DZ + i], ad, Ls[V_Z + i]);
-        }
+        // (a clamped row stores the value its own lane stores: the same inputs, loaded by the
+        // same instruction before either store)
+        QPB_BROWS(BNX, i, { Ls[V_X + i] = __builtin_fma(Ls[V_DX + i], ap, Ls[V_X + i]); });
+        if constexpr (BNY > 0) QPB_BROWS(BNY, i, { Ls[V_Y + i] = __builtin_fma(Ls[V_RY + i], ad, Ls[V_Y + i]); });
+        QPB_BROWS(BNZ, i, {
+            const double sn = __builtin_fma(Ls[V_RZ + i], ap, Ls[V_S + i]);
+            const double zn = __builtin_fma(Ls[V_DZ + i], ad, Ls[V_Z + i]);
+            Ls[V_S + i] = sn;
+            Ls[V_Z + i] = zn;
+        });
         qpb_wsync();
         QPB_BT(4);
         it++;
