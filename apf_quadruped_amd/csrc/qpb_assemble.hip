@@ -183,6 +183,7 @@ extern "C" int qpb_assemble_contact(const qpb_plan *plan, long B, const double *
     if (!feet || !wrench || !P || !A || !G || !c || !h || !b) return qpb::set_error(QPB_EINVAL, "NULL data pointer");
     // one block per 64-QP tile x 4 slot chunks (16 waves share a tile's ~190 slots)
     const unsigned tiles = (unsigned)((B + 63) / 64);
+    (void)hipGetLastError();   // a stale error of an earlier API call is not this launch's
     hipLaunchKernelGGL(qpb_assemble_contact_k, dim3(tiles, 4), dim3(256), 0, (hipStream_t)stream, B, feet, wrench, mp,
                        P, A, G, c, h, b);
     hipError_t e = hipGetLastError();
@@ -454,6 +455,7 @@ extern "C" int qpb_assemble_controller(const qpb_plan *plan_c, long B, const dou
     const qpb::Plan &pl = plan->pl;
     CtlArgs a{terms, terms_shared ? 0L : 1L, wdes, (const int *)tab, (int)(nent / 2),
               (int)pl.Pin.nnz(), (int)pl.A.nnz(), (int)pl.G.nnz(), mu, P, A, G, c, h, b, check, B};
+    (void)hipGetLastError();   // a stale error of an earlier API call is not these launches'
     if (check)
         hipLaunchKernelGGL(qpb_fill_int_k, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, check,
                            B, 1);
@@ -482,6 +484,7 @@ extern "C" int qpb_apf_wrench(long K, const qpb_apf_state *st, const double *tar
     if (K == 0) return QPB_OK;
     if (!targets || !wrench) return qpb::set_error(QPB_EINVAL, "NULL data pointer");
     ApfArgs a{*st, targets, wrench, com_des, K};
+    (void)hipGetLastError();   // a stale error of an earlier API call is not this launch's
     hipLaunchKernelGGL(qpb_apf_wrench_k, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return qpb::set_error(QPB_EHIP, (std::string("apf: ") + hipGetErrorString(e)).c_str());

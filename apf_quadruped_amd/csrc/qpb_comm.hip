@@ -162,6 +162,7 @@ void qpb_comm_destroy(void *comm) {
 
 int qpb_argmin_reduce(const double *gathered, long world, long n, double *out, void *stream) {
     if (!gathered || !out || world < 1 || n < 0) return qpb::set_error(QPB_EINVAL, "bad argmin reduce arguments");
+    (void)hipGetLastError();   // a stale error of an earlier API call is not this launch's
     hipLaunchKernelGGL(qpb_payload_reduce_k, dim3(1), dim3(64), 0, (hipStream_t)stream, gathered, world, n, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return qpb::set_error(QPB_EHIP, hipGetErrorString(e));
@@ -196,6 +197,7 @@ int qpb_argmin_allgather(const double *best, const double *x, long n, long B, lo
         buf = sc.first;
     }
     double *send = buf, *recv = buf + w;
+    (void)hipGetLastError();   // a stale error of an earlier API call is not this launch's
     hipLaunchKernelGGL(qpb_payload_k, dim3(1), dim3(64), 0, (hipStream_t)stream, best, x, n, B, base, send);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return qpb::set_error(QPB_EHIP, hipGetErrorString(e));

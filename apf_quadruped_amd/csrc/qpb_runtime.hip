@@ -414,12 +414,23 @@ int compile_kernel(const std::string &kname, const std::function<std::string()> 
     const std::string dir = cache_dir();
     const std::string path = dir + "/" + kname + "." + tag + ".hsaco";
     auto code = std::make_shared<std::vector<char>>();
-    if (!getenv("QPB_NO_DISK_CACHE") && read_file(path, *code)) {
+    // a cached object must define the kernel it is filed under (its symbol table holds the
+    // name): one that does not is discarded and rebuilt
+    auto defines = [&kname](const std::vector<char> &obj) {
+        return std::search(obj.begin(), obj.end(), kname.begin(), kname.end()) != obj.end();
+    };
+    if (!getenv("QPB_NO_DISK_CACHE") && read_file(path, *code) && defines(*code)) {
         g_code[kname] = code;
         *out = code;
         return QPB_OK;
     }
     std::string src = gen_src();
+    // the name is a hash of the source the plan was made with; a source generated under
+    // other knobs (QPB_WAVE_OPTS changed since the plan was made) defines another kernel
+    // and must not be filed under this name
+    if (src.find(kname) == std::string::npos)
+        return fail(QPB_ECOMPILE, "kernel " + kname + ": the source generated now defines another kernel "
+                                  "(QPB_WAVE_OPTS changed since the plan was made?)");
     std::string fix;
     int rc = cc.clang.empty() ? compile_with_hiprtc(kname, src, exact, *code)
                               : compile_with_clang(cc.clang, kname, src, exact, *code, &fix);
@@ -669,10 +680,17 @@ int load_function(const std::string &kname, const std::shared_ptr<std::vector<ch
     if (it != g_funcs.end()) { *fn = it->second.second; return QPB_OK; }
     hipModule_t mod;
     hipError_t e = hipModuleLoadData(&mod, code->data());
-    if (e != hipSuccess) return fail(QPB_EHIP, std::string("hipModuleLoadData: ") + hipGetErrorString(e));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();     // not left behind for a later launch's hipGetLastError to report
+        return fail(QPB_EHIP, std::string("hipModuleLoadData: ") + hipGetErrorString(e));
+    }
     hipFunction_t f;
     e = hipModuleGetFunction(&f, mod, kname.c_str());
-    if (e != hipSuccess) return fail(QPB_EHIP, std::string("hipModuleGetFunction: ") + hipGetErrorString(e));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipModuleUnload(mod);
+        return fail(QPB_EHIP, std::string("hipModuleGetFunction(") + kname + "): " + hipGetErrorString(e));
+    }
     g_funcs[key] = {mod, f};
     *fn = f;
     return QPB_OK;
@@ -686,6 +704,7 @@ int strided_copy(const CopySegs &t, void *stream) {
     long mx = 1;
     for (int i = 0; i < t.nseg; i++) mx = std::max(mx, t.seg[i].n);
     const unsigned gx = (unsigned)std::min<long>(64, (mx + 255) / 256);
+    (void)hipGetLastError();   // a stale error of an earlier API call is not this launch's
     hipLaunchKernelGGL(qpb_strided_copy, dim3(gx, (unsigned)t.nseg), dim3(256), 0, (hipStream_t)stream, t);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("strided copy: ") + hipGetErrorString(e));
@@ -1483,6 +1502,7 @@ int qpb_group_solve(qpb_group *g, const qpb_io *io, const qpb_settings *st, doub
 
 int qpb_winner(const double *best, const double *x, long n, long B, double *out, void *stream) {
     if (!best || !x || !out || n < 0 || B < 0) return fail(QPB_EINVAL, "bad winner arguments");
+    (void)hipGetLastError();   // a stale error of an earlier API call is not this launch's
     hipLaunchKernelGGL(qpb_winner_k, dim3(1), dim3(64), 0, (hipStream_t)stream, best, x, n, B, out);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(QPB_EHIP, std::string("winner: ") + hipGetErrorString(e));
@@ -1501,6 +1521,7 @@ int qpb_argmin(long B, const double *fval, const int *flag, double *out2, void *
     if (int rc = qpb::argmin_scratch(stream, nb, &part, &ctr)) return rc;
     double *pv = (double *)part;
     long *pi = (long *)((char *)part + nb * 8);
+    (void)hipGetLastError();   // a stale error of an earlier API call is not these launches'
     if (nb == 1) {   // one block covers the batch: a single launch writes the result
         hipLaunchKernelGGL(qpb_argmin_single, dim3(1), dim3(1024), 0, (hipStream_t)stream, B, fval, flag, out2);
     } else {

@@ -25,6 +25,7 @@ def test_row_kernel_zf128_variant_runs_clean(oracle, monkeypatch):
     monkeypatch.setenv("QPB_WAVE_OPTS", "QPB_R_ZF128=1")
     plan = Plan.from_dense(12, 20, 6, d["P"][0], d["A"][0], d["G"][0])
     kn = plan.kernel_name(B)
+    plan.compile(B=B)               # the variant is generated from the options in force: compile it now
     monkeypatch.delenv("QPB_WAVE_OPTS")
     assert kn.startswith("qpb_row_") and kn != base.kernel_name(B), (kn, base.kernel_name(B))
     vals = plan.pack(d["P"], d["A"], d["G"], d["c"], d["h"], d["b"])
