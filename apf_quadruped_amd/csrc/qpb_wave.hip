@@ -130,6 +130,9 @@ struct qpb_args {
 #ifndef QPB_W_LDSB_SYNC     // 1: a wave fence between publishing column k+1 and reading it (diagnostic)
 #define QPB_W_LDSB_SYNC 0
 #endif
+#ifndef QPB_W_KDIAG        // 1: a dense z row's kd on its diagonal before the factor (0: added to the
+#define QPB_W_KDIAG 1      // pivot at its step, round 5)
+#endif
 #ifndef QPB_W_RCH          // residual / solve products G x, A x, P x in chunks of this many columns,
 #define QPB_W_RCH 4        // each chunk's LDS loads issued together (0: per column -- the allocator
 #endif                     // then kept one load in flight: an LDS round trip per column)
@@ -721,10 +724,29 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         }
         if (fstamp) QPB_TS(fstamp + 1);
         double kdz[ND];
+#if QPB_W_KDIAG
+        // a dense z row's diagonal is kd alone (H0 and G'WG put nothing there): it enters
+        // the row before the factor, as in the reference's KKT matrix (ldl.c starts each
+        // pivot from the diagonal) -- its loads batched here, not one LDS round trip on
+        // the pivot chain per z pivot
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             if constexpr (qpb_dkind[k] == 2) kdz[k] = Vb[VBW + NZ + qpb_didx[k]];
         });
+        qpb_for<0, ND>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (qpb_dkind[k] == 2) qpb_wpin(kdz[k]);
+        });
+        qpb_for<0, ND>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (qpb_dkind[k] == 2) H[k] = ln == k ? H[k] + kdz[k] : H[k];
+        });
+#else
+        qpb_for<0, ND>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (qpb_dkind[k] == 2) kdz[k] = Vb[VBW + NZ + qpb_didx[k]];
+        });
+#endif
         // The pivot recurrence is the critical path: D_{k+1} is formed from
         // H'(k+1,k) and H'(k+1,k+1) (values before step k) with exactly the
         // operations lane k+1's own update performs, so the trailing updates
@@ -754,7 +776,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             qpb_wsync();                         // every read before Tx is reused
         }
         double dpiv = qpb_dpp<0x150>(Hlo[0]);    // row 0's H(0,0): lane 0 of every DPP row
-        if constexpr (qpb_dkind[0] == 2) dpiv += kdz[0];
+        if constexpr (!QPB_W_KDIAG && qpb_dkind[0] == 2) dpiv += kdz[0];
         const int lr = ln & 15;
         qpb_for<0, ND>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
@@ -764,7 +786,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 const double h = qpb_dpp<0x150 + (r1 & 15)>(r1 < 16 ? Hlo[k] : Hhi[k]);
                 const double hkk = qpb_dpp<0x150 + (r1 & 15)>(r1 < 16 ? Hlo[k + 1] : Hhi[k + 1]);
                 dpiv = __builtin_fma(h, h * -rd, hkk);
-                if constexpr (qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
+                if constexpr (!QPB_W_KDIAG && qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
             }
             rDd = ln == k ? rd : rDd;
             const double nlo = Hlo[k] * -rd, nhi = Hhi[k] * -rd;
@@ -793,7 +815,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
         Bc[ln] = H[0];
 #endif
         double dpiv = qpb_xb<0>(H[0]);
-        if constexpr (qpb_dkind[0] == 2) dpiv += kdz[0];
+        if constexpr (!QPB_W_KDIAG && qpb_dkind[0] == 2) dpiv += kdz[0];
 #if QPB_W_BLK
         // Blocked right-looking LDL': pivots in permutation order as below, but each
         // step updates only its 16-column panel; after a panel [k0, k1) the rows and
@@ -817,7 +839,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             if constexpr (k + 1 < k1) {
                 const double h = qpb_xb<k + 1>(H[k]), hkk = qpb_xb<k + 1>(H[k + 1]);
                 dpiv = __builtin_fma(h, h * -rd, hkk);
-                if constexpr (qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
+                if constexpr (!QPB_W_KDIAG && qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
             }
             rDd = ln == k ? rd : rDd;
             if constexpr (k1 < ND) {
@@ -868,7 +890,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
                 });
                 // the next panel's first pivot, after its row got the trailing update
                 dpiv = qpb_xb<k1>(H[k1]);
-                if constexpr (qpb_dkind[k1] == 2) dpiv += kdz[k1];
+                if constexpr (!QPB_W_KDIAG && qpb_dkind[k1] == 2) dpiv += kdz[k1];
                 Tx[nb + ln] = H[k1];                                  // column k1 for step k1
             }
 #else
@@ -876,7 +898,7 @@ extern "C" __global__ void __launch_bounds__(QPB_WG, 1) QPB_KERNEL_NAME(qpb_args
             if constexpr (k + 1 < ND) {
                 const double h = qpb_xb<k + 1>(H[k]), hkk = qpb_xb<k + 1>(H[k + 1]);
                 dpiv = __builtin_fma(h, h * -rd, hkk);
-                if constexpr (qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
+                if constexpr (!QPB_W_KDIAG && qpb_dkind[k + 1] == 2) dpiv += kdz[k + 1];
             }
             rDd = ln == k ? rd : rDd;
             // -L(d,k): kept negated so every update (and the solves) is a plain
