@@ -46,6 +46,9 @@ static_assert(NX >= 1 && NX <= 32 && NY <= 32 && NZ >= 1 && NZ <= 128, "rowx ker
                           // 2: cycles per part instead (G'WG, pivots, -L parking, the solves'
                           //    right-hand sides, triangular chains, dz / dy)
 #endif
+#ifndef QPB_X_GWGP
+#define QPB_X_GWGP 1      // 1: G'WG issues each row's FMAs one row behind its products (0: right behind)
+#endif
 #ifndef QPB_X_PINH0
 #define QPB_X_PINH0 1     // 1: H0's rows and A's columns loaded before the first DPP FMA (0: round 5's
                           // schedule, one LDS round trip per FMA)
@@ -184,6 +187,26 @@ static constexpr int qpb_gw_at(int k) {
             if (qpb_gxs(r, s) && k-- == 0) return (s << 12) | r;
     }
     return -1;
+}
+// the G'WG term list's row groups: group of term k (rows with terms, in order), row of group g
+static constexpr int qpb_gw_grp(int k) {
+    int g = 0, last = -1;
+    for (int i = 0; i <= k; i++) {
+        const int r = qpb_gw_at(i) & 4095;
+        if (i > 0 && r != last) g++;
+        last = r;
+    }
+    return g;
+}
+static constexpr int qpb_gw_row(int g) {
+    int gi = 0, last = -1;
+    for (int i = 0; i < qpb_gw_n(); i++) {
+        const int r = qpb_gw_at(i) & 4095;
+        if (i > 0 && r != last) gi++;
+        if (gi == g) return r;
+        last = r;
+    }
+    return 0;
 }
 // for k in [0, N): coef_k = ld(k) (an LDS load), fx(k, coef_k); loads CH terms ahead
 template <int N, class LD, class FX>
@@ -432,6 +455,23 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
         // G(r, row) w_r -- the same LDS values serve as source and coefficient; the loads
         // pipelined ahead of the rows' FMAs
         double gc[XS], wl = 0.0;
+#if QPB_X_GWGP
+        double gcb[2][XS], crb[2][XS];
+#endif
+        (void)gc;
+        // row R's FMAs: += G(R, row) w_R G(R, j), lane j's G(R, j) (gcv) by DPP broadcast
+        auto gw_row = [&](auto rc, const double (&gcv)[XS], const double (&crv)[XS]) {
+            constexpr int R = decltype(rc)::value;
+            qpb_for<0, XS>([&](auto sc) {
+                constexpr int s2 = decltype(sc)::value;
+                if constexpr (qpb_gxs(R, s2)) {
+                    qpb_for<0, qpb_xhw(s2)>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        if constexpr (qpb_Gnz[R][j]) qpb_fxs<(j & 15)>(H[s2][j], gcv[j >> 4], crv[s2]);
+                    });
+                }
+            });
+        };
         if constexpr (QPB_X_WLDS) {
 #pragma unroll
             for (int u = 0; u < ZS; u++)
@@ -446,6 +486,24 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
             },
             [&](auto kc, double cf) {
                 constexpr int k = decltype(kc)::value, t = qpb_gw_at(k), ts = t >> 12, r = t & 4095;
+#if QPB_X_GWGP
+                // one row behind: row g's products G(r, row) w_r are formed, then row g-1's
+                // FMAs issue -- no FMA right behind the multiply that feeds it (a DPP
+                // operand written by the previous VALU waits); buffers by row parity, so
+                // each H entry still takes its rows in order (the same bits)
+                constexpr int g = qpb_gw_grp(k);
+                if constexpr (ts == 7) wl = cf;
+                else gcb[g & 1][ts] = cf;
+                if constexpr (k + 1 == qpb_gw_n() || (qpb_gw_at(k + 1) & 4095) != r) {   // the row's last term
+                    const double wr = QPB_X_WLDS ? wl : qpb_nb<(r & 15)>(w[r >> 4]);
+                    qpb_for<0, XS>([&](auto sc) {
+                        constexpr int s2 = decltype(sc)::value;
+                        if constexpr (qpb_gxs(r, s2)) crb[g & 1][s2] = gcb[g & 1][s2] * wr;
+                    });
+                    if constexpr (g > 0) gw_row(qpb_ic<qpb_gw_row(g - 1)>{}, gcb[(g - 1) & 1], crb[(g - 1) & 1]);
+                    if constexpr (k + 1 == qpb_gw_n()) gw_row(qpb_ic<r>{}, gcb[g & 1], crb[g & 1]);
+                }
+#else
                 if constexpr (ts == 7) wl = cf;
                 else gc[ts] = cf;
                 if constexpr (k + 1 == qpb_gw_n() || (qpb_gw_at(k + 1) & 4095) != r) {   // the row's last term
@@ -455,16 +513,9 @@ static __device__ __forceinline__ void qpb_rowx_body(const qpb_args &a, long lb,
                         constexpr int s2 = decltype(sc)::value;
                         if constexpr (qpb_gxs(r, s2)) cr[s2] = gc[s2] * wr;
                     });
-                    qpb_for<0, XS>([&](auto sc) {
-                        constexpr int s2 = decltype(sc)::value;
-                        if constexpr (qpb_gxs(r, s2)) {
-                            qpb_for<0, qpb_xhw(s2)>([&](auto jc) {
-                                constexpr int j = decltype(jc)::value;
-                                if constexpr (qpb_Gnz[r][j]) qpb_fxs<(j & 15)>(H[s2][j], gc[j >> 4], cr[s2]);
-                            });
-                        }
-                    });
+                    gw_row(qpb_ic<r>{}, gc, cr);
                 }
+#endif
             });
     };
     // right-looking LDL' in natural order; the pivot recurrence is the critical path:
