@@ -111,6 +111,9 @@ static __device__ __forceinline__ double qpb_bmax(double v) {
 // the rows lane, lane + 64, .. (< N) of a per-row pass, unrolled, each index clamped to N - 1
 // (ok_ false on the clamped ones) so that every LDS access is unconditional: a rolled
 // `for (i = lane; i < N; i += 64)` waited for each row's loads in turn
+#ifndef QPB_B_VFORM
+#define QPB_B_VFORM 1     // 1: the rank-MY Schur update as (AR' M) AR; 0: AR' (M AR) (round 5)
+#endif
 #ifndef QPB_B_ROWS
 #define QPB_B_ROWS 1      // 0: the rolled per-row loops (round 5)
 #endif
@@ -490,16 +493,40 @@ QPB_PRAGMA(unroll QPB_B_UNR)
 #pragma unroll
                     for (int l = 0; l < MY; l++) Ls[YB(k) + l * NB + c] = Yr[l];
                 }
-                double M[MY1], T[NB];
+                double M[MY1];
 #pragma unroll
                 for (int l = 0; l < MY; l++) M[l] = 0.0;
-#pragma unroll
-                for (int j = 0; j < NB; j++) T[j] = 0.0;
                 qpb_for<0, NB>([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
                     if constexpr ((qpb_bALu >> j) & 1)
                         qpb_for<0, MY>([&](auto lc) { qpb_fx<j>(M[decltype(lc)::value], Yr[decltype(lc)::value], alr[j]); });
                 });
+#if QPB_B_VFORM
+                // V = AR_k' M (x lanes: row c, MY wide), then H(c, j) -= 1e14 sum_l V(c, l) AR_k(l, j):
+                // MY * MY + MY * NB DPP FMAs instead of T = M AR_k's MY * NB + the same MY * NB
+                double V[MY1];
+#pragma unroll
+                for (int l = 0; l < MY; l++) V[l] = 0.0;
+                qpb_for<0, MY>([&](auto vc) {
+                    constexpr int v = decltype(vc)::value;
+                    qpb_for<0, MY>([&](auto lc) {
+                        constexpr int l = decltype(lc)::value;
+                        qpb_fx<l>(V[v], M[v], arc[l]);          // += AR(l, c) M(l, v)
+                    });
+                });
+#pragma unroll
+                for (int l = 0; l < MY; l++) V[l] *= -1e14;
+                qpb_for<0, MY>([&](auto lc) {
+                    constexpr int l = decltype(lc)::value;
+                    qpb_for<0, NB>([&](auto jc) {
+                        constexpr int j = decltype(jc)::value;
+                        if constexpr ((qpb_bARu >> j) & 1) qpb_fx<l>(Hs[j], arr[j], V[l]);
+                    });
+                });
+#else
+                double T[NB];
+#pragma unroll
+                for (int j = 0; j < NB; j++) T[j] = 0.0;
                 qpb_for<0, MY>([&](auto lc) {
                     constexpr int l = decltype(lc)::value;
                     qpb_for<0, NB>([&](auto jc) {
@@ -516,6 +543,7 @@ QPB_PRAGMA(unroll QPB_B_UNR)
                         if constexpr ((qpb_bARu >> j) & 1) qpb_fx<l>(Hs[j], T[j], m);
                     });
                 });
+#endif
             }
 #endif
             // LDL' of the stage block in natural order (the row kernel's pivot chain)
