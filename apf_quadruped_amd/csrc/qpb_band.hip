@@ -111,6 +111,9 @@ static __device__ __forceinline__ double qpb_bmax(double v) {
 // the rows lane, lane + 64, .. (< N) of a per-row pass, unrolled, each index clamped to N - 1
 // (ok_ false on the clamped ones) so that every LDS access is unconditional: a rolled
 // `for (i = lane; i < N; i += 64)` waited for each row's loads in turn
+#ifndef QPB_B_PREF
+#define QPB_B_PREF 0      // 1: each stage's static A slices loaded during the previous stage's pivots (measured: noise)
+#endif
 #ifndef QPB_B_VFORM
 #define QPB_B_VFORM 1     // 1: the rank-MY Schur update as (AR' M) AR; 0: AR' (M AR) (round 5)
 #endif
@@ -407,6 +410,13 @@ QPB_PRAGMA(unroll QPB_B_UNR)
     auto factor = [&](auto regc) {
         constexpr bool REG = decltype(regc)::value != 0;
         double H[NB];
+#if QPB_B_PREF && MY > 0
+        double pYr[MY1], parc[MY1], palr[NB];   // stage k's static slices, loaded during stage k - 1
+#pragma unroll
+        for (int l = 0; l < MY1; l++) pYr[l] = parc[l] = 0.0;
+#pragma unroll
+        for (int j = 0; j < NB; j++) palr[j] = 0.0;
+#endif
 #pragma unroll 1
         for (int k = 0; k < NS; k++) {
             QPB_BT0();
@@ -470,15 +480,22 @@ QPB_PRAGMA(unroll QPB_B_UNR)
                 //   Y_k = S_{k-1}^-1 AL_k' = L^-T D^-1 L^-1 AL_k'   (x lanes: row c of Y_k)
                 //   M = AL_k Y_k, T = M AR_k                          (y lanes: rows l)
                 //   H(c, j) -= 1e14 sum_l AR_k(l, c) T(l, j)          (x lanes)
-                double nlr[NB], nlc[NB], Yr[MY1], arc[MY1], alr[NB], arr[NB];
+                double nlr[NB], nlc[NB], Yr[MY1], arc[MY1], alr[NB];
                 row_L(k - 1, nlr);
                 col_L(k - 1, nlc);
                 const double rdp = Ls[O_RD + (k - 1) * NB + xc];
+#if QPB_B_PREF
+#pragma unroll
+                for (int l = 0; l < MY; l++) { Yr[l] = pYr[l]; arc[l] = parc[l]; }
+#pragma unroll
+                for (int j = 0; j < NB; j++) alr[j] = palr[j];
+#else
                 col_A(ALB(k), Yr);
                 col_A(ARB(k), arc);
-                const double *ALr = Ls + ALB(k) + yc * NB, *ARr = Ls + ARB(k) + yc * NB;
+                const double *ALr = Ls + ALB(k) + yc * NB;
 #pragma unroll
-                for (int j = 0; j < NB; j++) { alr[j] = ALr[j]; arr[j] = ARr[j]; }
+                for (int j = 0; j < NB; j++) alr[j] = ALr[j];
+#endif
                 qpb_for<0, NB>([&](auto fc) {
                     constexpr int f = decltype(fc)::value;
                     qpb_for<0, MY>([&](auto lc) { qpb_fxd<f>(Yr[decltype(lc)::value], nlr[f]); });
@@ -520,13 +537,14 @@ QPB_PRAGMA(unroll QPB_B_UNR)
                     constexpr int l = decltype(lc)::value;
                     qpb_for<0, NB>([&](auto jc) {
                         constexpr int j = decltype(jc)::value;
-                        if constexpr ((qpb_bARu >> j) & 1) qpb_fx<l>(Hs[j], arr[j], V[l]);
+                        if constexpr ((qpb_bARu >> j) & 1) qpb_fx<j>(Hs[j], arc[l], V[l]);   // AR(l, j): lane j
                     });
                 });
 #else
-                double T[NB];
+                double T[NB], arr[NB];
+                const double *ARr = Ls + ARB(k) + yc * NB;
 #pragma unroll
-                for (int j = 0; j < NB; j++) T[j] = 0.0;
+                for (int j = 0; j < NB; j++) { T[j] = 0.0; arr[j] = ARr[j]; }
                 qpb_for<0, MY>([&](auto lc) {
                     constexpr int l = decltype(lc)::value;
                     qpb_for<0, NB>([&](auto jc) {
@@ -544,6 +562,18 @@ QPB_PRAGMA(unroll QPB_B_UNR)
                     });
                 });
 #endif
+            }
+#endif
+#if QPB_B_PREF && MY > 0
+            // the next stage's static slices (AL_{k+1}, AR_{k+1} columns, AL_{k+1} row), loaded
+            // here so that they arrive under the pivot chain, which reads no LDS
+            {
+                const int kn = k + 1 < NS ? k + 1 : NS - 1;
+                col_A(ALB(kn), pYr);
+                col_A(ARB(kn), parc);
+                const double *ALr = Ls + ALB(kn) + yc * NB;
+#pragma unroll
+                for (int j = 0; j < NB; j++) palr[j] = ALr[j];
             }
 #endif
             // LDL' of the stage block in natural order (the row kernel's pivot chain)
